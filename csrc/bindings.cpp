@@ -1,0 +1,100 @@
+// pybind11 surface of the native HIP extension ``pytorch_ddp_mnist_amd._C``.
+// Device buffers are owned by torch (HBM via its caching allocator) and passed as raw
+// addresses; streams are passed as the integer handles of torch.cuda.Stream.cuda_stream.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "kernels/launch.h"
+#include "runtime/hip_check.h"
+#include "runtime/rccl_comm.h"
+#include "runtime/trainer.h"
+
+namespace py = pybind11;
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "MI355X (gfx950) native kernels, step runtime and RCCL communicator";
+
+  m.def("model_nparam", [](int model) { return model_nparam(static_cast<ModelKind>(model)); });
+  m.def("model_conv_params", [](int model) { return model_conv_params(static_cast<ModelKind>(model)); });
+  m.def("model_pack_size", [](int model) { return model_pack_size(static_cast<ModelKind>(model)); });
+  m.def("conv_bwd_blocks", &lenet_conv_bwd_blocks);
+  m.def("device_count", [] {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+  m.def("device_arch", [](int dev) {
+    hipDeviceProp_t p;
+    HIP_CHECK(hipGetDeviceProperties(&p, dev));
+    return std::string(p.gcnArchName);
+  });
+  m.def("rccl_version", &RcclComm::version);
+
+  py::class_<TrainerPtrs>(m, "TrainerPtrs")
+      .def(py::init<>())
+#define RW(f) .def_readwrite(#f, &TrainerPtrs::f)
+      RW(images) RW(labels) RW(idx) RW(step) RW(params) RW(grad) RW(mom) RW(pack) RW(slab_fc) RW(slab_conv)
+      RW(metrics) RW(xT) RW(h1T) RW(h2T) RW(dy1T) RW(dy2T) RW(dy3T) RW(p1) RW(m1) RW(p2) RW(m2) RW(dp2);
+#undef RW
+
+  py::class_<Bucket>(m, "Bucket")
+      .def(py::init([](int p0, int p1, int phase) { return Bucket{p0, p1, phase}; }))
+      .def_readwrite("p0", &Bucket::p0)
+      .def_readwrite("p1", &Bucket::p1)
+      .def_readwrite("phase", &Bucket::phase)
+      .def("__repr__", [](const Bucket& b) {
+        return "Bucket(" + std::to_string(b.p0) + ", " + std::to_string(b.p1) + ", phase=" + std::to_string(b.phase) + ")";
+      });
+
+  py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
+      .def_static("make_unique_id", [] { return py::bytes(RcclComm::make_unique_id()); })
+      .def(py::init([](py::bytes uid, int rank, int world, int device) {
+             return std::make_shared<RcclComm>(std::string(uid), rank, world, device);
+           }),
+           py::call_guard<py::gil_scoped_release>())
+      .def("all_reduce_sum_f32",
+           [](RcclComm& c, uintptr_t buf, size_t n, uintptr_t s) {
+             c.all_reduce_sum_f32(reinterpret_cast<float*>(buf), n, reinterpret_cast<hipStream_t>(s));
+           })
+      .def("broadcast_f32",
+           [](RcclComm& c, uintptr_t buf, size_t n, int root, uintptr_t s) {
+             c.broadcast_f32(reinterpret_cast<float*>(buf), n, root, reinterpret_cast<hipStream_t>(s));
+           })
+      .def("all_reduce_max_f64",
+           [](RcclComm& c, uintptr_t buf, size_t n, uintptr_t s) {
+             c.all_reduce_max_f64(reinterpret_cast<double*>(buf), n, reinterpret_cast<hipStream_t>(s));
+           })
+      .def("async_error", &RcclComm::async_error)
+      .def("wait_stream",
+           [](RcclComm& c, uintptr_t s, double timeout) { c.wait_stream(reinterpret_cast<hipStream_t>(s), timeout); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("abort", &RcclComm::abort)
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("world", &RcclComm::world);
+
+  py::class_<Trainer>(m, "Trainer")
+      .def(py::init<int, int, int, int, int, const TrainerPtrs&>(), py::arg("model"), py::arg("dtype"),
+           py::arg("batch"), py::arg("ld_b"), py::arg("fc_splits"), py::arg("ptrs"))
+      .def("set_comm", &Trainer::set_comm)
+      .def("set_world", &Trainer::set_world)
+      .def("set_optimizer", &Trainer::set_optimizer)
+      .def("set_dropout", &Trainer::set_dropout)
+      .def("set_buckets", &Trainer::set_buckets)
+      .def("buckets", &Trainer::buckets)
+      .def("set_overlap", &Trainer::set_overlap)
+      .def("pack", &Trainer::pack)
+      .def("train_step", &Trainer::train_step)
+      .def("forward_backward", &Trainer::forward_backward)
+      .def("reduce_grads", &Trainer::reduce_grads)
+      .def("optimizer_step", &Trainer::optimizer_step)
+      .def("eval_batch", &Trainer::eval_batch)
+      .def("capture", &Trainer::capture)
+      .def("replay", &Trainer::replay)
+      .def("invalidate", &Trainer::invalidate)
+      .def_property_readonly("captured", &Trainer::captured)
+      .def_property_readonly("nparam", &Trainer::nparam)
+      .def_property_readonly("pack_size", &Trainer::pack_size)
+      .def_property_readonly("conv_slabs", &Trainer::conv_slabs)
+      .def_property_readonly("conv_params", &Trainer::conv_params)
+      .def_property_readonly("fc_splits", &Trainer::fc_splits);
+}

@@ -1,0 +1,91 @@
+// Shared CDNA4 (gfx950) primitives for the MNIST training kernels.
+//
+// Every GEMM-shaped product in this framework is issued on the matrix cores with
+// the 16x16 MFMA family, one 64-lane wave per 16x16 output tile:
+//   fp32 path : v_mfma_f32_16x16x4_f32   (exact f32 products, K = 4 per instruction)
+//   bf16 path : v_mfma_f32_16x16x32_bf16 (K = 32 per instruction), f32 accumulate
+// To write the kernels once for both, a "K-chunk" abstraction is used: in a chunk
+// every lane supplies KV *contiguous* k-elements of its A row / B column
+//   lane l : row/col = l & 15, k in [ (l>>4)*KV , (l>>4)*KV + KV )
+// bf16: KV = 8 -> one 16x16x32 MFMA.  fp32: KV = 4 -> four 16x16x4 MFMAs where
+// instruction i consumes element i of every lane (k-slot g of lane group g is
+// k = 4g+i); A and B use the same permutation, so the chunk sum is exact.
+// Contiguous-k fragments mean every operand fetch is one vector load
+// (16 B for bf16, 16 B for fp32) from LDS or global memory.
+// C/D layout (dtype independent on gfx950): col = lane & 15, row = (lane>>4)*4 + i.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __bf16 bf16;
+
+#define DEV __device__ __forceinline__
+
+constexpr int WAVE = 64;
+
+template <typename T> struct Mma;
+
+template <> struct Mma<float> {
+  static constexpr int KV = 4;    // contiguous k per lane per chunk
+  static constexpr int KC = 16;   // k per chunk
+  struct Frag { f32x4 v; };
+  static DEV void mma(f32x4& acc, const Frag& a, const Frag& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[0], b.v[0], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[1], b.v[1], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[2], b.v[2], acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[3], b.v[3], acc, 0, 0, 0);
+  }
+  static DEV Frag load(const float* p) { Frag f; f.v = *reinterpret_cast<const f32x4*>(p); return f; }
+  static DEV Frag zero() { Frag f; f.v = f32x4{0.f, 0.f, 0.f, 0.f}; return f; }
+  static DEV void set(Frag& f, int j, float x) { f.v[j] = x; }
+  static DEV float get(const Frag& f, int j) { return f.v[j]; }
+};
+
+template <> struct Mma<bf16> {
+  static constexpr int KV = 8;
+  static constexpr int KC = 32;
+  struct Frag { bf16x8 v; };
+  static DEV void mma(f32x4& acc, const Frag& a, const Frag& b) {
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc, 0, 0, 0);
+  }
+  static DEV Frag load(const bf16* p) { Frag f; f.v = *reinterpret_cast<const bf16x8*>(p); return f; }
+  static DEV Frag zero() {
+    Frag f;
+    for (int j = 0; j < 8; ++j) f.v[j] = (bf16)0.f;
+    return f;
+  }
+  static DEV void set(Frag& f, int j, float x) { f.v[j] = (bf16)x; }
+  static DEV float get(const Frag& f, int j) { return (float)f.v[j]; }
+};
+
+template <typename T> DEV T to_t(float x) { return (T)x; }
+template <typename T> DEV float to_f(T x) { return (float)x; }
+
+DEV int lane_id() { return threadIdx.x & 63; }
+DEV int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
+
+DEV f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+// Counter-based hash RNG (dropout): a stateless 32-bit mix of (seed, stream, a, b).
+DEV uint32_t hash4(uint32_t seed, uint32_t s, uint32_t a, uint32_t b) {
+  uint32_t h = seed ^ 0x9E3779B9u;
+  h ^= s * 0x85EBCA6Bu; h = (h << 13) | (h >> 19); h = h * 5u + 0xE6546B64u;
+  h ^= a * 0xC2B2AE35u; h = (h << 13) | (h >> 19); h = h * 5u + 0xE6546B64u;
+  h ^= b * 0x27D4EB2Fu; h = (h << 13) | (h >> 19); h = h * 5u + 0xE6546B64u;
+  h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+  return h;
+}
+
+// MNIST normalisation of ToTensor()+Normalize((0.1307,),(0.3081,)) (ddp_tutorial_cpu.py:13-16).
+DEV float mnist_norm(uint32_t u8) { return (float(u8) * (1.0f / 255.0f) - 0.1307f) * (1.0f / 0.3081f); }
+
+DEV int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+// wave-level reductions (64 lanes)
+DEV float wave_sum(float v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}

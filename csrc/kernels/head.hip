@@ -1,0 +1,527 @@
+// Fused fully-connected head: forward, softmax cross-entropy, and backward (dgrad) in ONE
+// kernel per R-row tile of the batch, plus the grouped weight-gradient GEMM.
+//
+// Replaces, for the reference MLP (ddp_tutorial_cpu.py:43-53, step loop :70-78), the ATen
+// sequence addmm -> relu -> native_dropout -> addmm -> relu -> mm -> _log_softmax ->
+// nll_loss -> nll_loss_backward -> _log_softmax_backward -> mm x2 -> threshold_backward ->
+// addmm-backward ... (survey §2.6 K1..K13) and, for LeNet-5, its three Linear layers.
+// All activations of a tile stay in LDS; the only HBM traffic is the input tile, the packed
+// weights (L2 resident) and the transposed activations/gradients that the wgrad GEMM needs.
+//
+// Per tile (4 waves, R = 16*MT rows):
+//   stage X -> LDS (MLP: gather dataset[idx[r]] + normalise, fused; LeNet: pool2 rows)
+//   H1 = relu(X W1^T + b1) [dropout]      H2 = relu(H1 W2^T + b2)      Z = H2 W3^T [+ b3]
+//   loss/acc + dZ = softmax(Z) - onehot(y)         (1/B applied by the gradient reduce)
+//   dH2 = (dZ W3) * [H2>0]    dH1 = (dH2 W2) * [H1>0] (/keep)    [LeNet] dX = dH1 W1
+// Every product is a 16x16 MFMA tile loop (common.h); epilogues fuse bias, ReLU, dropout
+// masks, padding and the transposed global stores.
+#include <algorithm>
+
+#include "common.h"
+#include "launch.h"
+#include "models.h"
+
+namespace {
+
+template <typename T, class H, int MT>
+struct HeadSmem {
+  static constexpr int R = MT * 16;
+  static constexpr int PX = H::K0P + 8;
+  static constexpr int P1 = H::N1P + 8;
+  static constexpr int P2 = H::N2P + 8;
+  static constexpr int PD = H::NCK + 8;
+  static constexpr int OFF_X = 0;
+  static constexpr int OFF_H1 = rup(OFF_X + R * PX * (int)sizeof(T), 16);
+  static constexpr int OFF_H2 = rup(OFF_H1 + R * P1 * (int)sizeof(T), 16);
+  static constexpr int OFF_D = rup(OFF_H2 + R * P2 * (int)sizeof(T), 16);
+  static constexpr int OFF_L = rup(OFF_D + R * PD * (int)sizeof(T), 16);
+  static constexpr int OFF_I = OFF_L + R * 16 * 4;
+  static constexpr int TOTAL = rup(OFF_I + R * 4, 16);
+  static constexpr bool FITS = TOTAL <= 160 * 1024;
+};
+
+// store 4 consecutive-row values of one column into a transposed [col][ldB] buffer
+template <typename T>
+DEV void store_col4(T* base, float a, float b, float c, float d) {
+  if constexpr (sizeof(T) == 2) {
+    bf16x4 v; v[0] = (bf16)a; v[1] = (bf16)b; v[2] = (bf16)c; v[3] = (bf16)d;
+    *reinterpret_cast<bf16x4*>(base) = v;
+  } else {
+    *reinterpret_cast<f32x4*>(base) = f32x4{a, b, c, d};
+  }
+}
+
+template <typename T, class H, int MT, bool TRAIN>
+__global__ __launch_bounds__(256) void head_kernel(BatchRef br, HeadBuffers hb) {
+  using S = HeadSmem<T, H, MT>;
+  using M = Mma<T>;
+  using Frag = typename M::Frag;
+  constexpr int R = S::R, KV = M::KV, KC = M::KC;
+  static_assert(S::FITS, "head tile does not fit in LDS");
+  __shared__ __attribute__((aligned(16))) char smem[S::TOTAL];
+  T* sX = reinterpret_cast<T*>(smem + S::OFF_X);
+  T* sH1 = reinterpret_cast<T*>(smem + S::OFF_H1);
+  T* sH2 = reinterpret_cast<T*>(smem + S::OFF_H2);
+  T* sD = reinterpret_cast<T*>(smem + S::OFF_D);
+  float* sLog = reinterpret_cast<float*>(smem + S::OFF_L);
+  int* sIdx = reinterpret_cast<int*>(smem + S::OFF_I);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
+  const int row = lane & 15, grp = lane >> 4;
+  const int r0 = blockIdx.x * R;
+  const int B = br.B;
+  const int step = br.step_ptr[0];
+  const int gstep = br.step_ptr[1];
+  const int32_t* idx = br.idx_epoch + (size_t)step * br.batch_stride;
+  const T* pack = reinterpret_cast<const T*>(hb.pack);
+  const float* prm = hb.params;
+  const int ldB = hb.ldB;
+
+  if (tid < R) sIdx[tid] = (r0 + tid < B) ? idx[r0 + tid] : -1;
+  __syncthreads();
+
+  // ---------------------------------------------------------------- stage the input tile
+  if constexpr (H::GATHER) {
+    constexpr int CH = H::K0P / 8;
+    T* xT = reinterpret_cast<T*>(hb.xT);
+    for (int e = tid; e < R * CH; e += 256) {
+      const int r = e % R, k = (e / R) * 8;
+      const int s = sIdx[r];
+      float v[8];
+      if (s >= 0 && k < H::K0) {
+        const uint2 u = *reinterpret_cast<const uint2*>(br.images + (size_t)s * 784 + k);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] = mnist_norm((u.x >> (8 * j)) & 255u);
+          v[j + 4] = mnist_norm((u.y >> (8 * j)) & 255u);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sX[r * S::PX + k + j] = to_t<T>(v[j]);
+      if constexpr (TRAIN) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xT[(size_t)(k + j) * ldB + r0 + r] = to_t<T>(v[j]);
+      }
+    }
+  } else {
+    constexpr int VE = 16 / (int)sizeof(T);
+    constexpr int CH = H::K0P / VE;
+    const T* xin = reinterpret_cast<const T*>(hb.xin);
+    T* xT = reinterpret_cast<T*>(hb.xT);
+    for (int e = tid; e < R * CH; e += 256) {
+      const int r = e % R, k = (e / R) * VE;
+      uint4 u = make_uint4(0, 0, 0, 0);
+      if (r0 + r < B) u = *reinterpret_cast<const uint4*>(xin + (size_t)(r0 + r) * H::K0P + k);
+      *reinterpret_cast<uint4*>(sX + r * S::PX + k) = u;
+      if constexpr (TRAIN) {
+        const T* tv = reinterpret_cast<const T*>(&u);
+#pragma unroll
+        for (int j = 0; j < VE; ++j) xT[(size_t)(k + j) * ldB + r0 + r] = tv[j];
+      }
+    }
+  }
+  __syncthreads();
+
+  const float keep_scale = H::DROPOUT ? 1.0f / (1.0f - hb.drop_p) : 1.0f;
+  const uint32_t drop_thr = H::DROPOUT ? (uint32_t)(hb.drop_p * 4294967295.0f) : 0u;
+
+  // ---------------------------------------------------------------- L1: H1 = relu(X W1^T + b1)
+  {
+    constexpr int NT = H::N1P / 16, KCH = H::K0P / KC;
+    T* h1T = reinterpret_cast<T*>(hb.h1T);
+    for (int nt = w; nt < NT; nt += 4) {
+      f32x4 acc[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = zero4();
+      const T* bp = pack + H::F1 + (nt * 16 + row) * H::K0P + grp * KV;
+      const T* ap = sX + row * S::PX + grp * KV;
+      for (int kc = 0; kc < KCH; ++kc) {
+        const Frag b = M::load(bp + kc * KC);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) M::mma(acc[m], M::load(ap + m * 16 * S::PX + kc * KC), b);
+      }
+      const int n = nt * 16 + row;
+      const float bias = n < H::N1 ? prm[H::B1 + n] : 0.f;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = m * 16 + grp * 4 + i, rg = r0 + r;
+          float x = fmaxf(acc[m][i] + bias, 0.f);
+          if constexpr (H::DROPOUT && TRAIN) {
+            const uint32_t h = hash4(hb.seed, (uint32_t)gstep, (uint32_t)rg, (uint32_t)n);
+            x = (h >= drop_thr) ? x * keep_scale : 0.f;
+          }
+          if (n >= H::N1 || rg >= B) x = 0.f;
+          sH1[r * S::P1 + n] = to_t<T>(x);
+          v[i] = to_f(to_t<T>(x));
+        }
+        if constexpr (TRAIN)
+          store_col4<T>(h1T + (size_t)n * ldB + r0 + m * 16 + grp * 4, v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---------------------------------------------------------------- L2: H2 = relu(H1 W2^T + b2)
+  {
+    constexpr int NT = H::N2P / 16, KCH = H::N1P / KC;
+    T* h2T = reinterpret_cast<T*>(hb.h2T);
+    for (int nt = w; nt < NT; nt += 4) {
+      f32x4 acc[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = zero4();
+      const T* bp = pack + H::F2 + (nt * 16 + row) * H::N1P + grp * KV;
+      const T* ap = sH1 + row * S::P1 + grp * KV;
+      for (int kc = 0; kc < KCH; ++kc) {
+        const Frag b = M::load(bp + kc * KC);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) M::mma(acc[m], M::load(ap + m * 16 * S::P1 + kc * KC), b);
+      }
+      const int n = nt * 16 + row;
+      const float bias = n < H::N2 ? prm[H::B2 + n] : 0.f;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = m * 16 + grp * 4 + i, rg = r0 + r;
+          float x = fmaxf(acc[m][i] + bias, 0.f);
+          if (n >= H::N2 || rg >= B) x = 0.f;
+          sH2[r * S::P2 + n] = to_t<T>(x);
+          v[i] = to_f(to_t<T>(x));
+        }
+        if constexpr (TRAIN)
+          store_col4<T>(h2T + (size_t)n * ldB + r0 + m * 16 + grp * 4, v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---------------------------------------------------------------- L3: logits = H2 W3^T (+ b3)
+  {
+    constexpr int KCH = H::N2P / KC;
+    for (int m = w; m < MT; m += 4) {
+      f32x4 acc = zero4();
+      const T* bp = pack + H::F3 + row * H::N2P + grp * KV;
+      const T* ap = sH2 + (m * 16 + row) * S::P2 + grp * KV;
+      for (int kc = 0; kc < KCH; ++kc) M::mma(acc, M::load(ap + kc * KC), M::load(bp + kc * KC));
+      const int c = row;
+      const float bias = (H::BIAS3 && c < H::NC) ? prm[H::B3 + c] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sLog[(m * 16 + grp * 4 + i) * 16 + c] = acc[i] + bias;
+    }
+  }
+  __syncthreads();
+
+  // ---------------------------------------------------------------- softmax cross-entropy
+  if (w == 0) {
+    float loss = 0.f, corr = 0.f, cnt = 0.f;
+    T* dy3T = reinterpret_cast<T*>(hb.dy3T);
+    for (int r = lane; r < R; r += 64) {
+      const int rg = r0 + r;
+      const bool valid = rg < B;
+      float z[H::NC];
+      float mx = -INFINITY;
+      int am = 0;
+#pragma unroll
+      for (int c = 0; c < H::NC; ++c) {
+        z[c] = sLog[r * 16 + c];
+        if (z[c] > mx) { mx = z[c]; am = c; }
+      }
+      float se = 0.f;
+#pragma unroll
+      for (int c = 0; c < H::NC; ++c) se += __expf(z[c] - mx);
+      const int y = valid ? (int)br.labels[sIdx[r]] : 0;
+      const float lse = mx + __logf(se);
+      if (valid) {
+        loss += lse - z[y];
+        corr += (am == y) ? 1.f : 0.f;
+        cnt += 1.f;
+      }
+      if constexpr (TRAIN) {
+        const float inv = 1.f / se;
+#pragma unroll
+        for (int c = 0; c < H::NCK; ++c) {
+          float d = 0.f;
+          if (valid && c < H::NC) d = __expf(z[c] - mx) * inv - (c == y ? 1.f : 0.f);
+          sD[r * S::PD + c] = to_t<T>(d);
+          if (c < H::NCP) dy3T[(size_t)c * ldB + rg] = to_t<T>(d);
+        }
+      }
+    }
+    loss = wave_sum(loss);
+    corr = wave_sum(corr);
+    cnt = wave_sum(cnt);
+    if (lane == 0) {
+      atomicAdd(hb.metrics + 0, loss);
+      atomicAdd(hb.metrics + 1, corr);
+      atomicAdd(hb.metrics + 2, cnt);
+    }
+  }
+  if constexpr (!TRAIN) return;
+  __syncthreads();
+
+  // ---------------------------------------------------------------- dH2 = (dZ W3) * [H2 > 0]
+  {
+    constexpr int NT = H::N2P / 16, KCH = H::NCK / KC;
+    T* dy2T = reinterpret_cast<T*>(hb.dy2T);
+    for (int nt = w; nt < NT; nt += 4) {
+      f32x4 acc[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = zero4();
+      const T* bp = pack + H::F3T + (nt * 16 + row) * H::NCK + grp * KV;
+      const T* ap = sD + row * S::PD + grp * KV;
+#pragma unroll
+      for (int kc = 0; kc < KCH; ++kc) {
+        const Frag b = M::load(bp + kc * KC);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) M::mma(acc[m], M::load(ap + m * 16 * S::PD + kc * KC), b);
+      }
+      const int n = nt * 16 + row;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = m * 16 + grp * 4 + i;
+          T* h = &sH2[r * S::P2 + n];
+          const float x = to_f(*h) > 0.f ? acc[m][i] : 0.f;
+          *h = to_t<T>(x);  // in place: H2 becomes dH2
+          v[i] = to_f(to_t<T>(x));
+        }
+        store_col4<T>(dy2T + (size_t)n * ldB + r0 + m * 16 + grp * 4, v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---------------------------------------------------------------- dH1 = (dH2 W2) * [H1 > 0] / keep
+  {
+    constexpr int NT = H::N1P / 16, KCH = H::N2P / KC;
+    T* dy1T = reinterpret_cast<T*>(hb.dy1T);
+    for (int nt = w; nt < NT; nt += 4) {
+      f32x4 acc[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = zero4();
+      const T* bp = pack + H::F2T + (nt * 16 + row) * H::N2P + grp * KV;
+      const T* ap = sH2 + row * S::P2 + grp * KV;
+      for (int kc = 0; kc < KCH; ++kc) {
+        const Frag b = M::load(bp + kc * KC);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) M::mma(acc[m], M::load(ap + m * 16 * S::P2 + kc * KC), b);
+      }
+      const int n = nt * 16 + row;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = m * 16 + grp * 4 + i;
+          T* h = &sH1[r * S::P1 + n];
+          const float x = to_f(*h) > 0.f ? acc[m][i] * keep_scale : 0.f;
+          *h = to_t<T>(x);  // in place: H1 becomes dH1
+          v[i] = to_f(to_t<T>(x));
+        }
+        store_col4<T>(dy1T + (size_t)n * ldB + r0 + m * 16 + grp * 4, v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+
+  // ---------------------------------------------------------------- dX = dH1 W1 (LeNet: into pool2 grads)
+  if constexpr (H::DX) {
+    __syncthreads();
+    constexpr int NT = rup(H::K0, 16) / 16, KCH = H::N1P / KC;
+    T* dx = reinterpret_cast<T*>(hb.dx);
+    for (int nt = w; nt < NT; nt += 4) {
+      f32x4 acc[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) acc[m] = zero4();
+      const T* bp = pack + H::F1T + (nt * 16 + row) * H::N1P + grp * KV;
+      const T* ap = sH1 + row * S::P1 + grp * KV;
+      for (int kc = 0; kc < KCH; ++kc) {
+        const Frag b = M::load(bp + kc * KC);
+#pragma unroll
+        for (int m = 0; m < MT; ++m) M::mma(acc[m], M::load(ap + m * 16 * S::P1 + kc * KC), b);
+      }
+      const int k = nt * 16 + row;
+#pragma unroll
+      for (int m = 0; m < MT; ++m) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int rg = r0 + m * 16 + grp * 4 + i;
+          if (rg < B) dx[(size_t)rg * H::K0P + k] = to_t<T>(acc[m][i]);
+        }
+      }
+    }
+  }
+}
+
+// ====================================================================================
+// Grouped weight-gradient GEMM:  dW[n][k] = sum_r dY^T[n][r] * X^T[k][r]  (+ bias column k == K)
+// Both operands are stored row = feature, contiguous batch, so each lane's K-chunk fragment is
+// one 16-byte load.  A 64x64 output block per workgroup (each wave 32x32 = 2x2 MFMA tiles);
+// the batch is split over gridDim.y, each split writes its own fp32 slab row (deterministic).
+// ====================================================================================
+template <typename T>
+struct WgJob {
+  const T* dyT;
+  const T* xT;
+  int N, K, NP, bias, out_off, nblk_k, blk_begin;
+};
+template <typename T>
+struct WgArgs {
+  WgJob<T> job[3];
+  int njobs, ldB, rlen, Bp, slab_ld;
+  float* slab;
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
+  using M = Mma<T>;
+  using Frag = typename M::Frag;
+  constexpr int KV = M::KV, KC = M::KC;
+  const int lane = threadIdx.x & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
+  int j = 0;
+  while (j + 1 < a.njobs && (int)blockIdx.x >= a.job[j + 1].blk_begin) ++j;
+  const WgJob<T>& J = a.job[j];
+  const int lb = blockIdx.x - J.blk_begin;
+  const int bn = lb / J.nblk_k, bk = lb % J.nblk_k;
+  const int n0 = bn * 64 + (w >> 1) * 32, k0 = bk * 64 + (w & 1) * 32;
+  const int Kb = J.K + (J.bias ? 1 : 0);
+  if (n0 >= J.N || k0 >= Kb) return;
+  const bool nv1 = n0 + 16 < J.NP;
+  const int rs = blockIdx.y * a.rlen;
+  const int re = min(rs + a.rlen, a.Bp);
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = zero4();
+
+  Frag ones;
+#pragma unroll
+  for (int q = 0; q < KV; ++q) M::set(ones, q, 1.f);
+  const Frag zf = M::zero();
+
+  const T* ap0 = J.dyT + (size_t)(n0 + row) * a.ldB + grp * KV;
+  const T* ap1 = J.dyT + (size_t)(n0 + 16 + row) * a.ldB + grp * KV;
+  const int kk0 = k0 + row, kk1 = k0 + 16 + row;
+  const T* bp0 = J.xT + (size_t)min(kk0, J.K > 0 ? J.K - 1 : 0) * a.ldB + grp * KV;
+  const T* bp1 = J.xT + (size_t)min(kk1, J.K > 0 ? J.K - 1 : 0) * a.ldB + grp * KV;
+  const int sel0 = kk0 < J.K ? 0 : (kk0 == J.K && J.bias ? 1 : 2);
+  const int sel1 = kk1 < J.K ? 0 : (kk1 == J.K && J.bias ? 1 : 2);
+
+  for (int rc = rs; rc < re; rc += KC) {
+    const Frag a0 = M::load(ap0 + rc);
+    const Frag a1 = nv1 ? M::load(ap1 + rc) : zf;
+    const Frag bl0 = M::load(bp0 + rc);
+    const Frag bl1 = M::load(bp1 + rc);
+    const Frag b0 = sel0 == 0 ? bl0 : (sel0 == 1 ? ones : zf);
+    const Frag b1 = sel1 == 0 ? bl1 : (sel1 == 1 ? ones : zf);
+    M::mma(acc[0][0], a0, b0);
+    M::mma(acc[0][1], a0, b1);
+    M::mma(acc[1][0], a1, b0);
+    M::mma(acc[1][1], a1, b1);
+  }
+
+  float* out = a.slab + (size_t)blockIdx.y * a.slab_ld + J.out_off;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const int k = k0 + ni * 16 + row;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int n = n0 + mi * 16 + grp * 4 + i;
+        if (n >= J.N) continue;
+        if (k < J.K) out[(size_t)n * J.K + k] = acc[mi][ni][i];
+        else if (k == J.K && J.bias) out[(size_t)J.N * J.K + n] = acc[mi][ni][i];
+      }
+    }
+}
+
+template <typename T, class H>
+int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab_ld, hipStream_t s) {
+  WgArgs<T> a{};
+  auto mk = [&](int i, const void* dy, const void* x, int N, int K, int NP, bool bias, int off, int& blk) {
+    WgJob<T>& J = a.job[i];
+    J.dyT = reinterpret_cast<const T*>(dy);
+    J.xT = reinterpret_cast<const T*>(x);
+    J.N = N; J.K = K; J.NP = NP; J.bias = bias ? 1 : 0; J.out_off = off;
+    J.nblk_k = (K + (bias ? 1 : 0) + 63) / 64;
+    J.blk_begin = blk;
+    blk += ((N + 63) / 64) * J.nblk_k;
+  };
+  int blk = 0;
+  mk(0, hb.dy1T, hb.xT, H::N1, H::K0, H::N1P, true, H::W1, blk);
+  mk(1, hb.dy2T, hb.h1T, H::N2, H::N1, H::N2P, true, H::W2, blk);
+  mk(2, hb.dy3T, hb.h2T, H::NC, H::N2, H::NCP, H::BIAS3, H::W3, blk);
+  a.njobs = 3;
+  a.ldB = hb.ldB;
+  constexpr int KC = Mma<T>::KC;
+  a.Bp = rup(B, KC);
+  splits = std::max(1, std::min(splits, a.Bp / KC));
+  a.rlen = rup((a.Bp + splits - 1) / splits, KC);
+  splits = (a.Bp + a.rlen - 1) / a.rlen;
+  a.slab = slab;
+  a.slab_ld = slab_ld;
+  hipLaunchKernelGGL(wgrad_kernel<T>, dim3(blk, splits), dim3(256), 0, s, a);
+  return splits;
+}
+
+template <typename T, class H, int MT>
+void head_launch_mt(bool train, const BatchRef& br, const HeadBuffers& hb, hipStream_t s) {
+  const int rows = rup(br.B, 32);
+  const int grid = (rows + MT * 16 - 1) / (MT * 16);
+  if (train)
+    hipLaunchKernelGGL((head_kernel<T, H, MT, true>), dim3(grid), dim3(256), 0, s, br, hb);
+  else
+    hipLaunchKernelGGL((head_kernel<T, H, MT, false>), dim3(grid), dim3(256), 0, s, br, hb);
+}
+
+template <typename T, class H>
+void head_launch_t(bool train, const BatchRef& br, const HeadBuffers& hb, int rows, hipStream_t s) {
+  if (rows <= 16) head_launch_mt<T, H, 1>(train, br, hb, s);
+  else if (rows <= 32 || !HeadSmem<T, H, 4>::FITS) {
+    if constexpr (HeadSmem<T, H, 2>::FITS) head_launch_mt<T, H, 2>(train, br, hb, s);
+    else head_launch_mt<T, H, 1>(train, br, hb, s);
+  } else {
+    if constexpr (HeadSmem<T, H, 4>::FITS) head_launch_mt<T, H, 4>(train, br, hb, s);
+  }
+}
+
+}  // namespace
+
+int head_rows_per_block(ModelKind m, DType t, int B) {
+  if (B <= 256) return 16;
+  if (t == DType::F32) return 32;
+  if (m == ModelKind::MLP) return B >= 4096 ? 64 : 32;
+  return B >= 2048 ? 64 : 32;
+}
+
+void launch_head(ModelKind m, DType t, bool train, const BatchRef& br, const HeadBuffers& hb, int rows,
+                 hipStream_t s) {
+  if (m == ModelKind::MLP) {
+    if (t == DType::F32) head_launch_t<float, MlpModel::Head>(train, br, hb, rows, s);
+    else head_launch_t<bf16, MlpModel::Head>(train, br, hb, rows, s);
+  } else {
+    if (t == DType::F32) head_launch_t<float, LenetModel::Head>(train, br, hb, rows, s);
+    else head_launch_t<bf16, LenetModel::Head>(train, br, hb, rows, s);
+  }
+}
+
+int launch_head_wgrad(ModelKind m, DType t, const HeadBuffers& hb, int B, int splits, float* slab,
+                      int slab_ld, hipStream_t s) {
+  if (m == ModelKind::MLP) {
+    if (t == DType::F32) return wgrad_launch<float, MlpModel::Head>(hb, B, splits, slab, slab_ld, s);
+    return wgrad_launch<bf16, MlpModel::Head>(hb, B, splits, slab, slab_ld, s);
+  }
+  if (t == DType::F32) return wgrad_launch<float, LenetModel::Head>(hb, B, splits, slab, slab_ld, s);
+  return wgrad_launch<bf16, LenetModel::Head>(hb, B, splits, slab, slab_ld, s);
+}

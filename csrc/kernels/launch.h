@@ -1,0 +1,80 @@
+// Host-side launch interface of the HIP kernels (all launches are stream-ordered,
+// allocation-free and synchronisation-free, so the whole step is hipGraph-capturable).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+enum class ModelKind : int { MLP = 0, LENET = 1 };
+enum class DType : int { F32 = 0, BF16 = 1 };
+
+// Batch addressing shared by all kernels of a step: the rows of the current step are
+// idx_epoch[*step_ptr * batch_stride + r], r < B.  A device-side step counter (bumped
+// by the optimizer kernel) keeps captured graphs valid across steps.
+struct BatchRef {
+  const uint8_t* images;     // [N][784] uint8, HBM-resident dataset
+  const uint8_t* labels;     // [N]
+  const int32_t* idx_epoch;  // this rank's sample order for the epoch
+  const int32_t* step_ptr;   // device step counter
+  int32_t batch_stride;      // regular batch size
+  int32_t B;                 // rows in this batch (<= batch_stride)
+};
+
+struct HeadBuffers {
+  const float* params;   // fp32 master slab
+  const void* pack;      // packed T operands
+  const void* xin;       // LeNet: p2 [B][K0P] (T); MLP: unused (gather)
+  void* xT;              // [K0P][ldB]  layer-1 input, transposed (wgrad operand)
+  void* h1T;             // [N1P][ldB]
+  void* h2T;             // [N2P][ldB]
+  void* dy1T;            // [N1P][ldB]
+  void* dy2T;            // [N2P][ldB]
+  void* dy3T;            // [16][ldB]
+  void* dx;              // LeNet: dp2 [B][K0P]
+  float* metrics;        // [loss_sum, correct, count]
+  int32_t ldB;
+  uint32_t seed;
+  float drop_p;
+};
+
+struct LenetConvBuffers {
+  const float* params;
+  const void* pack;
+  void* p1;              // [B][196][8] T  pool1 output (NHWC, C padded to 8)
+  uint8_t* m1;           // [B][196][8]    pool1 argmax(2b)|relu-positive(bit 2)
+  void* p2;              // [B][K0P=416] T pool2 output (NCHW flatten), cols >=400 zero
+  uint8_t* m2;           // [B][400]
+  const void* dp2;       // [B][416] T   (backward input)
+  float* slab;           // conv partial grads, row per workgroup: [G][2572]
+};
+
+int head_rows_per_block(ModelKind m, DType t, int B);
+
+void launch_head(ModelKind m, DType t, bool train, const BatchRef& br, const HeadBuffers& hb,
+                 int rows_per_block, hipStream_t s);
+
+// Grouped weight-gradient GEMM over the batch (split-K over rows): writes S slabs, returns S.
+int launch_head_wgrad(ModelKind m, DType t, const HeadBuffers& hb, int B, int splits, float* slab,
+                       int slab_ld, hipStream_t s);
+
+void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetConvBuffers& cb,
+                           hipStream_t s);
+void launch_lenet_conv_bwd(DType t, const BatchRef& br, const LenetConvBuffers& cb, int* nslab_out,
+                           hipStream_t s);
+int lenet_conv_bwd_blocks(int B);
+
+// grad[p] = scale * sum_s slab[s][p]  for p in [p0, p1)
+void launch_reduce(const float* slab, int slab_ld, int nslab, int p0, int p1, float scale, float* grad,
+                   hipStream_t s);
+
+// SGD (+momentum) on the flat fp32 slab, then re-pack operands; optionally bumps the step counter.
+void launch_sgd_pack(ModelKind m, DType t, float* params, const float* grad, float* mom, void* pack,
+                     int nparam, float lr, float momentum, float gscale, int32_t* step_ptr,
+                     hipStream_t s);
+void launch_pack(ModelKind m, DType t, const float* params, void* pack, int nparam, hipStream_t s);
+
+void launch_gather_normalize(DType t, const BatchRef& br, void* out, int ld, hipStream_t s);
+
+// model geometry queried by the host runtime
+int model_nparam(ModelKind m);
+int model_conv_params(ModelKind m);
+int model_pack_size(ModelKind m);

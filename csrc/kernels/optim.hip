@@ -1,0 +1,141 @@
+// Gradient reduction, optimizer and operand packing kernels.
+//
+//  reduce_slabs : grad[p] = scale * sum_s slab[s][p] in a FIXED order (bitwise reproducible,
+//                 no float atomics).  Replaces the per-parameter .grad accumulation + the DDP
+//                 Reducer's bucket copy (survey N6/N9); `scale` carries the 1/B of the mean loss.
+//  sgd_pack     : p -= lr * (mu*buf + g/W) over the flat fp32 master slab (torch SGD semantics,
+//                 dampening 0, ddp_tutorial_cpu.py:61), 1/W of DDP averaging folded in, then the
+//                 updated value is re-packed into the compute-dtype MFMA operand images
+//                 (models.h) and the device step counters are advanced.  Replaces the
+//                 _foreach_add_ multi-tensor apply (survey K15) plus any weight cast kernels.
+#include <algorithm>
+
+#include "common.h"
+#include "launch.h"
+#include "models.h"
+
+namespace {
+
+// One block = 64 consecutive parameters (lane) x NW waves splitting the slab rows; the per-wave
+// partial sums are combined in a fixed tree, so the result is bitwise reproducible.
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void reduce_slabs_kernel(const float* __restrict__ slab, int ld, int nslab,
+                                                               int p0, int p1, float scale, float* __restrict__ grad) {
+  __shared__ float part[NW][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int p = p0 + blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (p < p1) {
+    const int per = (nslab + NW - 1) / NW;
+    const int sb = w * per, se = min(nslab, sb + per);
+    int k = sb;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    for (; k + 4 <= se; k += 4) {
+      s0 += slab[(size_t)k * ld + p];
+      s1 += slab[(size_t)(k + 1) * ld + p];
+      s2 += slab[(size_t)(k + 2) * ld + p];
+      s3 += slab[(size_t)(k + 3) * ld + p];
+    }
+    for (; k < se; ++k) s0 += slab[(size_t)k * ld + p];
+    s = (s0 + s1) + (s2 + s3);
+  }
+  part[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && p < p1) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) t += part[i][lane];
+    grad[p] = t * scale;
+  }
+}
+
+template <class Model, typename T>
+__global__ __launch_bounds__(256) void sgd_pack_kernel(float* __restrict__ params, const float* __restrict__ grad,
+                                                       float* __restrict__ mom, T* __restrict__ pack, int n,
+                                                       float lr, float mu, float gscale, int32_t* step_ptr,
+                                                       int update) {
+  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
+    float v = params[p];
+    if (update) {
+      float g = grad[p] * gscale;
+      if (mom) {
+        const float b = mu * mom[p] + g;
+        mom[p] = b;
+        g = b;
+      }
+      v = v - lr * g;
+      params[p] = v;
+    }
+    Packer<Model, T>::pack(p, v, pack);
+  }
+  if (update && step_ptr && blockIdx.x == 0 && threadIdx.x == 0) {
+    step_ptr[0] += 1;  // step within epoch (batch addressing)
+    step_ptr[1] += 1;  // global step (dropout stream)
+  }
+}
+
+template <class Model, typename T>
+void sgd_launch(float* params, const float* grad, float* mom, void* pack, int n, float lr, float mu, float gscale,
+                int32_t* step_ptr, int update, hipStream_t s) {
+  const int grid = std::min(1024, (n + 255) / 256);
+  hipLaunchKernelGGL((sgd_pack_kernel<Model, T>), dim3(grid), dim3(256), 0, s, params, grad, mom,
+                     reinterpret_cast<T*>(pack), n, lr, mu, gscale, step_ptr, update);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gather_normalize_kernel(BatchRef br, T* out, int ld) {
+  const int r = blockIdx.x;
+  if (r >= br.B) return;
+  const int32_t* idx = br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride;
+  const uint8_t* img = br.images + (size_t)idx[r] * 784;
+  for (int k = threadIdx.x; k < 784; k += blockDim.x) out[(size_t)r * ld + k] = to_t<T>(mnist_norm(img[k]));
+}
+
+}  // namespace
+
+void launch_reduce(const float* slab, int slab_ld, int nslab, int p0, int p1, float scale, float* grad,
+                   hipStream_t s) {
+  if (p1 <= p0) return;
+  const int grid = (p1 - p0 + 63) / 64;
+  if (nslab >= 64)
+    hipLaunchKernelGGL(reduce_slabs_kernel<16>, dim3(grid), dim3(1024), 0, s, slab, slab_ld, nslab, p0, p1, scale, grad);
+  else if (nslab >= 8)
+    hipLaunchKernelGGL(reduce_slabs_kernel<4>, dim3(grid), dim3(256), 0, s, slab, slab_ld, nslab, p0, p1, scale, grad);
+  else
+    hipLaunchKernelGGL(reduce_slabs_kernel<1>, dim3(grid), dim3(64), 0, s, slab, slab_ld, nslab, p0, p1, scale, grad);
+}
+
+void launch_sgd_pack(ModelKind m, DType t, float* params, const float* grad, float* mom, void* pack, int nparam,
+                     float lr, float momentum, float gscale, int32_t* step_ptr, hipStream_t s) {
+  float* mb = momentum != 0.f ? mom : nullptr;
+  if (m == ModelKind::MLP) {
+    if (t == DType::F32) sgd_launch<MlpModel, float>(params, grad, mb, pack, nparam, lr, momentum, gscale, step_ptr, 1, s);
+    else sgd_launch<MlpModel, bf16>(params, grad, mb, pack, nparam, lr, momentum, gscale, step_ptr, 1, s);
+  } else {
+    if (t == DType::F32) sgd_launch<LenetModel, float>(params, grad, mb, pack, nparam, lr, momentum, gscale, step_ptr, 1, s);
+    else sgd_launch<LenetModel, bf16>(params, grad, mb, pack, nparam, lr, momentum, gscale, step_ptr, 1, s);
+  }
+}
+
+void launch_pack(ModelKind m, DType t, const float* params, void* pack, int nparam, hipStream_t s) {
+  float* p = const_cast<float*>(params);
+  if (m == ModelKind::MLP) {
+    if (t == DType::F32) sgd_launch<MlpModel, float>(p, nullptr, nullptr, pack, nparam, 0.f, 0.f, 0.f, nullptr, 0, s);
+    else sgd_launch<MlpModel, bf16>(p, nullptr, nullptr, pack, nparam, 0.f, 0.f, 0.f, nullptr, 0, s);
+  } else {
+    if (t == DType::F32) sgd_launch<LenetModel, float>(p, nullptr, nullptr, pack, nparam, 0.f, 0.f, 0.f, nullptr, 0, s);
+    else sgd_launch<LenetModel, bf16>(p, nullptr, nullptr, pack, nparam, 0.f, 0.f, 0.f, nullptr, 0, s);
+  }
+}
+
+void launch_gather_normalize(DType t, const BatchRef& br, void* out, int ld, hipStream_t s) {
+  if (br.B <= 0) return;
+  if (t == DType::F32)
+    hipLaunchKernelGGL(gather_normalize_kernel<float>, dim3(br.B), dim3(256), 0, s, br, reinterpret_cast<float*>(out), ld);
+  else
+    hipLaunchKernelGGL(gather_normalize_kernel<bf16>, dim3(br.B), dim3(256), 0, s, br, reinterpret_cast<bf16*>(out), ld);
+}
+
+int model_nparam(ModelKind m) { return m == ModelKind::MLP ? MlpModel::NPARAM : LenetModel::NPARAM; }
+int model_conv_params(ModelKind m) { return m == ModelKind::MLP ? 0 : LenetModel::CONV_PARAMS; }
+int model_pack_size(ModelKind m) { return m == ModelKind::MLP ? MlpModel::PACK_SIZE : LenetModel::PACK_SIZE; }

@@ -1,0 +1,86 @@
+#include "rccl_comm.h"
+
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+#include <thread>
+
+#include "hip_check.h"
+
+#define NCCL_CHECK(x)                                                                        \
+  do {                                                                                       \
+    ncclResult_t r_ = (x);                                                                   \
+    if (r_ != ncclSuccess && r_ != ncclInProgress)                                          \
+      throw std::runtime_error(std::string("RCCL error: ") + ncclGetErrorString(r_) + " at " \
+                               + __FILE__ + ":" + std::to_string(__LINE__));                 \
+  } while (0)
+
+std::string RcclComm::make_unique_id() {
+  ncclUniqueId id;
+  NCCL_CHECK(ncclGetUniqueId(&id));
+  return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
+}
+
+int RcclComm::version() {
+  int v = 0;
+  ncclGetVersion(&v);
+  return v;
+}
+
+RcclComm::RcclComm(const std::string& uid, int rank, int world, int device) : rank_(rank), world_(world) {
+  if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("RcclComm: bad unique id size");
+  ncclUniqueId id;
+  std::memcpy(&id, uid.data(), sizeof(id));
+  HIP_CHECK(hipSetDevice(device));
+  NCCL_CHECK(ncclCommInitRank(&comm_, world, id, rank));
+}
+
+RcclComm::~RcclComm() {
+  if (comm_ && !aborted_) ncclCommDestroy(comm_);
+}
+
+void RcclComm::all_reduce_sum_f32(float* buf, size_t count, hipStream_t s) {
+  if (world_ == 1 || count == 0) return;
+  NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm_, s));
+}
+
+void RcclComm::broadcast_f32(float* buf, size_t count, int root, hipStream_t s) {
+  if (world_ == 1 || count == 0) return;
+  NCCL_CHECK(ncclBroadcast(buf, buf, count, ncclFloat32, root, comm_, s));
+}
+
+void RcclComm::all_reduce_max_f64(double* buf, size_t count, hipStream_t s) {
+  if (world_ == 1 || count == 0) return;
+  NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclFloat64, ncclMax, comm_, s));
+}
+
+std::string RcclComm::async_error() {
+  if (!comm_) return "communicator not initialised";
+  ncclResult_t e = ncclSuccess;
+  if (ncclCommGetAsyncError(comm_, &e) != ncclSuccess) return "ncclCommGetAsyncError failed";
+  if (e == ncclSuccess || e == ncclInProgress) return "";
+  return ncclGetErrorString(e);
+}
+
+void RcclComm::wait_stream(hipStream_t s, double timeout_s) {
+  auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) HIP_CHECK(q);
+    std::string err = async_error();
+    double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (!err.empty() || (timeout_s > 0 && el > timeout_s)) {
+      abort();
+      throw std::runtime_error("RCCL collective failed: " + (err.empty() ? std::string("timeout") : err));
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
+void RcclComm::abort() {
+  if (comm_ && !aborted_) {
+    ncclCommAbort(comm_);
+    aborted_ = true;
+  }
+}

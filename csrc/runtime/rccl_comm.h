@@ -1,0 +1,39 @@
+// Native RCCL communicator (the GPU data plane of the DDP gradient exchange).
+//
+// Replaces c10d ProcessGroupNCCL as used by the reference (ddp_tutorial_multi_gpu.py:133-134,
+// DDP Reducer all-reduce per step; survey B1/N10).  One communicator per process/GPU; the
+// 128-byte ncclUniqueId is produced by rank 0 and exchanged through the control-plane TCP
+// store (parallel/comm.py).  Collectives are enqueued on caller-provided HIP streams so they
+// can be overlapped with backward kernels and captured into the step's hipGraph.  Failure
+// handling: ncclCommGetAsyncError polling with a deadline, then ncclCommAbort (survey §5.3).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <string>
+
+class RcclComm {
+ public:
+  static std::string make_unique_id();  // 128 raw bytes
+  RcclComm(const std::string& uid, int rank, int world, int device);
+  ~RcclComm();
+  RcclComm(const RcclComm&) = delete;
+  RcclComm& operator=(const RcclComm&) = delete;
+
+  void all_reduce_sum_f32(float* buf, size_t count, hipStream_t s);
+  void broadcast_f32(float* buf, size_t count, int root, hipStream_t s);
+  void all_reduce_max_f64(double* buf, size_t count, hipStream_t s);
+  // Returns "" if healthy, else the error string.  Non-blocking.
+  std::string async_error();
+  // Wait for `s` with async-error polling; aborts the communicator and throws on error/timeout.
+  void wait_stream(hipStream_t s, double timeout_s);
+  void abort();
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  static int version();
+
+ private:
+  ncclComm_t comm_ = nullptr;
+  int rank_, world_;
+  bool aborted_ = false;
+};

@@ -1,0 +1,89 @@
+// Static-schedule training step: the whole forward/backward/all-reduce/update of one batch as a
+// fixed list of stream-ordered launches (no autograd tape, survey N8), optionally captured into
+// one hipGraph and replayed per step.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../kernels/launch.h"
+#include "rccl_comm.h"
+
+struct TrainerPtrs {
+  uintptr_t images = 0, labels = 0, idx = 0, step = 0;
+  uintptr_t params = 0, grad = 0, mom = 0, pack = 0;
+  uintptr_t slab_fc = 0, slab_conv = 0, metrics = 0;
+  uintptr_t xT = 0, h1T = 0, h2T = 0, dy1T = 0, dy2T = 0, dy3T = 0;
+  uintptr_t p1 = 0, m1 = 0, p2 = 0, m2 = 0, dp2 = 0;
+};
+
+// A gradient bucket = contiguous range of the flat grad slab, all-reduced as one RCCL call as
+// soon as the backward phase that produces it has been reduced (phase 0 = FC head, 1 = conv).
+struct Bucket {
+  int p0, p1, phase;
+};
+
+class Trainer {
+ public:
+  Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const TrainerPtrs& p);
+  ~Trainer();
+
+  void set_comm(std::shared_ptr<RcclComm> c) { comm_ = std::move(c); }
+  void set_world(int w) { world_ = w; }
+  void set_optimizer(float lr, float momentum) { lr_ = lr; momentum_ = momentum; invalidate(); }
+  void set_dropout(float p, uint32_t seed) { drop_p_ = p; seed_ = seed; invalidate(); }
+  void set_buckets(const std::vector<Bucket>& b) { buckets_ = b; invalidate(); }
+  std::vector<Bucket> buckets() const { return buckets_; }
+  void set_overlap(bool on) { overlap_ = on; invalidate(); }
+
+  void pack(uintptr_t stream);
+  // Full eager step for a batch of B rows (B <= batch).
+  void train_step(int B, uintptr_t stream);
+  // Phases (used by the torch.distributed comm path and by tests).
+  void forward_backward(int B, uintptr_t stream);
+  void reduce_grads(int B, uintptr_t stream);
+  void optimizer_step(float gscale, uintptr_t stream);
+  // Forward-only metrics over an explicit index vector (eval loop).
+  void eval_batch(uintptr_t images, uintptr_t labels, uintptr_t idx, int B, uintptr_t metrics,
+                  uintptr_t stream);
+
+  // hipGraph of train_step(batch) captured on `stream`, replayed by replay().
+  void capture(uintptr_t stream);
+  void replay(uintptr_t stream);
+  bool captured() const { return exec_ != nullptr; }
+  void invalidate();
+
+  int nparam() const { return nparam_; }
+  int pack_size() const;
+  int conv_slabs() const;
+  int conv_params() const;
+  int fc_splits() const { return fc_splits_; }
+
+ private:
+  BatchRef batch_ref(int B) const;
+  HeadBuffers head_buffers(float* metrics) const;
+  LenetConvBuffers conv_buffers() const;
+  void launch_step(int B, hipStream_t s);
+  void comm_phase(int phase, hipStream_t s);
+
+  ModelKind model_;
+  DType dtype_;
+  int batch_, ldb_, fc_splits_, nparam_;
+  TrainerPtrs p_;
+  float lr_ = 0.01f, momentum_ = 0.f, drop_p_ = 0.2f;
+  uint32_t seed_ = 1234;
+  int world_ = 1;
+  bool overlap_ = true;
+  std::shared_ptr<RcclComm> comm_;
+  std::vector<Bucket> buckets_;
+  hipStream_t comm_stream_ = nullptr;
+  std::vector<hipEvent_t> events_;
+  hipGraph_t graph_ = nullptr;
+  hipGraphExec_t exec_ = nullptr;
+  int zero_step_dev_ = 0;
+  int32_t* zero_counter_ = nullptr;  // device {0,0} for eval batch addressing
+};

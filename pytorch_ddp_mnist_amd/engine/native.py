@@ -1,0 +1,242 @@
+"""Python façade of the native MI355X trainer (``csrc/runtime/trainer.cpp``).
+
+Owns every device buffer of a training run (allocated once through torch's HBM caching
+allocator, never re-allocated per step) and exposes epoch-level operations:
+
+  * the train set lives in HBM as uint8 ``[N,784]`` + uint8 labels (47 MB for MNIST — the
+    reference instead re-decodes PIL images in 4 DataLoader workers every epoch, survey N13/N14);
+  * one int32 index vector per epoch (bit-equal to DistributedSampler) is uploaded with a single
+    async copy; kernels address their batch through a device step counter, so the captured
+    hipGraph of a step is replayed unchanged for every full batch;
+  * loss / accuracy are accumulated on the device and read back once per epoch (the reference
+    syncs with ``.item()`` every batch, survey K16).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from ..models import MODEL_IDS, build_model, flatten_state, unflatten_state
+from ..ops.native import require_gpu
+
+HEAD_DIMS = {  # K0P, N1P, N2P  (csrc/kernels/models.h)
+    "mlp": (800, 128, 128),
+    "lenet5": (416, 128, 96),
+}
+
+
+def _rup(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+@dataclass
+class EpochStats:
+    loss_sum: float
+    correct: float
+    count: float
+
+    @property
+    def mean_loss(self) -> float:
+        return self.loss_sum / max(self.count, 1.0)
+
+    @property
+    def accuracy(self) -> float:
+        return self.correct / max(self.count, 1.0)
+
+
+class NativeTrainer:
+    def __init__(self, model: str, dtype: str, batch: int, images: torch.Tensor, labels: torch.Tensor,
+                 device: Optional[torch.device] = None, lr: float = 0.01, momentum: float = 0.0,
+                 dropout: float = 0.2, seed: int = 1234, fc_splits: Optional[int] = None,
+                 init: Optional[torch.nn.Module] = None, max_indices: Optional[int] = None):
+        C = require_gpu()
+        self.C = C
+        self.model_name = model
+        self.dtype_name = dtype
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.batch = int(batch)
+        mid = MODEL_IDS[model]
+        tdt = torch.float32 if dtype == "fp32" else torch.bfloat16
+        did = 0 if dtype == "fp32" else 1
+        dev = self.device
+        self.nparam = C.model_nparam(mid)
+        self.images = images.to(dev, torch.uint8).contiguous().view(-1, 784)
+        self.labels = labels.to(dev, torch.uint8).contiguous().view(-1)
+        n_max = max_indices or self.images.shape[0]
+        self.ld_b = _rup(self.batch, 64)
+        KC = 16 if dtype == "fp32" else 32
+        if fc_splits is None:
+            fc_splits = max(1, min(16, _rup(self.batch, KC) // 512))
+        K0P, N1P, N2P = HEAD_DIMS[model]
+        z = lambda *s, dt=tdt: torch.zeros(*s, dtype=dt, device=dev)  # noqa: E731
+        self.params = z(self.nparam, dt=torch.float32)
+        self.grad = z(self.nparam, dt=torch.float32)
+        self.mom = z(self.nparam, dt=torch.float32)
+        self.pack_buf = z(C.model_pack_size(mid))
+        self.idx = torch.zeros(n_max, dtype=torch.int32, device=dev)
+        self.step_ctr = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.metrics = z(3, dt=torch.float32)
+        self.eval_metrics = z(3, dt=torch.float32)
+        self.xT, self.h1T, self.h2T = z(K0P, self.ld_b), z(N1P, self.ld_b), z(N2P, self.ld_b)
+        self.dy1T, self.dy2T, self.dy3T = z(N1P, self.ld_b), z(N2P, self.ld_b), z(16, self.ld_b)
+        self.slab_fc = z(fc_splits, self.nparam, dt=torch.float32)
+        conv_slabs = C.conv_bwd_blocks(self.batch) if model == "lenet5" else 0
+        ncp = C.model_conv_params(mid)
+        self.slab_conv = z(max(conv_slabs, 1), max(ncp, 1), dt=torch.float32)
+        if model == "lenet5":
+            self.p1 = z(self.ld_b * 196 * 8)
+            self.m1 = z(self.ld_b * 196 * 8, dt=torch.uint8)
+            self.p2 = z(self.ld_b, 416)
+            self.m2 = z(self.ld_b * 400, dt=torch.uint8)
+            self.dp2 = z(self.ld_b, 416)
+        else:
+            self.p1 = self.m1 = self.p2 = self.m2 = self.dp2 = None
+
+        P = C.TrainerPtrs()
+        ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
+        P.images, P.labels, P.idx, P.step = ptr(self.images), ptr(self.labels), ptr(self.idx), ptr(self.step_ctr)
+        P.params, P.grad, P.mom, P.pack = ptr(self.params), ptr(self.grad), ptr(self.mom), ptr(self.pack_buf)
+        P.slab_fc, P.slab_conv, P.metrics = ptr(self.slab_fc), ptr(self.slab_conv), ptr(self.metrics)
+        P.xT, P.h1T, P.h2T = ptr(self.xT), ptr(self.h1T), ptr(self.h2T)
+        P.dy1T, P.dy2T, P.dy3T = ptr(self.dy1T), ptr(self.dy2T), ptr(self.dy3T)
+        P.p1, P.m1, P.p2, P.m2, P.dp2 = ptr(self.p1), ptr(self.m1), ptr(self.p2), ptr(self.m2), ptr(self.dp2)
+        self._ptrs = P
+        self.rt = C.Trainer(mid, did, self.batch, self.ld_b, fc_splits, P)
+        self.rt.set_optimizer(float(lr), float(momentum))
+        self.rt.set_dropout(float(dropout), int(seed) & 0xFFFFFFFF)
+        self.stream = torch.cuda.Stream(device=dev)
+        self.world = 1
+        self.comm = None
+        self.module_template = build_model(model)
+        if init is not None:
+            self.load_module(init)
+        else:
+            self.load_module(self.module_template)
+
+    # ------------------------------------------------------------------ parameters
+    def _sync_in(self):
+        """Order our stream after torch's current stream (tensors written by torch ops)."""
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+
+    def _sync_out(self):
+        torch.cuda.current_stream(self.device).wait_stream(self.stream)
+
+    def load_flat(self, flat: torch.Tensor) -> None:
+        self.params.copy_(flat.to(self.device, torch.float32).view(-1))
+        self._sync_in()
+        self.rt.pack(self.stream.cuda_stream)
+        self._sync_out()
+
+    def load_module(self, module: torch.nn.Module) -> None:
+        self.load_flat(flatten_state(module))
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        self.stream.synchronize()
+        return unflatten_state(self.module_template, self.params)
+
+    def to_module(self) -> torch.nn.Module:
+        m = build_model(self.model_name)
+        m.load_state_dict(self.state_dict())
+        return m
+
+    # ------------------------------------------------------------------ distributed
+    def attach_comm(self, comm, world: int, overlap: bool = True) -> None:
+        """Use a native RcclComm for the gradient all-reduce (None = local only)."""
+        self.comm, self.world = comm, world
+        if comm is not None:
+            self.rt.set_comm(comm)
+        self.rt.set_world(world)
+        self.rt.set_overlap(overlap)
+
+    def set_buckets(self, ranges) -> None:
+        self.rt.set_buckets([self.C.Bucket(int(a), int(b), int(ph)) for a, b, ph in ranges])
+
+    def broadcast_params(self, root: int = 0) -> None:
+        """DDP construction semantics: every rank starts from rank 0's parameters."""
+        if self.comm is None or self.world == 1:
+            return
+        self._sync_in()
+        self.comm.broadcast_f32(self.params.data_ptr(), self.nparam, root, self.stream.cuda_stream)
+        self.rt.pack(self.stream.cuda_stream)
+        self.comm.wait_stream(self.stream.cuda_stream, 300.0)
+
+    # ------------------------------------------------------------------ training
+    def set_epoch_indices(self, indices: torch.Tensor) -> None:
+        n = indices.numel()
+        if n > self.idx.numel():
+            raise ValueError(f"epoch has {n} indices, buffer holds {self.idx.numel()}")
+        src = indices.to(torch.int32)
+        if src.device.type == "cpu":
+            src = src.pin_memory()
+        with torch.cuda.stream(self.stream):
+            self.idx[:n].copy_(src, non_blocking=True)
+            self.step_ctr[0].zero_()
+        self.n_epoch = n
+
+    def reset_metrics(self) -> None:
+        with torch.cuda.stream(self.stream):
+            self.metrics.zero_()
+
+    def read_metrics(self, which: str = "train") -> EpochStats:
+        self.stream.synchronize()
+        m = (self.metrics if which == "train" else self.eval_metrics).tolist()
+        return EpochStats(*m)
+
+    def capture(self) -> None:
+        self.rt.capture(self.stream.cuda_stream)
+
+    def step(self, B: Optional[int] = None, use_graph: bool = True) -> None:
+        B = self.batch if B is None else B
+        if use_graph and B == self.batch:
+            if not self.rt.captured:
+                self.capture()
+            self.rt.replay(self.stream.cuda_stream)
+        else:
+            self.rt.train_step(B, self.stream.cuda_stream)
+
+    def train_epoch(self, indices: torch.Tensor, use_graph: bool = True, progress=None) -> EpochStats:
+        self.set_epoch_indices(indices)
+        self.reset_metrics()
+        n = indices.numel()
+        nfull, last = divmod(n, self.batch)
+        for i in range(nfull):
+            self.step(self.batch, use_graph)
+            if progress is not None:
+                progress(i)
+        if last:
+            self.step(last, use_graph=False)
+        return self.read_metrics("train")
+
+    def evaluate(self, images: torch.Tensor, labels: torch.Tensor, indices: torch.Tensor) -> EpochStats:
+        """Forward-only loss/accuracy over ``indices`` (device int32) of (images, labels)."""
+        with torch.cuda.stream(self.stream):
+            self.eval_metrics.zero_()
+        idx = indices.to(self.device, torch.int32).contiguous()
+        imgs = images.to(self.device, torch.uint8).contiguous()
+        labs = labels.to(self.device, torch.uint8).contiguous()
+        n = idx.numel()
+        for s in range(0, n, self.batch):
+            b = min(self.batch, n - s)
+            self.rt.eval_batch(imgs.data_ptr(), labs.data_ptr(), idx.data_ptr() + 4 * s, b,
+                               self.eval_metrics.data_ptr(), self.stream.cuda_stream)
+        self._keep = (imgs, labs, idx)
+        return self.read_metrics("eval")
+
+    # ------------------------------------------------------------------ phases (tests / torch comm)
+    def forward_backward(self, B: Optional[int] = None) -> None:
+        B = self.batch if B is None else B
+        self.rt.forward_backward(B, self.stream.cuda_stream)
+        self.rt.reduce_grads(B, self.stream.cuda_stream)
+
+    def optimizer_step(self, gscale: float = 1.0) -> None:
+        self.rt.optimizer_step(float(gscale), self.stream.cuda_stream)
+
+    def grads(self) -> torch.Tensor:
+        self.stream.synchronize()
+        return self.grad.detach().cpu().clone()
+
+    def synchronize(self) -> None:
+        self.stream.synchronize()

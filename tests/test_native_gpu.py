@@ -1,0 +1,182 @@
+"""Native HIP kernels vs a plain PyTorch fp32 reference of the same op (survey §4 tiers T2/T3).
+
+Every test runs the native trainer on one MI355X and compares against torch autograd on the CPU
+with identical weights and batch order.  Dropout is disabled (p=0) where bit-level comparisons
+are made; dropout statistics are tested separately.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from pytorch_ddp_mnist_amd.models import build_model, flatten_grads, flatten_state
+
+pytestmark = pytest.mark.gpu
+
+
+def _normalize(x_u8):
+    return (torch.from_numpy(x_u8).float() / 255.0 - 0.1307) / 0.3081
+
+
+def torch_grads(model_name, module, x_u8, y_u8):
+    m = copy.deepcopy(module).float()
+    m.zero_grad()
+    x = _normalize(x_u8)
+    x = x.view(len(x), -1) if model_name == "mlp" else x.view(len(x), 1, 28, 28)
+    out = m(x)
+    y = torch.from_numpy(y_u8.astype(np.int64))
+    loss = F.nll_loss(out, y) if model_name == "lenet5" else F.cross_entropy(out, y)
+    loss.backward()
+    pred = out.argmax(1)
+    return flatten_grads(m), float(loss) * len(y), int((pred == y).sum())
+
+
+def make_trainer(model_name, dtype, batch, x, y, module, dropout=0.0, **kw):
+    from pytorch_ddp_mnist_amd.engine.native import NativeTrainer
+    return NativeTrainer(model_name, dtype, batch, torch.from_numpy(x.reshape(-1, 784)), torch.from_numpy(y),
+                         dropout=dropout, init=module, **kw)
+
+
+def rel_err(a, b):
+    return float((a - b).norm() / (b.norm() + 1e-12))
+
+
+@pytest.mark.parametrize("model_name", ["mlp", "lenet5"])
+@pytest.mark.parametrize("dtype,tol", [("fp32", 2e-4), ("bf16", 3e-2)])
+@pytest.mark.parametrize("batch", [128, 96, 16])
+def test_grads_match_torch(native, small_mnist, model_name, dtype, tol, batch):
+    x, y, _, _ = small_mnist
+    torch.manual_seed(0)
+    module = build_model(model_name)
+    tr = make_trainer(model_name, dtype, 128, x, y, module)
+    idx = torch.arange(batch, dtype=torch.int32) * 3 % len(y)
+    tr.set_epoch_indices(idx)
+    tr.reset_metrics()
+    tr.forward_backward(batch)
+    g = tr.grads()
+    gref, loss_sum, correct = torch_grads(model_name, module, x[idx.numpy()], y[idx.numpy()])
+    assert g.shape == gref.shape
+    e = rel_err(g, gref)
+    assert e < tol, f"{model_name}/{dtype}/B={batch}: grad rel err {e}"
+    # per-layer check so a single wrong small tensor cannot hide in the norm
+    off = 0
+    for k, v in module.state_dict().items():
+        n = v.numel()
+        le = rel_err(g[off:off + n], gref[off:off + n])
+        assert le < 5 * tol, f"{k}: rel err {le}"
+        off += n
+    st = tr.read_metrics()
+    assert st.count == batch
+    assert abs(st.loss_sum - loss_sum) / loss_sum < max(tol, 1e-4) * 10
+    assert abs(st.correct - correct) <= max(1, batch // 50)
+
+
+@pytest.mark.parametrize("model_name", ["mlp", "lenet5"])
+def test_sgd_step_matches_torch(native, small_mnist, model_name):
+    x, y, _, _ = small_mnist
+    torch.manual_seed(1)
+    module = build_model(model_name)
+    tr = make_trainer(model_name, "fp32", 64, x, y, module, momentum=0.9, lr=0.05)
+    ref = copy.deepcopy(module)
+    opt = torch.optim.SGD(ref.parameters(), lr=0.05, momentum=0.9)
+    idx = torch.randperm(len(y), generator=torch.Generator().manual_seed(3))[:64 * 5].to(torch.int32)
+    tr.set_epoch_indices(idx)
+    for s in range(5):
+        tr.step(64, use_graph=False)
+        b = idx[s * 64:(s + 1) * 64].numpy()
+        opt.zero_grad()
+        xb = _normalize(x[b])
+        xb = xb.view(64, -1) if model_name == "mlp" else xb.view(64, 1, 28, 28)
+        out = ref(xb)
+        yb = torch.from_numpy(y[b].astype(np.int64))
+        (F.nll_loss(out, yb) if model_name == "lenet5" else F.cross_entropy(out, yb)).backward()
+        opt.step()
+    tr.synchronize()
+    e = rel_err(tr.params.cpu(), flatten_state(ref))
+    assert e < 1e-5, e
+
+
+@pytest.mark.parametrize("model_name,dtype", [("mlp", "fp32"), ("mlp", "bf16"), ("lenet5", "fp32"), ("lenet5", "bf16")])
+def test_graph_replay_equals_eager(native, small_mnist, model_name, dtype):
+    x, y, _, _ = small_mnist
+    torch.manual_seed(2)
+    module = build_model(model_name)
+    idx = torch.randperm(len(y), generator=torch.Generator().manual_seed(5))[:128 * 4].to(torch.int32)
+    res = []
+    for use_graph in (False, True):
+        tr = make_trainer(model_name, dtype, 128, x, y, module, dropout=0.2)
+        tr.set_epoch_indices(idx)
+        for _ in range(4):
+            tr.step(128, use_graph=use_graph)
+        tr.synchronize()
+        res.append(tr.params.cpu().clone())
+    assert torch.equal(res[0], res[1]), "hipGraph replay must be bitwise identical to eager launches"
+
+
+def test_determinism(native, small_mnist):
+    x, y, _, _ = small_mnist
+    module = build_model("lenet5")
+    idx = torch.arange(256, dtype=torch.int32)
+    out = []
+    for _ in range(2):
+        tr = make_trainer("lenet5", "bf16", 128, x, y, module)
+        tr.set_epoch_indices(idx)
+        tr.step(128, use_graph=False)
+        tr.step(128, use_graph=False)
+        tr.synchronize()
+        out.append(tr.params.cpu().clone())
+    assert torch.equal(out[0], out[1]), "fixed-order slab reductions must make steps bitwise reproducible"
+
+
+@pytest.mark.parametrize("model_name,dtype", [("mlp", "fp32"), ("lenet5", "bf16")])
+def test_training_learns(native, small_mnist, model_name, dtype):
+    x, y, xt, yt = small_mnist
+    torch.manual_seed(3)
+    tr = make_trainer(model_name, dtype, 128, x, y, build_model(model_name), lr=0.05, momentum=0.9)
+    g = torch.Generator().manual_seed(0)
+    for ep in range(3):
+        st = tr.train_epoch(torch.randperm(len(y), generator=g).to(torch.int32))
+    ev = tr.evaluate(torch.from_numpy(xt.reshape(-1, 784)), torch.from_numpy(yt),
+                     torch.arange(len(yt), dtype=torch.int32))
+    assert ev.count == len(yt)
+    assert ev.accuracy > 0.9, (st, ev)
+
+
+def test_eval_matches_torch(native, small_mnist):
+    x, y, xt, yt = small_mnist
+    torch.manual_seed(4)
+    module = build_model("lenet5")
+    tr = make_trainer("lenet5", "fp32", 128, x, y, module)
+    ev = tr.evaluate(torch.from_numpy(xt.reshape(-1, 784)), torch.from_numpy(yt), torch.arange(300, dtype=torch.int32))
+    with torch.no_grad():
+        out = module(_normalize(xt[:300]).view(300, 1, 28, 28))
+        yy = torch.from_numpy(yt[:300].astype(np.int64))
+        loss = F.nll_loss(out, yy, reduction="sum").item()
+        corr = int((out.argmax(1) == yy).sum())
+    assert abs(ev.loss_sum - loss) / loss < 1e-4
+    assert ev.correct == corr
+
+
+def test_dropout_statistics(native, small_mnist):
+    """Native dropout keeps ~80% of units and scales by 1/(1-p): E[grad] matches p=0 on average."""
+    x, y, _, _ = small_mnist
+    torch.manual_seed(5)
+    module = build_model("mlp")
+    tr = make_trainer("mlp", "fp32", 512, x, y, module, dropout=0.2)
+    tr.set_epoch_indices(torch.arange(512, dtype=torch.int32))
+    tr.forward_backward(512)
+    tr.synchronize()
+    h1 = tr.h1T[:128, :512].float().cpu()
+    # units with positive pre-activation: fraction zeroed by dropout ~ 0.2
+    tr2 = make_trainer("mlp", "fp32", 512, x, y, module, dropout=0.0)
+    tr2.set_epoch_indices(torch.arange(512, dtype=torch.int32))
+    tr2.forward_backward(512)
+    tr2.synchronize()
+    h0 = tr2.h1T[:128, :512].float().cpu()
+    pos = h0 > 0
+    kept = (h1[pos] > 0).float().mean().item()
+    assert 0.77 < kept < 0.83, kept
+    ratio = (h1[pos & (h1 > 0)] / h0[pos & (h1 > 0)])
+    assert torch.allclose(ratio, torch.full_like(ratio, 1.25), rtol=1e-5)
