@@ -1,0 +1,175 @@
+#!/usr/bin/env python3
+"""Headline benchmark: whole-node training images/sec of LeNet-5 MNIST DDP on MI355X (+ top-1).
+
+Metric/config from BASELINE.json: "images/sec (whole node) MNIST ConvNet DDP at 1/2/4/8 MI355X;
+top-1 acc", config "LeNet-5 MNIST DDP 8xMI355X large-batch 8192/GPU bf16".  Weak scaling:
+8192 images per GPU per step, global batch = 8192 * N.
+
+Each timed step is a COMPLETE data-parallel training step through the native path: gather +
+normalise of the step's samples from the HBM-resident uint8 dataset, LeNet-5 forward and
+backward (hand-written CDNA4 MFMA kernels, bf16 inputs / fp32 accumulate / fp32 master
+weights), the gradient all-reduce (native RCCL communicator, two buckets overlapped with the
+convolution backward) and the SGD-momentum update, replayed as one hipGraph per step.
+Epoch boundaries inside the timed region (new DistributedSampler permutation upload) are
+included.  Data: synthetic 28x28 uint8 images of the MNIST shape (no network), random init.
+
+Launch: ``python bench.py`` (1 GPU) or
+``python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
+--master-port P bench.py --gpus N --steps K --warmup W``.  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--model", default="lenet5", choices=["lenet5", "mlp"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--batch", type=int, default=8192, help="per-GPU batch")
+    ap.add_argument("--lr", type=float, default=0.05)
+    ap.add_argument("--momentum", type=float, default=0.9)
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "torch"])
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--eval", action="store_true", default=True)
+    ap.add_argument("--no-eval", dest="eval", action="store_false")
+    ap.add_argument("--json-out", default=None)
+    return ap.parse_args()
+
+
+def main() -> int:
+    a = parse()
+    import numpy as np
+    import torch
+
+    from pytorch_ddp_mnist_amd.data.sampler import epoch_indices, num_samples
+    from pytorch_ddp_mnist_amd.data.synthetic import make_split
+    from pytorch_ddp_mnist_amd.engine.native import NativeTrainer
+    from pytorch_ddp_mnist_amd.models import build_model
+    from pytorch_ddp_mnist_amd.parallel.comm import init_distributed
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    ctx = init_distributed(None, parallel=world_env > 1, device="cuda", comm=a.comm)
+    if ctx.world != a.gpus and ctx.rank == 0:
+        print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={ctx.world}; using {ctx.world}", file=sys.stderr)
+    W, rank, dev = ctx.world, ctx.rank, ctx.device
+
+    # ---- data: MNIST-shaped synthetic set; repeated so every rank has >= 8 full batches per epoch
+    base_x, base_y = make_split(60000, seed=1)
+    reps = max(1, -(-(W * a.batch * 8) // 60000))
+    N = 60000 * reps
+    images = torch.from_numpy(base_x.reshape(-1, 784)).to(dev).repeat(reps, 1)
+    labels = torch.from_numpy(base_y).to(dev).repeat(reps)
+    test_x, test_y = make_split(10000, seed=2)
+
+    torch.manual_seed(0)
+    tr = NativeTrainer(a.model, a.dtype, a.batch, images, labels, device=dev, lr=a.lr, momentum=a.momentum,
+                       dropout=0.0, init=build_model(a.model), max_indices=num_samples(N, W))
+    if W > 1:
+        if a.comm == "rccl":
+            tr.attach_comm(ctx.rccl, W, overlap=not a.no_overlap)
+            tr.broadcast_params(0)
+        else:
+            import torch.distributed as dist
+            dist.broadcast(tr.params, 0)
+            tr.load_flat(tr.params.clone())
+
+    ns = num_samples(N, W)
+    steps_per_epoch = ns // a.batch
+    total = a.warmup + a.steps
+    n_epochs = -(-total // steps_per_epoch)
+    # DistributedSampler(seed=42) permutations, pinned, prepared before timing
+    perms = [epoch_indices(N, W, rank, e, seed=42).to(torch.int32).pin_memory() for e in range(n_epochs)]
+
+    use_graph = not a.no_graph and a.comm == "rccl"
+    state = {"epoch": -1, "in_epoch": steps_per_epoch}
+
+    def one_step():
+        if state["in_epoch"] >= steps_per_epoch:
+            state["epoch"] += 1
+            state["in_epoch"] = 0
+            tr.set_epoch_indices(perms[state["epoch"]])
+        if a.comm == "rccl" or W == 1:
+            tr.step(a.batch, use_graph=use_graph)
+        else:
+            import torch.distributed as dist
+            tr.forward_backward(a.batch)
+            with torch.cuda.stream(tr.stream):
+                dist.all_reduce(tr.grad)
+            tr.optimizer_step(1.0 / W)
+        state["in_epoch"] += 1
+
+    tr.reset_metrics()
+    for _ in range(a.warmup):
+        one_step()
+    tr.synchronize()
+    ctx.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        one_step()
+    tr.synchronize()
+    torch.cuda.synchronize(dev)
+    ctx.barrier()
+    t1 = time.perf_counter()
+    elapsed = ctx.all_reduce_max(t1 - t0)
+    train = tr.read_metrics()
+
+    top1 = None
+    if a.eval:
+        ev = tr.evaluate(torch.from_numpy(test_x.reshape(-1, 784)), torch.from_numpy(test_y),
+                         torch.arange(10000, dtype=torch.int32))
+        top1 = ev.accuracy
+
+    ms = elapsed / a.steps * 1e3
+    value = W * a.batch * a.steps / elapsed
+    out = {
+        "metric": "images/sec (whole node) MNIST ConvNet DDP at 1/2/4/8 MI355X; top-1 acc",
+        "value": round(value, 1),
+        "unit": "images/s",
+        "n_gpus": W,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": a.dtype,
+        "data": "synthetic (MNIST-shaped 28x28 uint8, class-template + noise; random-init weights)",
+        "config": {
+            "model": "LeNet-5" if a.model == "lenet5" else "MLP-784-128-128-10",
+            "global_batch": W * a.batch,
+            "per_gpu_batch": a.batch,
+            "seq_len": None,
+            "image_shape": [1, 28, 28],
+            "parallelism": f"dp{W}",
+            "optimizer": f"SGD(lr={a.lr}, momentum={a.momentum})",
+            "comm": "native RCCL, 2 buckets overlapped with conv backward" if a.comm == "rccl" else "c10d nccl",
+            "hipgraph": use_graph,
+        },
+        "top1": None if top1 is None else round(top1, 4),
+        "train_loss_mean": round(train.mean_loss, 4),
+    }
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                f.write(line + "\n")
+    ctx.finalize()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -138,6 +138,7 @@ __global__ __launch_bounds__(256) void head_kernel(BatchRef br, HeadBuffers hb) 
       for (int m = 0; m < MT; ++m) acc[m] = zero4();
       const T* bp = pack + H::F1 + (nt * 16 + row) * H::K0P + grp * KV;
       const T* ap = sX + row * S::PX + grp * KV;
+#pragma unroll
       for (int kc = 0; kc < KCH; ++kc) {
         const Frag b = M::load(bp + kc * KC);
 #pragma unroll
@@ -177,6 +178,7 @@ __global__ __launch_bounds__(256) void head_kernel(BatchRef br, HeadBuffers hb) 
       for (int m = 0; m < MT; ++m) acc[m] = zero4();
       const T* bp = pack + H::F2 + (nt * 16 + row) * H::N1P + grp * KV;
       const T* ap = sH1 + row * S::P1 + grp * KV;
+#pragma unroll
       for (int kc = 0; kc < KCH; ++kc) {
         const Frag b = M::load(bp + kc * KC);
 #pragma unroll
@@ -310,6 +312,7 @@ __global__ __launch_bounds__(256) void head_kernel(BatchRef br, HeadBuffers hb) 
       for (int m = 0; m < MT; ++m) acc[m] = zero4();
       const T* bp = pack + H::F2T + (nt * 16 + row) * H::N2P + grp * KV;
       const T* ap = sH2 + row * S::P2 + grp * KV;
+#pragma unroll
       for (int kc = 0; kc < KCH; ++kc) {
         const Frag b = M::load(bp + kc * KC);
 #pragma unroll
@@ -343,6 +346,7 @@ __global__ __launch_bounds__(256) void head_kernel(BatchRef br, HeadBuffers hb) 
       for (int m = 0; m < MT; ++m) acc[m] = zero4();
       const T* bp = pack + H::F1T + (nt * 16 + row) * H::N1P + grp * KV;
       const T* ap = sH1 + row * S::P1 + grp * KV;
+#pragma unroll
       for (int kc = 0; kc < KCH; ++kc) {
         const Frag b = M::load(bp + kc * KC);
 #pragma unroll
@@ -417,13 +421,24 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
   const int sel0 = kk0 < J.K ? 0 : (kk0 == J.K && J.bias ? 1 : 2);
   const int sel1 = kk1 < J.K ? 0 : (kk1 == J.K && J.bias ? 1 : 2);
 
+  // software pipeline: the next K-chunk's four fragments are in flight while this one computes
+  Frag na0, na1, nb0, nb1;
+  if (rs < re) {
+    na0 = M::load(ap0 + rs);
+    na1 = nv1 ? M::load(ap1 + rs) : zf;
+    nb0 = M::load(bp0 + rs);
+    nb1 = M::load(bp1 + rs);
+  }
   for (int rc = rs; rc < re; rc += KC) {
-    const Frag a0 = M::load(ap0 + rc);
-    const Frag a1 = nv1 ? M::load(ap1 + rc) : zf;
-    const Frag bl0 = M::load(bp0 + rc);
-    const Frag bl1 = M::load(bp1 + rc);
-    const Frag b0 = sel0 == 0 ? bl0 : (sel0 == 1 ? ones : zf);
-    const Frag b1 = sel1 == 0 ? bl1 : (sel1 == 1 ? ones : zf);
+    const Frag a0 = na0, a1 = na1;
+    const Frag b0 = sel0 == 0 ? nb0 : (sel0 == 1 ? ones : zf);
+    const Frag b1 = sel1 == 0 ? nb1 : (sel1 == 1 ? ones : zf);
+    if (rc + KC < re) {
+      na0 = M::load(ap0 + rc + KC);
+      na1 = nv1 ? M::load(ap1 + rc + KC) : zf;
+      nb0 = M::load(bp0 + rc + KC);
+      nb1 = M::load(bp1 + rc + KC);
+    }
     M::mma(acc[0][0], a0, b0);
     M::mma(acc[0][1], a0, b1);
     M::mma(acc[1][0], a1, b0);
@@ -502,7 +517,7 @@ int head_rows_per_block(ModelKind m, DType t, int B) {
   if (B <= 256) return 16;
   if (t == DType::F32) return 32;
   if (m == ModelKind::MLP) return B >= 4096 ? 64 : 32;
-  return B >= 2048 ? 64 : 32;
+  return 32;  // 256+ workgroups at B=8192: one wave per SIMD chip-wide instead of half the SIMDs idle
 }
 
 void launch_head(ModelKind m, DType t, bool train, const BatchRef& br, const HeadBuffers& hb, int rows,

@@ -30,29 +30,31 @@ using L = LenetModel;
 constexpr int K0P = L::Head::K0P;  // 416
 
 template <typename T>
+DEV void zero_lds(T* p, int n) {
+  for (int e = threadIdx.x; e < n; e += blockDim.x) p[e] = to_t<T>(0.f);
+}
+
+// MFMA fragment of KV ones (bias-gradient column) / zeros
+template <typename T>
+DEV typename Mma<T>::Frag ones_frag() {
+  typename Mma<T>::Frag f;
+#pragma unroll
+  for (int j = 0; j < Mma<T>::KV; ++j) Mma<T>::set(f, j, 1.f);
+  return f;
+}
+
+// ====================================================================================
+// forward
+// LDS: xs8[s][y][x] = xpad[y][x+s] for s = 0..7 (8 shifted copies of the zero-padded 32x32
+// input) so that any run of KV consecutive taps of one kernel row, starting at any column, is
+// an ALIGNED 16-byte read: conv1's im2col A fragment with k = kh*8 + kw is one ds_read_b128.
+template <typename T>
 struct FwdSmem {
-  static constexpr int OFF_X = 0;                                  // [32][32] padded input
-  static constexpr int OFF_P1 = rup(32 * 32 * (int)sizeof(T), 16);  // [196][8]
+  static constexpr int XP = 1048;  // plane pitch (32x32 + pad): 2-way worst-case conflicts (was 8-way at 1024)
+  static constexpr int OFF_XS = 0;                                        // [8][XP] T
+  static constexpr int OFF_P1 = rup(8 * XP * (int)sizeof(T), 16);         // [196][8] T
   static constexpr int TOTAL = rup(OFF_P1 + 196 * 8 * (int)sizeof(T), 16);
 };
-
-// Stage dataset image `s` normalised into the zero-padded 32x32 LDS tile (cooperative).
-template <typename T>
-DEV void stage_image(T* xpad, const uint8_t* images, int s, bool valid) {
-  for (int e = threadIdx.x; e < 32 * 32; e += blockDim.x) xpad[e] = to_t<T>(0.f);
-  __syncthreads();
-  if (valid) {
-    const uint8_t* img = images + (size_t)s * 784;
-    for (int e = threadIdx.x; e < 196; e += blockDim.x) {  // 196 x 4 pixels
-      const uint32_t u = *reinterpret_cast<const uint32_t*>(img + e * 4);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = e * 4 + j, y = k / 28, x = k % 28;
-        xpad[(y + 2) * 32 + x + 2] = to_t<T>(mnist_norm((u >> (8 * j)) & 255u));
-      }
-    }
-  }
-}
 
 template <typename T, bool TRAIN>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
@@ -61,51 +63,56 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(BatchRef br, LenetConvBuf
   using S = FwdSmem<T>;
   constexpr int KV = M::KV, KC = M::KC;
   __shared__ __attribute__((aligned(16))) char smem[S::TOTAL];
-  T* xpad = reinterpret_cast<T*>(smem + S::OFF_X);
+  T* xs = reinterpret_cast<T*>(smem + S::OFF_XS);
   T* p1s = reinterpret_cast<T*>(smem + S::OFF_P1);
-  const int lane = threadIdx.x & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
   const int32_t* idx = br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride;
   const T* pack = reinterpret_cast<const T*>(cb.pack);
   const float* prm = cb.params;
 
-  // ---- per-lane constants: conv1 B fragments + tap offsets, conv2 B fragments
-  constexpr int C1CH = 32 / KC;          // conv1 K = 32 (25 taps + pad)
+  constexpr int C1CH = 64 / KC;                 // conv1 K = 5 rows x 8 (kw padded)
   constexpr int C2CH = (25 * 8 + KC - 1) / KC;  // conv2 K = 25 taps x 8 ch (7 bf16 / 13 f32 chunks)
-  Frag b1[C1CH];
-  int koff1[C1CH][KV];
+  Frag b1[C1CH], b2[C2CH];
 #pragma unroll
-  for (int kc = 0; kc < C1CH; ++kc) {
-    b1[kc] = M::load(pack + L::C1 + row * 32 + kc * KC + grp * KV);
-#pragma unroll
-    for (int j = 0; j < KV; ++j) {
-      const int k = kc * KC + grp * KV + j;
-      koff1[kc][j] = k < 25 ? (k / 5) * 32 + (k % 5) : 0;
-    }
-  }
-  Frag b2[C2CH];
+  for (int kc = 0; kc < C1CH; ++kc) b1[kc] = M::load(pack + L::C1 + row * 64 + kc * KC + grp * KV);
 #pragma unroll
   for (int kc = 0; kc < C2CH; ++kc) b2[kc] = M::load(pack + L::C2F + row * 224 + kc * KC + grp * KV);
   const float bias1 = row < 6 ? prm[L::CB1 + row] : 0.f;
   const float bias2 = prm[L::CB2 + row];
 
+  zero_lds<T>(xs, 8 * S::XP);
+  __syncthreads();
   for (int t = 0; t < ipb; ++t) {
     const int b = blockIdx.x * ipb + t;
     const bool valid = b < br.B;
-    stage_image<T>(xpad, br.images, valid ? idx[b] : 0, valid);
+    // ---- stage: gather + normalise, scattered into the 8 shifted copies
+    if (tid < 196) {
+      uint32_t u = 0;
+      if (valid) u = *reinterpret_cast<const uint32_t*>(br.images + (size_t)idx[b] * 784 + tid * 4);
+      const int k = tid * 4, y = k / 28 + 2, x = k % 28 + 2;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const T v = to_t<T>(valid ? mnist_norm((u >> (8 * j)) & 255u) : 0.f);
+#pragma unroll
+        for (int s8 = 0; s8 < 8; ++s8) {
+          const int xx = x + j - s8;
+          if (xx >= 0) xs[s8 * S::XP + y * 32 + xx] = v;
+        }
+      }
+    }
     __syncthreads();
 
     // ---- conv1 + bias + ReLU + maxpool: 49 M-tiles (4 pooled outputs x 4 window elems each)
     for (int mt = w; mt < 49; mt += 4) {
       const int q = row >> 2, e = row & 3;
       const int p = mt * 4 + q, py = p / 14, px = p % 14;
-      const int base = (2 * py + (e >> 1)) * 32 + 2 * px + (e & 1);
+      const int oh = 2 * py + (e >> 1), ow = 2 * px + (e & 1);
       f32x4 acc = zero4();
 #pragma unroll
       for (int kc = 0; kc < C1CH; ++kc) {
-        Frag a;
-#pragma unroll
-        for (int j = 0; j < KV; ++j) M::set(a, j, to_f(xpad[base + koff1[kc][j]]));
-        M::mma(acc, a, b1[kc]);
+        const int k0 = kc * KC + grp * KV;
+        const int kh = min(k0 >> 3, 4), x = ow + (k0 & 7);
+        M::mma(acc, M::load(xs + (x & 7) * S::XP + (oh + kh) * 32 + (x & ~7)), b1[kc]);
       }
       // lane: channel n = row, pooled position pp = mt*4 + grp, window elems in acc[0..3]
       const int n = row, pp = mt * 4 + grp;
@@ -160,16 +167,33 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(BatchRef br, LenetConvBuf
 }
 
 // ====================================================================================
+// backward
+// LDS images chosen so that every MFMA operand fragment is ONE aligned 16-byte read:
+//   XS  [5][32][32]     xs[kw][y][x]  = xpad[y][x+kw]          conv1 wgrad B (im2col^T rows)
+//   P1T [5][6][14][16]  p1t[kw][c][y][x] = pool1[y][x+kw][c]   conv2 wgrad B
+//   DY2T[16][10*16]     conv2 pre-act grad, channel-major, rows padded 10->16   conv2 wgrad A
+//   DYS [18][18][16]    same grad, position-major (NHWC), zero border of 4 so the full-correlation
+//                       dgrad reads it without bounds checks                     conv2 dgrad A
+//   W2  [16][424]       packed conv2 dgrad operand (C2d)                         conv2 dgrad B
+//   DY1T[8][28*32]      conv1 pre-act grad, channel-major, rows padded 28->32    conv1 wgrad A
+// The pool1 un-pooling (argmax + ReLU) is fused into the conv2-dgrad epilogue, which writes DY1T
+// directly; pool2 un-pooling is a cooperative scatter.  Both scatters write every position of
+// their map (2x2 windows tile it), so nothing but the padding is ever zero-filled.
 template <typename T>
 struct BwdSmem {
-  static constexpr int OFF_X = 0;                                        // [32][32] T
-  static constexpr int OFF_P1 = rup(OFF_X + 32 * 32 * (int)sizeof(T), 16);  // [196][8] T
-  static constexpr int OFF_M1 = rup(OFF_P1 + 196 * 8 * (int)sizeof(T), 16); // [196][8] u8
-  static constexpr int OFF_DY = rup(OFF_M1 + 196 * 8, 16);                 // [100][16] T
-  static constexpr int OFF_DYT = rup(OFF_DY + 100 * 16 * (int)sizeof(T), 16);  // [16][128] T
-  static constexpr int OFF_DP1 = rup(OFF_DYT + 16 * 128 * (int)sizeof(T), 16); // [196][8] f32
-  static constexpr int OFF_RED = rup(OFF_DP1 + 196 * 8 * 4, 16);           // [4][2][256] f32
-  static constexpr int TOTAL = rup(OFF_RED + 4 * 2 * 256 * 4, 16);
+  // pitches padded so the fragment reads and the un-pooling scatters are <= 2-way bank
+  // conflicted (measured 60% conflict cycles with the unpadded 1024/224/160/896 pitches)
+  static constexpr int W2P = 424, XP = 1048, P1P = 240, D2P = 176, D1P = 912;
+  static constexpr int OFF_XS = 0;
+  static constexpr int OFF_P1T = rup(OFF_XS + 5 * XP * (int)sizeof(T), 16);
+  static constexpr int OFF_DY2T = rup(OFF_P1T + 5 * 6 * P1P * (int)sizeof(T), 16);
+  static constexpr int OFF_DYS = rup(OFF_DY2T + 16 * D2P * (int)sizeof(T), 16);   // [18][18][16] zero-padded
+  static constexpr int OFF_W2 = rup(OFF_DYS + 18 * 18 * 16 * (int)sizeof(T), 16);
+  static constexpr int OFF_DY1T = rup(OFF_W2 + 16 * W2P * (int)sizeof(T), 16);
+  static constexpr int OFF_M1 = rup(OFF_DY1T + 8 * D1P * (int)sizeof(T), 16);
+  static constexpr int TOTAL = rup(OFF_M1 + 196 * 8, 16);
+  static constexpr int OFF_RED = OFF_XS;  // [4][2][256] f32 scratch after the image loop
+  static_assert(4 * 2 * 256 * 4 <= OFF_P1T, "reduction scratch must fit in the aliased XS region");
 };
 
 template <typename T>
@@ -179,138 +203,186 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   using S = BwdSmem<T>;
   constexpr int KV = M::KV, KC = M::KC;
   __shared__ __attribute__((aligned(16))) char smem[S::TOTAL];
-  T* xpad = reinterpret_cast<T*>(smem + S::OFF_X);
-  T* p1s = reinterpret_cast<T*>(smem + S::OFF_P1);
+  T* xs = reinterpret_cast<T*>(smem + S::OFF_XS);
+  T* p1t = reinterpret_cast<T*>(smem + S::OFF_P1T);
+  T* dy2t = reinterpret_cast<T*>(smem + S::OFF_DY2T);
+  T* dys = reinterpret_cast<T*>(smem + S::OFF_DYS);
+  T* w2 = reinterpret_cast<T*>(smem + S::OFF_W2);
+  T* dy1t = reinterpret_cast<T*>(smem + S::OFF_DY1T);
   uint8_t* m1s = reinterpret_cast<uint8_t*>(smem + S::OFF_M1);
-  T* dys = reinterpret_cast<T*>(smem + S::OFF_DY);
-  T* dyT = reinterpret_cast<T*>(smem + S::OFF_DYT);
-  float* dp1 = reinterpret_cast<float*>(smem + S::OFF_DP1);
   float* red = reinterpret_cast<float*>(smem + S::OFF_RED);
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
   const int32_t* idx = br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride;
   const T* pack = reinterpret_cast<const T*>(cb.pack);
   const T* dp2 = reinterpret_cast<const T*>(cb.dp2);
+  const T* p1g = reinterpret_cast<const T*>(cb.p1);
 
-  constexpr int W2CH = 128 / KC;              // conv2 wgrad reduction over 100 (->128) positions
+  constexpr int W2CH = 160 / KC;              // conv2 wgrad: 10 rows x 16 positions
   constexpr int D2CH = (400 + KC - 1) / KC;   // conv2 dgrad K = 25 taps x 16 ch (13 bf16 / 25 f32)
-  constexpr int W1CH = (784 + KC - 1) / KC;   // conv1 wgrad over 784 positions (25 bf16 / 49 f32)
+  constexpr int W1CH = 896 / KC;              // conv1 wgrad: 28 rows x 32 positions (28 bf16 / 56 f32)
 
-  f32x4 accW2[4];   // conv2 wgrad tiles nt = w + 4*i (13 tiles over kcol = tap*8 + c, + bias col 200)
-  f32x4 accW1[2];   // conv1 wgrad partial (this wave's share of the positions), kcol = tap, bias col 25
+  // ---- once per workgroup: zero every padded image, stage C2d
+  zero_lds<T>(xs, 5 * S::XP);
+  zero_lds<T>(p1t, 5 * 6 * S::P1P);
+  zero_lds<T>(dy2t, 16 * S::D2P);
+  zero_lds<T>(dy1t, 8 * S::D1P);
+  zero_lds<T>(dys, 18 * 18 * 16);
+  {
+    constexpr int VE = 16 / (int)sizeof(T);
+    for (int e = tid; e < 16 * 416 / VE; e += 256) {
+      const int r = e / (416 / VE), c = (e % (416 / VE)) * VE;
+      *reinterpret_cast<uint4*>(w2 + r * S::W2P + c) = *reinterpret_cast<const uint4*>(pack + L::C2D + r * 416 + c);
+    }
+  }
+  // ---- static cost-balanced work split of phase B (dgrad tile = 13 K-chunks, wgrad tile = 5):
+  //      waves 0-2: 3 dgrad M-tiles + 4 wgrad N-tiles; wave 3: 4 dgrad + 1 wgrad (~59 chunks each)
+  const int nd = w == 3 ? 4 : 3, d0 = w * 3;          // dgrad tiles [d0, d0 + nd)
+  const int nw = w == 3 ? 1 : 4, n0w = w * 4;         // wgrad tiles [n0w, n0w + nw)
+  // ---- per-lane operand offsets (loop invariant)
+  int w2off[4];   // conv2 wgrad B: this wave's output tiles (kcol = tap*8 + c; 200 = bias)
+  int w2sel[4];   // 0 data, 1 ones (bias), 2 zero
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int kcol = (n0w + i) * 16 + row, tap = kcol >> 3, c = kcol & 7;
+    w2sel[i] = (kcol < 200 && c < 6) ? 0 : (kcol == 200 ? 1 : 2);
+    w2off[i] = w2sel[i] == 0 ? ((tap % 5) * 6 + c) * S::P1P + (tap / 5) * 16 : 0;
+  }
+  int w1off[2], w1sel[2];  // conv1 wgrad B: tiles over kcol = tap (25 = bias)
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    const int tap = nt * 16 + row;
+    w1sel[nt] = tap < 25 ? 0 : (tap == 25 ? 1 : 2);
+    w1off[nt] = tap < 25 ? (tap % 5) * S::XP + (tap / 5) * 32 : 0;
+  }
+  const Frag ones = ones_frag<T>(), zf = M::zero();
+  int doff[D2CH];  // conv2 dgrad A: -(tap row, col) shift of the lane's K-chunk inside the padded DYS
+#pragma unroll
+  for (int kc = 0; kc < D2CH; ++kc) {
+    int tap, n0;
+    if constexpr (KV == 8) { tap = kc * 2 + (grp >> 1); n0 = (grp & 1) * 8; }
+    else { tap = kc; n0 = grp * 4; }
+    doff[kc] = tap < 25 ? (-(tap / 5) * 18 - (tap % 5)) * 16 + n0 : -(1 << 20);
+  }
+
+  f32x4 accW2[4], accW1[2];
 #pragma unroll
   for (int i = 0; i < 4; ++i) accW2[i] = zero4();
   accW1[0] = zero4();
   accW1[1] = zero4();
+  __syncthreads();
 
   for (int t = 0; t < ipb; ++t) {
     const int b = blockIdx.x * ipb + t;
     const bool valid = b < br.B;
-    stage_image<T>(xpad, br.images, valid ? idx[b] : 0, valid);
-    // pool1 activations + codes, zeroed grads
-    {
-      constexpr int P1V = 196 * 8 * (int)sizeof(T) / 16, M1V = 196 * 8 / 16;
-      const uint4* psrc = reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(cb.p1) + (size_t)b * 196 * 8);
-      const uint4* msrc = reinterpret_cast<const uint4*>(cb.m1 + (size_t)b * 196 * 8);
-      const uint4 z = make_uint4(0, 0, 0, 0);
-      for (int e = tid; e < P1V; e += 256) reinterpret_cast<uint4*>(p1s)[e] = valid ? psrc[e] : z;
-      for (int e = tid; e < M1V; e += 256) reinterpret_cast<uint4*>(m1s)[e] = valid ? msrc[e] : z;
-    }
-    for (int e = tid; e < 100 * 16; e += 256) dys[e] = to_t<T>(0.f);
-    for (int e = tid; e < 16 * 128; e += 256) dyT[e] = to_t<T>(0.f);
-    __syncthreads();
-    // ---- scatter pool2 grads through argmax + ReLU mask into conv2 pre-activation grads
-    if (valid) {
-      for (int e = tid; e < 400; e += 256) {
-        const int n = e / 25, p = e % 25;
-        const uint8_t code = cb.m2[(size_t)b * 400 + e];
-        if (code & 4) {
-          const int win = code & 3, py = p / 5, px = p % 5;
-          const int pos = (2 * py + (win >> 1)) * 10 + 2 * px + (win & 1);
-          const T g = dp2[(size_t)b * K0P + e];
-          dys[pos * 16 + n] = g;
-          dyT[n * 128 + pos] = g;
+    // ---- phase A: stage input (5 shifted copies), pool1 (5 shifted channel-major copies),
+    //      pool1 codes, and the pool2 un-pooling scatter into DYS / DY2T
+    if (tid < 196) {
+      uint32_t u = 0;
+      if (valid) u = *reinterpret_cast<const uint32_t*>(br.images + (size_t)idx[b] * 784 + tid * 4);
+      const int k = tid * 4, y = k / 28 + 2, x = k % 28 + 2;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const T v = to_t<T>(valid ? mnist_norm((u >> (8 * j)) & 255u) : 0.f);
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) {
+          const int xx = x + j - kw;
+          if (xx >= 0) xs[kw * S::XP + y * 32 + xx] = v;
         }
+      }
+      // pool1 position tid: 8 channels
+      T pv[8];
+      if (valid) {
+        if constexpr (sizeof(T) == 2) {
+          *reinterpret_cast<uint4*>(pv) = *reinterpret_cast<const uint4*>(p1g + ((size_t)b * 196 + tid) * 8);
+        } else {
+          *reinterpret_cast<uint4*>(pv) = *reinterpret_cast<const uint4*>(p1g + ((size_t)b * 196 + tid) * 8);
+          *reinterpret_cast<uint4*>(pv + 4) = *reinterpret_cast<const uint4*>(p1g + ((size_t)b * 196 + tid) * 8 + 4);
+        }
+        *reinterpret_cast<uint2*>(m1s + tid * 8) = *reinterpret_cast<const uint2*>(cb.m1 + ((size_t)b * 196 + tid) * 8);
+      } else {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) pv[c] = to_t<T>(0.f);
+        *reinterpret_cast<uint2*>(m1s + tid * 8) = make_uint2(0, 0);
+      }
+      const int py = tid / 14, px = tid % 14;
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw) {
+        const int xx = px - kw;
+        if (xx >= 0) {
+#pragma unroll
+          for (int c = 0; c < 6; ++c) p1t[(kw * 6 + c) * S::P1P + py * 16 + xx] = pv[c];
+        }
+      }
+    }
+    for (int e = tid; e < 400; e += 256) {
+      const int n = e & 15, p = e >> 4, py = p / 5, px = p % 5;  // channel fastest: conflict-free DYS writes
+      uint8_t code = 0;
+      float g = 0.f;
+      if (valid) {
+        code = cb.m2[(size_t)b * 400 + n * 25 + p];
+        g = to_f(dp2[(size_t)b * K0P + n * 25 + p]);
+      }
+#pragma unroll
+      for (int win = 0; win < 4; ++win) {
+        const int oh = 2 * py + (win >> 1), ow = 2 * px + (win & 1);
+        const T v = to_t<T>(((code & 4) && (code & 3) == win) ? g : 0.f);
+        dys[((oh + 4) * 18 + ow + 4) * 16 + n] = v;
+        dy2t[n * S::D2P + oh * 16 + ow] = v;
       }
     }
     __syncthreads();
 
-    // ---- conv2 wgrad: dW2[n][tap*8+c] += sum_m dY2[m][n] * im2col(p1)[m][tap*8+c]
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int nt = w + 4 * i;
-      if (nt >= 13) break;
-      const int kcol = nt * 16 + row;
-      const int tap = min(kcol >> 3, 24), c = kcol & 7;
-      const int toff = ((tap / 5) * 14 + tap % 5) * 8 + c;
-      const float sel = kcol < 200 ? 0.f : (kcol == 200 ? 1.f : -1.f);  // 0: data, 1: bias col, -1: zero
-      for (int kc = 0; kc < W2CH; ++kc) {
-        const Frag a = M::load(dyT + row * 128 + kc * KC + grp * KV);
-        Frag bf;
-#pragma unroll
-        for (int j = 0; j < KV; ++j) {
-          const int m = kc * KC + grp * KV + j;
-          const int mm = min(m, 99), oh = mm / 10, ow = mm % 10;
-          float x = to_f(p1s[(oh * 14 + ow) * 8 + toff]);
-          if (sel != 0.f) x = (sel > 0.f && m < 100) ? 1.f : 0.f;
-          M::set(bf, j, x);
-        }
-        M::mma(accW2[i], a, bf);
-      }
-    }
-
-    // ---- conv2 dgrad: dP1[q][c] = sum_{tap,n} dY2[q - tap][n] * W2[n][c][tap]
-    for (int mt = w; mt < 13; mt += 4) {
-      const int q = mt * 16 + row;
-      const int qy = q / 14, qx = q % 14;
-      f32x4 acc = zero4();
-      for (int kc = 0; kc < D2CH; ++kc) {
-        int tap, n0;
-        if constexpr (KV == 8) { tap = kc * 2 + (grp >> 1); n0 = (grp & 1) * 8; }
-        else { tap = kc; n0 = grp * 4; }
-        const int oy = qy - tap / 5, ox = qx - tap % 5;
-        Frag a = M::zero();
-        if (q < 196 && tap < 25 && oy >= 0 && oy < 10 && ox >= 0 && ox < 10) a = M::load(dys + (oy * 10 + ox) * 16 + n0);
-        M::mma(acc, a, M::load(pack + L::C2D + row * 416 + kc * KC + grp * KV));
-      }
-      const int c = row;
+    // ---- phase B1: conv2 wgrad  dW2[n][tap*8+c] += sum_pos dY2[pos][n] * pool1[pos + tap][c]
+    for (int kc = 0; kc < W2CH; ++kc) {
+      const int p0 = kc * KC + grp * KV, oh = p0 >> 4, ow0 = p0 & 15;
+      const Frag a = M::load(dy2t + row * S::D2P + p0);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int qq = mt * 16 + grp * 4 + i;
-        if (c < 8 && qq < 196) dp1[qq * 8 + c] = c < 6 ? acc[i] : 0.f;
+        if (i < nw) {
+          const Frag bf = w2sel[i] == 0 ? M::load(p1t + w2off[i] + oh * 16 + ow0) : (w2sel[i] == 1 ? ones : zf);
+          M::mma(accW2[i], a, bf);
+        }
+      }
+    }
+
+    // ---- phase B2: conv2 dgrad  dP1[q][c] = sum_{tap,n} dY2[q - tap][n] * W2[n][c][tap],
+    //      epilogue: pool1 un-pooling (argmax + ReLU) straight into DY1T
+    for (int mt = d0; mt < d0 + nd; ++mt) {
+      const int q = min(mt * 16 + row, 195);   // rows >= 196 are computed on a valid row and dropped
+      const int qy = q / 14, qx = q % 14;
+      const T* abase = dys + ((qy + 4) * 18 + qx + 4) * 16;
+      f32x4 acc = zero4();
+#pragma unroll
+      for (int kc = 0; kc < D2CH; ++kc) {
+        const Frag a = doff[kc] > -(1 << 19) ? M::load(abase + doff[kc]) : zf;
+        M::mma(acc, a, M::load(w2 + row * S::W2P + kc * KC + grp * KV));
+      }
+      const int c = row;
+      if (c < 6) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int qq = mt * 16 + grp * 4 + i;
+          if (qq < 196) {
+            const uint8_t code = m1s[qq * 8 + c];
+            const int y = qq / 14, x = qq % 14;
+            const float v = (code & 4) ? acc[i] : 0.f;
+            const int am = code & 3;
+#pragma unroll
+            for (int win = 0; win < 4; ++win)
+              dy1t[c * S::D1P + (2 * y + (win >> 1)) * 32 + 2 * x + (win & 1)] = to_t<T>(win == am ? v : 0.f);
+          }
+        }
       }
     }
     __syncthreads();
 
-    // ---- conv1 wgrad: dW1[n][tap] += sum_{m1} dY1[m1][n] * xpad-im2col[m1][tap]; m1 = pp*4 + e
+    // ---- phase C: conv1 wgrad  dW1[n][tap] += sum_pos dY1[pos][n] * xpad[pos + tap]
     for (int kc = w; kc < W1CH; kc += 4) {
-      Frag a;
-      const int n = row;
-#pragma unroll
-      for (int j = 0; j < KV; ++j) {
-        const int m1 = kc * KC + grp * KV + j;
-        const int pp = m1 >> 2, e = m1 & 3;
-        float v = 0.f;
-        if (n < 6 && pp < 196) {
-          const uint8_t code = m1s[pp * 8 + n];
-          if ((code & 4) && (code & 3) == e) v = dp1[pp * 8 + n];
-        }
-        M::set(a, j, v);
-      }
+      const int p0 = kc * KC + grp * KV, oh = p0 >> 5, ow0 = p0 & 31;
+      const Frag a = row < 8 ? M::load(dy1t + row * S::D1P + p0) : zf;
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
-        const int kcol = nt * 16 + row;
-        const int tap = min(kcol, 24);
-        const int toff = (tap / 5) * 32 + tap % 5;
-        Frag bf;
-#pragma unroll
-        for (int j = 0; j < KV; ++j) {
-          const int m1 = kc * KC + grp * KV + j;
-          const int pp = min(m1 >> 2, 195), e = m1 & 3;
-          const int base = (2 * (pp / 14) + (e >> 1)) * 32 + 2 * (pp % 14) + (e & 1);
-          float x = to_f(xpad[base + toff]);
-          if (kcol >= 25) x = (kcol == 25 && (m1 >> 2) < 196) ? 1.f : 0.f;
-          M::set(bf, j, x);
-        }
+        const Frag bf = w1sel[nt] == 0 ? M::load(xs + w1off[nt] + oh * 32 + ow0) : (w1sel[nt] == 1 ? ones : zf);
         M::mma(accW1[nt], a, bf);
       }
     }
@@ -321,9 +393,8 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   float* out = cb.slab + (size_t)blockIdx.x * L::CONV_PARAMS;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int nt = w + 4 * i;
-    if (nt >= 13) break;
-    const int kcol = nt * 16 + row;
+    if (i >= nw) break;
+    const int kcol = (n0w + i) * 16 + row;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = grp * 4 + r;
@@ -354,7 +425,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
 }  // namespace
 
 static int fwd_ipb(int B) { return std::max(1, (B + 1023) / 1024); }
-static int bwd_ipb(int B) { return std::max(1, (B + 255) / 256); }
+static int bwd_ipb(int B) { return std::max(1, (B + 1023) / 1024); }
 
 int lenet_conv_bwd_blocks(int B) {
   const int ipb = bwd_ipb(B);

@@ -14,7 +14,7 @@
 // operand layouts the kernels consume (zero padded to MFMA tile multiples):
 //   F*  [NP][KP]  forward  B operand (row n, contiguous k)
 //   F*t [KP][NP]  dgrad    B operand (row k_in, contiguous n_out)
-//   C1  [16][32]  conv1 B operand, k = kh*5+kw
+//   C1  [16][64]  conv1 B operand, k = kh*8 + kw (kw padded 5->8: one tap row = 8 contiguous k)
 //   C2f [16][224] conv2 forward B operand, k = (kh*5+kw)*8 + c   (channels padded 6->8)
 //   C2d [16][416] conv2 dgrad B operand, row = c, k' = (kh*5+kw)*16 + n
 // so every fragment fetch is one 16-byte vector load and no kernel converts or
@@ -53,8 +53,8 @@ struct MlpModel {
 
 struct LenetModel {
   static constexpr int CW1 = 0, CB1 = 150, CW2 = 156, CB2 = 2556;
-  static constexpr int C1 = 0;                 // [16][32]
-  static constexpr int C2F = C1 + 16 * 32;     // [16][224]
+  static constexpr int C1 = 0;                 // [16][64]
+  static constexpr int C2F = C1 + 16 * 64;     // [16][224]
   static constexpr int C2D = C2F + 16 * 224;   // [16][416]
   static constexpr int CONV_PACK_END = C2D + 16 * 416;
   using Head = HeadDims<400, 120, 84, true, false, false, true,
@@ -97,7 +97,7 @@ template <typename T> struct Packer<LenetModel, T> {
     using L = LenetModel;
     if (p < L::CB1) {                     // conv1.weight [6][1][5][5]
       int n = p / 25, k = p % 25;
-      pack[L::C1 + n * 32 + k] = to_t<T>(v);
+      pack[L::C1 + n * 64 + (k / 5) * 8 + k % 5] = to_t<T>(v);
     } else if (p >= L::CW2 && p < L::CB2) {  // conv2.weight [16][6][5][5]
       int q = p - L::CW2, n = q / 150, r = q % 150, c = r / 25, pos = r % 25;
       pack[L::C2F + n * 224 + pos * 8 + c] = to_t<T>(v);
