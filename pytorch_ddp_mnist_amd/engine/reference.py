@@ -1,0 +1,121 @@
+"""Torch-CPU engine: the reference training loop, kept as the plumbing path and test oracle.
+
+It reproduces ``main()`` of ddp_tutorial_cpu.py:56-97 / mnist_cpu_mp.py:357-418 step for step —
+``zero_grad`` -> forward -> CrossEntropy (NLL for LeNet's log-softmax head) -> ``backward`` ->
+gradient all-reduce (``GlooReducer``, DDP semantics, only when world > 1) -> ``SGD.step`` — on
+pre-normalised in-memory tensors (no per-sample PIL/ToTensor work; identical values).
+"""
+from __future__ import annotations
+
+import os
+import time
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+from ..data.datasets import normalize_batch
+from ..data.sampler import batch_slices
+from ..models import build_model
+from ..parallel.ddp import GlooReducer, model_phases, plan_buckets
+
+
+@dataclass
+class EpochResult:
+    loss_sum: float = 0.0        # sum of per-sample losses
+    correct: float = 0.0
+    count: float = 0.0
+    full_sum: float = 0.0        # loss sum over full batches (for the reference's epoch_loss)
+    n_full: int = 0
+    last_sum: float = 0.0
+    last_b: int = 0
+    seconds: float = 0.0
+    steps: int = 0
+
+    @property
+    def mean_loss(self) -> float:
+        return self.loss_sum / max(1.0, self.count)
+
+    @property
+    def accuracy(self) -> float:
+        return self.correct / max(1.0, self.count)
+
+
+class TorchCPUEngine:
+    name = "torch-cpu"
+
+    def __init__(self, model: str, batch: int, lr: float, momentum: float, dropout: float,
+                 xtr: np.ndarray, ytr: np.ndarray, xte: np.ndarray, yte: np.ndarray, world: int = 1,
+                 bucket_cap_kb: Optional[int] = None, init: Optional[torch.nn.Module] = None):
+        self.model_name, self.batch = model, batch
+        # share the host's cores between co-located ranks instead of oversubscribing them
+        local = int(os.environ.get("LOCAL_WORLD_SIZE", world if world > 1 else 1))
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // max(1, local)))
+        self.module = init if init is not None else build_model(model)
+        if model == "mlp":
+            self.module[2].p = dropout
+        shape = (-1, 784) if model == "mlp" else (-1, 1, 28, 28)
+        self.x = normalize_batch(torch.from_numpy(np.ascontiguousarray(xtr))).reshape(shape)
+        self.y = torch.from_numpy(ytr.astype(np.int64))
+        self.xt = normalize_batch(torch.from_numpy(np.ascontiguousarray(xte))).reshape(shape)
+        self.yt = torch.from_numpy(yte.astype(np.int64))
+        self.opt = torch.optim.SGD(self.module.parameters(), lr=lr, momentum=momentum)
+        cap = None if bucket_cap_kb is None else bucket_cap_kb * 1024
+        self.reducer = GlooReducer(self.module, world, plan_buckets(model_phases(model), cap))
+        self.crit = F.nll_loss if model == "lenet5" else F.cross_entropy
+
+    def train_epoch(self, indices: torch.Tensor, progress=None) -> EpochResult:
+        r = EpochResult()
+        self.module.train()
+        t0 = time.perf_counter()
+        slices = batch_slices(indices.numel(), self.batch)
+        for s, b in slices:
+            idx = indices[s:s + b]
+            x, y = self.x[idx], self.y[idx]
+            self.opt.zero_grad()
+            out = self.module(x)
+            loss = self.crit(out, y)
+            loss.backward()
+            self.reducer.sync_grads()
+            self.opt.step()
+            lv = float(loss.item()) * b
+            r.loss_sum += lv
+            r.correct += float((out.argmax(1) == y).sum())
+            r.count += b
+            if b == self.batch:
+                r.full_sum += lv
+                r.n_full += 1
+            else:
+                r.last_sum, r.last_b = lv, b
+            r.steps += 1
+            if progress:
+                progress(float(loss.item()))
+        r.seconds = time.perf_counter() - t0
+        return r
+
+    @torch.no_grad()
+    def evaluate(self, indices: torch.Tensor) -> EpochResult:
+        r = EpochResult()
+        self.module.eval()
+        for s, b in batch_slices(indices.numel(), self.batch):
+            idx = indices[s:s + b]
+            out = self.module(self.xt[idx])
+            y = self.yt[idx]
+            lv = float(self.crit(out, y, reduction="sum"))
+            r.loss_sum += lv
+            r.correct += float((out.argmax(1) == y).sum())
+            r.count += b
+            if b == self.batch:
+                r.full_sum += lv
+                r.n_full += 1
+            else:
+                r.last_sum, r.last_b = lv, b
+        return r
+
+    def state_dict(self):
+        return {k: v.detach().clone() for k, v in self.module.state_dict().items()}
+
+    def finish(self) -> None:
+        pass

@@ -1,0 +1,201 @@
+"""Epoch driver shared by every entry script.
+
+``run(cfg, entry)`` = the reference's ``__main__`` blocks + ``main()`` re-designed once:
+wire-up -> data (idx / netCDF / synthetic) -> engine (native MI355X trainer on a GPU, torch-CPU
+reference loop otherwise) -> per epoch {DistributedSampler-equivalent order, train, full test-set
+eval, reference epoch line} -> rank-0 ``model.pt``.
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..config import TrainConfig
+from ..data.datasets import load_arrays
+from ..data.sampler import epoch_indices
+from ..models import build_model
+from ..parallel.comm import DistContext, init_distributed
+from ..parallel.ddp import model_phases, plan_buckets
+from ..utils.checkpoint import save_model
+from ..utils.logging import MetricsWriter, banner, epoch_line, reference_epoch_loss
+from ..utils.profiling import enable as enable_roctx, range_
+from .reference import EpochResult, TorchCPUEngine
+
+
+class NativeEngine:
+    """Adapter of :class:`NativeTrainer` to the epoch driver (GPU path)."""
+    name = "native-hip"
+
+    def __init__(self, cfg: TrainConfig, ctx: DistContext, xtr, ytr, xte, yte, init: torch.nn.Module):
+        from ..data.device_loader import upload_arrays
+        from .native import NativeTrainer
+        dev = ctx.device
+        images, labels = upload_arrays(xtr, ytr, dev)
+        self.test_images, self.test_labels = upload_arrays(xte, yte, dev)
+        self.batch = cfg.batch_size
+        self.cfg, self.ctx = cfg, ctx
+        self.tr = NativeTrainer(cfg.model, cfg.dtype, cfg.batch_size, images, labels, device=dev, lr=cfg.lr,
+                                momentum=cfg.momentum, dropout=cfg.dropout if cfg.model == "mlp" else 0.0,
+                                seed=cfg.seed * 7919 + ctx.rank, init=init)
+        cap = None if cfg.bucket_cap_kb is None else cfg.bucket_cap_kb * 1024
+        self.tr.set_buckets(plan_buckets(model_phases(cfg.model), cap))
+        self.torch_comm = ctx.world > 1 and ctx.rccl is None
+        if ctx.world > 1 and ctx.rccl is not None:
+            self.tr.attach_comm(ctx.rccl, ctx.world)
+            self.tr.broadcast_params(0)
+        elif self.torch_comm:
+            import torch.distributed as dist
+            dist.broadcast(self.tr.params, 0)
+            self.tr.load_flat(self.tr.params.clone())
+        self.use_graph = cfg.graph and not self.torch_comm
+
+    def _step(self, b: int) -> None:
+        if self.torch_comm:
+            import torch.distributed as dist
+            self.tr.forward_backward(b)
+            self.tr.synchronize()
+            dist.all_reduce(self.tr.grad)
+            self.tr.optimizer_step(1.0 / self.ctx.world)
+        else:
+            self.tr.step(b, use_graph=self.use_graph)
+
+    def train_epoch(self, indices: torch.Tensor, progress=None) -> EpochResult:
+        tr, B = self.tr, self.batch
+        r = EpochResult()
+        t0 = time.perf_counter()
+        tr.set_epoch_indices(indices)
+        tr.reset_metrics()
+        n = indices.numel()
+        nfull, last = divmod(n, B)
+        with range_("train_full_batches"):
+            for _ in range(nfull):
+                self._step(B)
+        m = tr.read_metrics()
+        r.full_sum, r.n_full = m.loss_sum, nfull
+        if last:
+            self._step(last)
+            m2 = tr.read_metrics()
+            r.last_sum, r.last_b = m2.loss_sum - m.loss_sum, last
+            m = m2
+        tr.synchronize()
+        r.loss_sum, r.correct, r.count = m.loss_sum, m.correct, m.count
+        r.seconds, r.steps = time.perf_counter() - t0, nfull + (1 if last else 0)
+        return r
+
+    def evaluate(self, indices: torch.Tensor) -> EpochResult:
+        tr, B = self.tr, self.batch
+        r = EpochResult()
+        idx = indices.to(self.ctx.device, torch.int32).contiguous()
+        with torch.cuda.stream(tr.stream):
+            tr.eval_metrics.zero_()
+        n = idx.numel()
+        nfull, last = divmod(n, B)
+
+        def run(s, b):
+            tr.rt.eval_batch(self.test_images.data_ptr(), self.test_labels.data_ptr(), idx.data_ptr() + 4 * s, b,
+                             tr.eval_metrics.data_ptr(), tr.stream.cuda_stream)
+        for i in range(nfull):
+            run(i * B, B)
+        m = tr.read_metrics("eval")
+        r.full_sum, r.n_full = m.loss_sum, nfull
+        if last:
+            run(nfull * B, last)
+            m2 = tr.read_metrics("eval")
+            r.last_sum, r.last_b = m2.loss_sum - m.loss_sum, last
+            m = m2
+        r.loss_sum, r.correct, r.count = m.loss_sum, m.correct, m.count
+        return r
+
+    def state_dict(self):
+        return self.tr.state_dict()
+
+    def finish(self) -> None:
+        self.tr.synchronize()
+
+
+def make_engine(cfg: TrainConfig, ctx: DistContext, xtr, ytr, xte, yte):
+    if cfg.init_seed is not None:
+        torch.manual_seed(cfg.init_seed)
+    init = build_model(cfg.model)
+    if ctx.device.type == "cuda":
+        return NativeEngine(cfg, ctx, xtr, ytr, xte, yte, init)
+    return TorchCPUEngine(cfg.model, cfg.batch_size, cfg.lr, cfg.momentum, cfg.dropout, xtr, ytr, xte, yte,
+                          world=ctx.world, bucket_cap_kb=cfg.bucket_cap_kb, init=init)
+
+
+def _data_format(cfg: TrainConfig, entry: str) -> str:
+    if cfg.data_format != "auto":
+        return cfg.data_format
+    return "netcdf" if "pnetcdf" in entry else "idx"
+
+
+def run(cfg: TrainConfig, entry: str = "ddp_tutorial_cpu", show_banner: bool = False,
+        ctx: Optional[DistContext] = None) -> dict:
+    if cfg.profile:
+        enable_roctx(True)
+    own_ctx = ctx is None
+    if ctx is None:
+        world_env = int(os.environ.get("WORLD_SIZE", "1"))
+        parallel = cfg.parallel or world_env > 1
+        method = cfg.wireup_method if (cfg.parallel and entry.startswith("mnist_")) else None
+        # The method only decides how rank/world/master are derived from the launcher env; the
+        # backend follows the device: no GPU -> gloo (the reference forces "gloo" here, which
+        # also drops the SLURM/PMI variables: mnist_cpu_mp.py:247-249 -- we keep them).
+        ctx = init_distributed(method, parallel=parallel, device=cfg.device, comm=cfg.comm)
+    fmt = _data_format(cfg, entry)
+    root = cfg.data_path if cfg.data_path else ("." if fmt == "netcdf" else "./mnist_data")
+    if fmt == "netcdf" and ctx.rank == 0:
+        print("=> Reading NetCDF File...")
+    # rank 0 creates missing files first, the others wait, then every rank reads
+    if ctx.rank == 0:
+        xtr, ytr, xte, yte, src = load_arrays(fmt, root, cfg.data_limit, create=True, verbose=True)
+    ctx.barrier()
+    if ctx.rank != 0:
+        xtr, ytr, xte, yte, src = load_arrays(fmt, root, cfg.data_limit, create=False, verbose=False)
+    if fmt == "netcdf" and ctx.rank == 0:
+        print("=> Dataset created, image nc file is : {}".format(os.path.join(root, "mnist_train_images.nc")))
+    n_gpus = torch.cuda.device_count() if ctx.device.type == "cuda" else 0
+    engine = make_engine(cfg, ctx, xtr, ytr, xte, yte)
+    if show_banner:
+        banner(ctx.rank, ctx.world, n_gpus, ctx.device, src, cfg.num_workers, cfg.n_epochs, cfg.parallel,
+               cfg.model, cfg.dtype if ctx.device.type == "cuda" else "fp32", engine.name)
+    metrics = MetricsWriter(cfg.metrics_jsonl, ctx.rank)
+    ntest = len(yte)
+    history = []
+    for i in range(cfg.n_epochs):
+        idx = epoch_indices(len(ytr), ctx.world, ctx.rank, i, cfg.seed)
+        with range_(f"epoch{i}.train"):
+            tr = engine.train_epoch(idx)
+        if cfg.shard_eval and ctx.world > 1:
+            tidx = torch.arange(ctx.rank, ntest, ctx.world)
+        else:
+            tidx = torch.arange(ntest)
+        with range_(f"epoch{i}.eval"):
+            ev = engine.evaluate(tidx)
+        train_loss = reference_epoch_loss(tr.full_sum, tr.n_full, cfg.batch_size, tr.last_sum, tr.last_b)
+        val_loss = reference_epoch_loss(ev.full_sum, ev.n_full, cfg.batch_size, ev.last_sum, ev.last_b)
+        print(epoch_line(i, train_loss, val_loss), flush=True)
+        g = ctx.all_reduce_sum([tr.loss_sum, tr.correct, tr.count, ev.loss_sum, ev.correct, ev.count])
+        secs = ctx.all_reduce_max(tr.seconds)
+        ips = g[2] / secs if secs > 0 else 0.0
+        rec = dict(epoch=i, train_loss_mean=g[0] / max(g[2], 1), train_acc=g[1] / max(g[2], 1),
+                   val_loss_mean=g[3] / max(g[5], 1), val_acc=g[4] / max(g[5], 1), images_per_sec=ips,
+                   epoch_seconds=secs, world=ctx.world, engine=engine.name)
+        history.append(rec)
+        if ctx.rank == 0:
+            print(f"[rank0] epoch={i} global_train_loss={rec['train_loss_mean']:.4f} train_acc={rec['train_acc']:.4f} "
+                  f"val_loss={rec['val_loss_mean']:.4f} val_acc={rec['val_acc']:.4f} "
+                  f"images/s={ips:,.0f} ({engine.name}, world={ctx.world})", flush=True)
+        metrics.write(**rec)
+    engine.finish()
+    sd = engine.state_dict()
+    if ctx.rank == 0 and cfg.save_path:
+        save_model(sd, cfg.save_path)
+    metrics.close()
+    if own_ctx:
+        ctx.finalize()
+    return {"history": history, "state_dict": sd, "rank": ctx.rank, "world": ctx.world}

@@ -1,0 +1,97 @@
+"""Data-parallel gradient exchange: bucket planning + a gloo reducer for the CPU path.
+
+Reference: ``DistributedDataParallel(model[, device_ids])`` (ddp_tutorial_multi_gpu.py:72,
+mnist_cpu_mp.py:371) — parameter broadcast from rank 0 at construction, bucketed SUM
+all-reduce of gradients during backward (first bucket <= 1 MiB, then 25 MiB caps, grads divided
+by the world size), ``model.module`` unwrap.  For both reference models every gradient fits the
+first bucket, so the reference does ONE 473,088-byte (MLP) all-reduce per step with no overlap
+(survey §2.7, CS5).
+
+MI355X design (GPU path, csrc/runtime/trainer.cpp): gradients are written by the kernels into
+ONE flat fp32 slab; a bucket is a contiguous range of it, launched on the comm stream as soon as
+the backward phase that produces it has been reduced.  :func:`plan_buckets` decides the ranges:
+for the small messages of these models the all-reduce is latency-bound on xGMI (7 point-to-point
+links, ~153 GB/s each — a 473 KB ring step is a few microseconds), so the plan is "as few buckets
+as possible, split only at phase boundaries where the remaining backward work can hide one":
+LeNet-5 gets two buckets (FC head 236.5 KB, overlapped with the convolution backward; conv 10 KB,
+exposed), the MLP one.  ``bucket_cap_kb`` forces further splits (A/B experiments).
+
+:class:`GlooReducer` is the same contract for the CPU path (plumbing / oracle): it broadcasts
+parameters at construction and all-reduces the flattened gradients in the same bucket plan.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+Range = Tuple[int, int, int]  # (p0, p1, phase)
+
+
+def plan_buckets(phases: Sequence[Tuple[int, int]], cap_bytes: Optional[int] = None,
+                 elem_bytes: int = 4) -> List[Range]:
+    """Split each backward phase's contiguous parameter range into <= cap-sized buckets.
+
+    ``phases`` lists (p0, p1) ranges in the order backward produces them; bucket k of phase i is
+    launched when phase i's gradients are complete.
+    """
+    out: List[Range] = []
+    for ph, (p0, p1) in enumerate(phases):
+        if cap_bytes is None or cap_bytes <= 0:
+            out.append((p0, p1, ph))
+            continue
+        step = max(1, cap_bytes // elem_bytes)
+        # later parameters of a phase are produced first in backward: cut from the end
+        e = p1
+        while e > p0:
+            s = max(p0, e - step)
+            out.append((s, e, ph))
+            e = s
+    return out
+
+
+def model_phases(model: str) -> List[Tuple[int, int]]:
+    from ..models import CONV_PARAMS, NPARAM
+    n, c = NPARAM[model], CONV_PARAMS[model]
+    return [(c, n), (0, c)] if c else [(0, n)]
+
+
+class GlooReducer:
+    """DDP semantics for the torch-CPU engine: broadcast at init, bucketed mean all-reduce."""
+
+    def __init__(self, module: torch.nn.Module, world: int, buckets: Optional[List[Range]] = None):
+        self.module = module
+        self.world = world
+        self.params = [p for p in module.parameters()]
+        self.numel = sum(p.numel() for p in self.params)
+        self.buckets = buckets or [(0, self.numel, 0)]
+        if world > 1 and dist.is_initialized():
+            with torch.no_grad():
+                flat = torch.cat([p.detach().reshape(-1) for p in self.params])
+                dist.broadcast(flat, 0)
+                self._unflatten(flat, grads=False)
+
+    def _unflatten(self, flat: torch.Tensor, grads: bool) -> None:
+        off = 0
+        for p in self.params:
+            n = p.numel()
+            v = flat[off:off + n].view_as(p)
+            if grads:
+                if p.grad is None:
+                    p.grad = v.clone()
+                else:
+                    p.grad.copy_(v)
+            else:
+                p.data.copy_(v)
+            off += n
+
+    def sync_grads(self) -> None:
+        if self.world <= 1 or not dist.is_initialized():
+            return
+        flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in self.params])
+        works = [dist.all_reduce(flat[a:b], async_op=True) for a, b, _ in self.buckets]
+        for wk in works:
+            wk.wait()
+        flat.div_(self.world)
+        self._unflatten(flat, grads=True)

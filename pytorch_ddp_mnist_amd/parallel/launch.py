@@ -1,0 +1,102 @@
+"""Local multi-process launcher (``mpiexec -n N`` stand-in; no MPI in this image, survey Q19).
+
+    python -m pytorch_ddp_mnist_amd.parallel.launch -n 4 [--style pmi|ompi|slurm|torch] -- \
+        python3 mnist_pnetcdf_cpu_mp.py --parallel --wireup_method mpich
+
+Spawns N children with the environment a real launcher would provide (PMI_RANK/PMI_SIZE for
+MPICH/Hydra, OMPI_COMM_WORLD_* for Open MPI, SLURM_* for srun, RANK/WORLD_SIZE/LOCAL_RANK for
+torchrun) plus MASTER_ADDR=127.0.0.1 and a free MASTER_PORT, so every reference wire-up method can
+be exercised on one host.  Failure detection: the first child that exits non-zero (or a timeout)
+terminates its siblings' process groups and the launcher exits with that child's code.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+from typing import List
+
+
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def child_env(style: str, rank: int, n: int, port: int, base=None) -> dict:
+    env = dict(os.environ if base is None else base)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    env["MASTER_ADDR"] = "127.0.0.1"
+    env["MASTER_PORT"] = str(port)
+    if style == "pmi":
+        env.update(PMI_RANK=str(rank), PMI_SIZE=str(n), MPI_LOCALRANKID=str(rank))
+    elif style == "ompi":
+        env.update(OMPI_COMM_WORLD_RANK=str(rank), OMPI_COMM_WORLD_SIZE=str(n), OMPI_COMM_WORLD_LOCAL_RANK=str(rank),
+                   PMIX_SERVER_URI2="pmix-server.1;tcp4://127.0.0.1:%d" % port)
+        env.pop("MASTER_ADDR")
+    elif style == "slurm":
+        env.update(SLURM_PROCID=str(rank), SLURM_NTASKS=str(n), SLURM_LOCALID=str(rank), SLURM_JOB_NUM_NODES="1",
+                   SLURM_TASKS_PER_NODE=str(n), SLURM_LAUNCH_NODE_IPADDR="127.0.0.1", SLURM_SRUN_COMM_PORT=str(port))
+        env.pop("MASTER_ADDR")
+        env.pop("MASTER_PORT")
+    else:  # torch
+        env.update(RANK=str(rank), WORLD_SIZE=str(n), LOCAL_RANK=str(rank))
+    return env
+
+
+def launch(cmd: List[str], n: int, style: str = "pmi", timeout: float = 0.0) -> int:
+    port = free_port()
+    procs = [subprocess.Popen(cmd, env=child_env(style, r, n, port), start_new_session=True) for r in range(n)]
+    t0 = time.time()
+    rc = 0
+    try:
+        while True:
+            alive = 0
+            for p in procs:
+                code = p.poll()
+                if code is None:
+                    alive += 1
+                elif code != 0 and rc == 0:
+                    rc = code
+            if rc != 0 or alive == 0:
+                break
+            if timeout and time.time() - t0 > timeout:
+                rc = 124
+                break
+            time.sleep(0.05)
+    finally:
+        if rc != 0:
+            for p in procs:
+                if p.poll() is None:
+                    try:
+                        os.killpg(p.pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+    return rc
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("-n", "--nproc", type=int, default=1)
+    ap.add_argument("--style", choices=["pmi", "ompi", "slurm", "torch"], default="pmi")
+    ap.add_argument("--timeout", type=float, default=0.0)
+    ap.add_argument("cmd", nargs=argparse.REMAINDER)
+    a = ap.parse_args(argv)
+    cmd = a.cmd[1:] if a.cmd and a.cmd[0] == "--" else a.cmd
+    if not cmd:
+        ap.error("no command")
+    return launch(cmd, a.nproc, a.style, a.timeout)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,85 @@
+"""Console output compatible with the reference, plus structured metrics.
+
+* the per-epoch line ``Epoch={i}, train_loss={:.4f}, val_loss={:.4f}`` printed by every rank,
+  with the reference's loss bookkeeping (sum over batches of ``mean_batch_loss / batch_size``,
+  survey quirk Q7) — kept byte-compatible;
+* the rank-0 banner of ``init_parallel`` (mnist_cpu_mp.py:278-299, ``"%-32s: %s"`` fields) with
+  accurate labels (Q15);
+* an additional rank-0 line with the true global mean loss, top-1 accuracy and images/sec, and
+  an optional JSON-lines metrics file.
+"""
+from __future__ import annotations
+
+import json
+import socket
+import sys
+import time
+from typing import Optional
+
+
+def epoch_line(i: int, train_loss: float, val_loss: float) -> str:
+    return f"Epoch={i}, train_loss={train_loss:.4f}, val_loss={val_loss:.4f}"
+
+
+def banner(rank: int, world: int, n_gpus: int, device, fmt: str, num_workers: int, n_epochs: int,
+           parallel: bool, model: str, dtype: str, engine: str, out=sys.stdout) -> None:
+    if rank != 0:
+        return
+    p = lambda k, v: print("%-32s: %s" % (k, v), file=out)  # noqa: E731
+    print("------------------------------------------------------------------", file=out)
+    print("\n======== MNIST %s training (%s) ========" % ("data-parallel" if parallel else "serial", engine), file=out)
+    p("Host name", socket.gethostname())
+    p("Number of processes", world)
+    p("number of GPUs per node", n_gpus)
+    if getattr(device, "type", "cpu") == "cuda":
+        p("Rank 0 GPU device", device)
+    else:
+        print("Rank 0 is Using CPU device", file=out)
+    p("Input file format", fmt)
+    p("DataLoader num_workers", num_workers)
+    p("Number of epochs", n_epochs)
+    p("Model / compute dtype", f"{model} / {dtype}")
+    print("------------------------------------------------------------------", file=out)
+
+
+def reference_epoch_loss(full_sum: float, n_full: int, batch: int, last_sum: float, last_b: int) -> float:
+    """sum_b mean_b / B_b  ==  full_sum / B^2 + last_sum / B_last^2 (Q7 formula)."""
+    v = full_sum / float(batch * batch) if n_full else 0.0
+    if last_b:
+        v += last_sum / float(last_b * last_b)
+    return v
+
+
+class MetricsWriter:
+    def __init__(self, path: Optional[str], rank: int = 0):
+        self.f = open(path, "a") if (path and rank == 0) else None
+
+    def write(self, **kw) -> None:
+        if self.f:
+            kw.setdefault("time", time.time())
+            self.f.write(json.dumps(kw) + "\n")
+            self.f.flush()
+
+    def close(self) -> None:
+        if self.f:
+            self.f.close()
+
+
+class Progress:
+    """Minimal tqdm stand-in honouring DISABLE_TQDM (ddp_tutorial_cpu.py:9, unused upstream)."""
+
+    def __init__(self, total: int, desc: str = "", disable: bool = True):
+        self.total, self.desc, self.disable = total, desc, disable
+        self.n = 0
+        self.t0 = time.perf_counter()
+
+    def set_description(self, d: str) -> None:
+        self.desc = d
+
+    def update(self, k: int = 1) -> None:
+        self.n += k
+        if not self.disable and (self.n == self.total or self.n % max(1, self.total // 20) == 0):
+            rate = self.n / max(1e-9, time.perf_counter() - self.t0)
+            print(f"\r{self.desc} {self.n}/{self.total} [{rate:.1f}it/s]", end="", file=sys.stderr, flush=True)
+            if self.n == self.total:
+                print(file=sys.stderr)

@@ -1,0 +1,56 @@
+"""End-to-end entry scripts on CPU (plumbing configs of BASELINE.json) + launcher failure handling."""
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ENV = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="2")
+LINE = re.compile(r"^Epoch=0, train_loss=\d+\.\d{4}, val_loss=\d+\.\d{4}$", re.M)
+
+
+def _run(args, cwd, timeout=300):
+    r = subprocess.run([sys.executable] + args, cwd=cwd, env=ENV, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                       text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-3000:]
+    return r.stdout
+
+
+def test_ddp_tutorial_cpu(tmp_path):
+    out = _run([os.path.join(ROOT, "ddp_tutorial_cpu.py"), "--data_limit", "2048"], tmp_path)
+    assert LINE.search(out), out
+    sd = torch.load(tmp_path / "model.pt", weights_only=True)
+    assert list(sd) == ["0.weight", "0.bias", "3.weight", "3.bias", "5.weight"]
+    assert (tmp_path / "mnist_data" / "MNIST" / "raw" / "train-images-idx3-ubyte").exists()
+
+
+def test_converter_and_pnetcdf_single(tmp_path):
+    _run([os.path.join(ROOT, "mnist_to_netcdf.py"), "--synthetic", "--output_dir", str(tmp_path)], tmp_path)
+    assert (tmp_path / "mnist_train_images.nc").exists()
+    out = _run([os.path.join(ROOT, "mnist_pnetcdf_cpu.py"), "--data_limit", "1024", "--model", "lenet5"], tmp_path)
+    assert "=> Reading NetCDF File..." in out and LINE.search(out)
+    assert not (tmp_path / "model.pt").exists()  # upstream mnist_pnetcdf_cpu.py saves nothing (Q13)
+
+
+@pytest.mark.parametrize("style,method,script", [("pmi", "mpich", "mnist_pnetcdf_cpu_mp.py"),
+                                                 ("ompi", "nccl-openmpi", "mnist_cpu_mp.py"),
+                                                 ("slurm", "nccl-slurm", "mnist_cpu_mp.py")])
+def test_mp_scripts_two_ranks(tmp_path, style, method, script):
+    out = _run(["-m", "pytorch_ddp_mnist_amd.parallel.launch", "-n", "2", "--style", style, "--timeout", "240", "--",
+                sys.executable, os.path.join(ROOT, script), "--parallel", "--wireup_method", method,
+                "--data_limit", "2048", "--device", "cpu"], tmp_path)
+    assert "Number of processes             : 2" in out
+    assert len(LINE.findall(out)) == 2          # every rank prints its epoch line (reference behaviour)
+    assert "world=2" in out
+    assert (tmp_path / "model.pt").exists()
+
+
+def test_launcher_propagates_failure(tmp_path):
+    # rank 1 fails at once; rank 0 would hang for 60 s: the launcher must kill it and return 3
+    code = "import os,sys,time; r=int(os.environ['PMI_RANK']); time.sleep(60 if r == 0 else 0); sys.exit(3 if r else 0)"
+    r = subprocess.run([sys.executable, "-m", "pytorch_ddp_mnist_amd.parallel.launch", "-n", "2", "--",
+                        sys.executable, "-c", code], cwd=tmp_path, env=ENV, timeout=25)
+    assert r.returncode == 3
