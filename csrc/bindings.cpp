@@ -49,9 +49,10 @@ PYBIND11_MODULE(_C, m) {
   py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
       .def_static("make_unique_id", [] { return py::bytes(RcclComm::make_unique_id()); })
       .def(py::init([](py::bytes uid, int rank, int world, int device) {
-             return std::make_shared<RcclComm>(std::string(uid), rank, world, device);
-           }),
-           py::call_guard<py::gil_scoped_release>())
+        std::string id(uid);  // copy while holding the GIL; init blocks on peers, so release it then
+        py::gil_scoped_release nogil;
+        return std::make_shared<RcclComm>(id, rank, world, device);
+      }))
       .def("all_reduce_sum_f32",
            [](RcclComm& c, uintptr_t buf, size_t n, uintptr_t s) {
              c.all_reduce_sum_f32(reinterpret_cast<float*>(buf), n, reinterpret_cast<hipStream_t>(s));

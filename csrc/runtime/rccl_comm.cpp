@@ -40,17 +40,17 @@ RcclComm::~RcclComm() {
 }
 
 void RcclComm::all_reduce_sum_f32(float* buf, size_t count, hipStream_t s) {
-  if (world_ == 1 || count == 0) return;
+  if (count == 0) return;
   NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm_, s));
 }
 
 void RcclComm::broadcast_f32(float* buf, size_t count, int root, hipStream_t s) {
-  if (world_ == 1 || count == 0) return;
+  if (count == 0) return;
   NCCL_CHECK(ncclBroadcast(buf, buf, count, ncclFloat32, root, comm_, s));
 }
 
 void RcclComm::all_reduce_max_f64(double* buf, size_t count, hipStream_t s) {
-  if (world_ == 1 || count == 0) return;
+  if (count == 0) return;
   NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclFloat64, ncclMax, comm_, s));
 }
 

@@ -168,7 +168,7 @@ void Trainer::optimizer_step(float gscale, uintptr_t stream) {
 }
 
 void Trainer::comm_phase(int phase, hipStream_t s) {
-  if (world_ <= 1 || !comm_) return;
+  if (!comm_) return;  // an attached communicator is always used (world 1 included: tests RCCL-in-graph)
   hipStream_t cs = s;
   if (overlap_) {
     HIP_CHECK(hipEventRecord(events_[phase], s));
@@ -204,7 +204,7 @@ void Trainer::launch_step(int B, hipStream_t s) {
     post_launch(s);
     comm_phase(1, s);
   }
-  if (world_ > 1 && comm_ && overlap_) {
+  if (comm_ && overlap_) {
     HIP_CHECK(hipEventRecord(events_[2], comm_stream_));
     HIP_CHECK(hipStreamWaitEvent(s, events_[2], 0));
   }

@@ -156,7 +156,7 @@ class NativeTrainer:
 
     def broadcast_params(self, root: int = 0) -> None:
         """DDP construction semantics: every rank starts from rank 0's parameters."""
-        if self.comm is None or self.world == 1:
+        if self.comm is None:
             return
         self._sync_in()
         self.comm.broadcast_f32(self.params.data_ptr(), self.nparam, root, self.stream.cuda_stream)

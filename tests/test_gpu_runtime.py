@@ -1,0 +1,85 @@
+"""T5: native RCCL communicator and the GPU paths of the entry scripts on one MI355X.
+
+RCCL refuses two ranks on one GPU, so multi-rank collectives are covered by the CPU gloo tests
+(test_ddp_cpu.py) and by the driver's 8-GPU bench; here the communicator runs at world size 1
+(a real ncclAllReduce / ncclBroadcast, also captured inside the step hipGraph).
+"""
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_rccl_world1_collectives(native):
+    C = native
+    comm = C.RcclComm(C.RcclComm.make_unique_id(), 0, 1, 0)
+    x = torch.arange(1000, dtype=torch.float32, device="cuda")
+    s = torch.cuda.current_stream()
+    comm.all_reduce_sum_f32(x.data_ptr(), x.numel(), s.cuda_stream)
+    comm.broadcast_f32(x.data_ptr(), x.numel(), 0, s.cuda_stream)
+    comm.wait_stream(s.cuda_stream, 60.0)
+    assert torch.equal(x.cpu(), torch.arange(1000, dtype=torch.float32))
+    assert comm.async_error() == ""
+    assert (comm.rank, comm.world) == (0, 1)
+
+
+@pytest.mark.parametrize("model_name", ["mlp", "lenet5"])
+def test_rccl_inside_captured_step(native, small_mnist, model_name):
+    """The step graph with the RCCL bucket all-reduces captured on the side stream == eager without comm."""
+    from pytorch_ddp_mnist_amd.engine.native import NativeTrainer
+    from pytorch_ddp_mnist_amd.models import build_model
+    x, y, _, _ = small_mnist
+    torch.manual_seed(0)
+    m = build_model(model_name)
+    idx = torch.randperm(len(y), generator=torch.Generator().manual_seed(1))[:128 * 3].to(torch.int32)
+    out = []
+    for with_comm in (False, True):
+        tr = NativeTrainer(model_name, "bf16", 128, torch.from_numpy(x.reshape(-1, 784)), torch.from_numpy(y),
+                           dropout=0.0, init=m)
+        if with_comm:
+            tr.attach_comm(native.RcclComm(native.RcclComm.make_unique_id(), 0, 1, 0), 1, overlap=True)
+            tr.broadcast_params(0)
+        tr.set_epoch_indices(idx)
+        for _ in range(3):
+            tr.step(128, use_graph=with_comm)
+        tr.synchronize()
+        out.append(tr.params.cpu())
+    assert torch.equal(out[0], out[1])
+
+
+def _run(args, cwd, timeout=600):
+    r = subprocess.run([sys.executable] + args, cwd=cwd, env=dict(os.environ, PYTHONPATH=ROOT),
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout[-3000:]
+    return r.stdout
+
+
+def test_multi_gpu_tutorial_single_rank(tmp_path):
+    out = _run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr", "127.0.0.1",
+                "--master-port", "29617", os.path.join(ROOT, "ddp_tutorial_multi_gpu.py"), "--epochs", "2",
+                "--model", "lenet5", "--dtype", "bf16", "--synthetic"], tmp_path)
+    lines = re.findall(r"^Epoch=(\d), train_loss=\d+\.\d{4}, val_loss=\d+\.\d{4}$", out, re.M)
+    assert lines == ["0", "1"], out
+    assert "native-hip" in out
+    sd = torch.load(tmp_path / "model.pt", weights_only=True)
+    assert list(sd)[0] == "0.weight" and sd["7.weight"].shape == (120, 400)
+    acc = float(re.findall(r"val_acc=([0-9.]+)", out)[-1])
+    assert acc > 0.5
+
+
+def test_reference_mlp_on_gpu_matches_cpu_engine(tmp_path):
+    """Same script, same seed, fp32, dropout 0: native GPU and torch-CPU epochs agree closely."""
+    args = [os.path.join(ROOT, "mnist_cpu_mp.py"), "--data_limit", "4096", "--synthetic", "--dropout", "0",
+            "--init_seed", "3", "--no_save"]
+    out_gpu = _run(args + ["--device", "cuda"], tmp_path)
+    out_cpu = _run(args + ["--device", "cpu"], tmp_path)
+    lg = re.search(r"global_train_loss=([0-9.]+).*val_loss=([0-9.]+) val_acc=([0-9.]+)", out_gpu).groups()
+    lc = re.search(r"global_train_loss=([0-9.]+).*val_loss=([0-9.]+) val_acc=([0-9.]+)", out_cpu).groups()
+    for a, b in zip(lg, lc):
+        assert abs(float(a) - float(b)) < 2e-3, (out_gpu, out_cpu)
