@@ -45,6 +45,7 @@ struct LenetConvBuffers {
   uint8_t* m2;           // [B][400]
   const void* dp2;       // [B][416] T   (backward input)
   float* slab;           // conv partial grads, row per workgroup: [G][2572]
+  int ablate = 0;        // diagnostics only: bitmask of phases to skip (timing ablation, wrong results)
 };
 
 int head_rows_per_block(ModelKind m, DType t, int B);

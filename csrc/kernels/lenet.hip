@@ -30,8 +30,10 @@ using L = LenetModel;
 constexpr int K0P = L::Head::K0P;  // 416
 
 template <typename T>
-DEV void zero_lds(T* p, int n) {
-  for (int e = threadIdx.x; e < n; e += blockDim.x) p[e] = to_t<T>(0.f);
+DEV void zero_lds(T* p, int n) {  // p 16-byte aligned; 16-byte stores, scalar tail
+  const int nv = n * (int)sizeof(T) / 16;
+  for (int e = threadIdx.x; e < nv; e += blockDim.x) reinterpret_cast<uint4*>(p)[e] = make_uint4(0, 0, 0, 0);
+  for (int e = nv * 16 / (int)sizeof(T) + threadIdx.x; e < n; e += blockDim.x) p[e] = to_t<T>(0.f);
 }
 
 // MFMA fragment of KV ones (bias-gradient column) / zeros
@@ -81,14 +83,21 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(BatchRef br, LenetConvBuf
   const float bias2 = prm[L::CB2 + row];
 
   zero_lds<T>(xs, 8 * S::XP);
+  // software pipeline: image t+1's pixels are in flight (registers) while image t computes
+  auto fetch = [&](int t) -> uint32_t {
+    const int bb = blockIdx.x * ipb + t;
+    if (tid >= 196 || t >= ipb || bb >= br.B) return 0u;
+    return *reinterpret_cast<const uint32_t*>(br.images + (size_t)idx[bb] * 784 + tid * 4);
+  };
+  uint32_t u_next = fetch(0);
   __syncthreads();
   for (int t = 0; t < ipb; ++t) {
     const int b = blockIdx.x * ipb + t;
     const bool valid = b < br.B;
-    // ---- stage: gather + normalise, scattered into the 8 shifted copies
-    if (tid < 196) {
-      uint32_t u = 0;
-      if (valid) u = *reinterpret_cast<const uint32_t*>(br.images + (size_t)idx[b] * 784 + tid * 4);
+    const uint32_t u = u_next;
+    u_next = fetch(t + 1);
+    // ---- stage: normalise, scattered into the 8 shifted copies
+    if (tid < 196 && !(cb.ablate & 1)) {
       const int k = tid * 4, y = k / 28 + 2, x = k % 28 + 2;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -103,7 +112,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(BatchRef br, LenetConvBuf
     __syncthreads();
 
     // ---- conv1 + bias + ReLU + maxpool: 49 M-tiles (4 pooled outputs x 4 window elems each)
-    for (int mt = w; mt < 49; mt += 4) {
+    for (int mt = w; mt < ((cb.ablate & 2) ? 0 : 49); mt += 4) {
       const int q = row >> 2, e = row & 3;
       const int p = mt * 4 + q, py = p / 14, px = p % 14;
       const int oh = 2 * py + (e >> 1), ow = 2 * px + (e & 1);
@@ -134,7 +143,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(BatchRef br, LenetConvBuf
     __syncthreads();
 
     // ---- conv2 + bias + ReLU + maxpool: 100 rows (25 pooled x 4) = 7 M-tiles, N = 16
-    for (int mt = w; mt < 7; mt += 4) {
+    for (int mt = w; mt < ((cb.ablate & 4) ? 0 : 7); mt += 4) {
       const int q = row >> 2, e = row & 3;
       const int p = min(mt * 4 + q, 24), py = p / 5, px = p % 5;
       const int base = ((2 * py + (e >> 1)) * 14 + 2 * px + (e & 1)) * 8;
@@ -184,14 +193,17 @@ struct BwdSmem {
   // pitches padded so the fragment reads and the un-pooling scatters are <= 2-way bank
   // conflicted (measured 60% conflict cycles with the unpadded 1024/224/160/896 pitches)
   static constexpr int W2P = 424, XP = 1048, P1P = 240, D2P = 176, D1P = 912;
+  // XS has 7 planes (5 shifted copies + an all-zero + an all-ones plane) and P1T 32 (30 + zero +
+  // ones): padding / bias-gradient columns read a constant plane instead of branching per lane
+  static constexpr int XPL = 7, PPL = 32;
   static constexpr int OFF_XS = 0;
-  static constexpr int OFF_P1T = rup(OFF_XS + 5 * XP * (int)sizeof(T), 16);
-  static constexpr int OFF_DY2T = rup(OFF_P1T + 5 * 6 * P1P * (int)sizeof(T), 16);
+  static constexpr int OFF_P1T = rup(OFF_XS + XPL * XP * (int)sizeof(T), 16);
+  static constexpr int OFF_DY2T = rup(OFF_P1T + PPL * P1P * (int)sizeof(T), 16);
   static constexpr int OFF_DYS = rup(OFF_DY2T + 16 * D2P * (int)sizeof(T), 16);   // [18][18][16] zero-padded
   static constexpr int OFF_W2 = rup(OFF_DYS + 18 * 18 * 16 * (int)sizeof(T), 16);
   static constexpr int OFF_DY1T = rup(OFF_W2 + 16 * W2P * (int)sizeof(T), 16);
-  static constexpr int OFF_M1 = rup(OFF_DY1T + 8 * D1P * (int)sizeof(T), 16);
-  static constexpr int TOTAL = rup(OFF_M1 + 196 * 8, 16);
+  static constexpr int OFF_M1 = rup(OFF_DY1T + 8 * D1P * (int)sizeof(T), 16);   // [6][14][16] u8 pool1 codes
+  static constexpr int TOTAL = rup(OFF_M1 + 6 * 14 * 16, 16);
   static constexpr int OFF_RED = OFF_XS;  // [4][2][256] f32 scratch after the image loop
   static_assert(4 * 2 * 256 * 4 <= OFF_P1T, "reduction scratch must fit in the aliased XS region");
 };
@@ -220,14 +232,18 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   constexpr int W2CH = 160 / KC;              // conv2 wgrad: 10 rows x 16 positions
   constexpr int D2CH = (400 + KC - 1) / KC;   // conv2 dgrad K = 25 taps x 16 ch (13 bf16 / 25 f32)
   constexpr int W1CH = 896 / KC;              // conv1 wgrad: 28 rows x 32 positions (28 bf16 / 56 f32)
+  constexpr bool WREG = false;  // register-resident dgrad B (52 VGPRs) pushed the kernel to 245 VGPRs and
+                                // made hipcc shuttle accumulators VGPR<->AGPR around every MFMA
 
   // ---- once per workgroup: zero every padded image, stage C2d
-  zero_lds<T>(xs, 5 * S::XP);
-  zero_lds<T>(p1t, 5 * 6 * S::P1P);
+  zero_lds<T>(xs, 6 * S::XP);
+  zero_lds<T>(p1t, 31 * S::P1P);
+  for (int e = tid; e < S::XP; e += 256) xs[6 * S::XP + e] = to_t<T>(1.f);
+  for (int e = tid; e < S::P1P; e += 256) p1t[31 * S::P1P + e] = to_t<T>(1.f);
   zero_lds<T>(dy2t, 16 * S::D2P);
   zero_lds<T>(dy1t, 8 * S::D1P);
   zero_lds<T>(dys, 18 * 18 * 16);
-  {
+  if constexpr (!WREG) {
     constexpr int VE = 16 / (int)sizeof(T);
     for (int e = tid; e < 16 * 416 / VE; e += 256) {
       const int r = e / (416 / VE), c = (e % (416 / VE)) * VE;
@@ -235,24 +251,25 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     }
   }
   // ---- static cost-balanced work split of phase B (dgrad tile = 13 K-chunks, wgrad tile = 5):
-  //      waves 0-2: 3 dgrad M-tiles + 4 wgrad N-tiles; wave 3: 4 dgrad + 1 wgrad (~59 chunks each)
-  const int nd = w == 3 ? 4 : 3, d0 = w * 3;          // dgrad tiles [d0, d0 + nd)
-  const int nw = w == 3 ? 1 : 4, n0w = w * 4;         // wgrad tiles [n0w, n0w + nw)
+  //      dgrad image rows {4,4,3,3}, wgrad tiles {2,2,4,5}  ->  62/62/59/64 chunks per wave
+  const int nd = w < 2 ? 4 : 3, d0 = w < 2 ? 4 * w : 8 + 3 * (w - 2);   // dgrad rows [d0, d0 + nd)
+  const int nw = w < 2 ? 2 : (w == 2 ? 4 : 5), n0w = w < 2 ? 2 * w : (w == 2 ? 4 : 8);
   // ---- per-lane operand offsets (loop invariant)
-  int w2off[4];   // conv2 wgrad B: this wave's output tiles (kcol = tap*8 + c; 200 = bias)
-  int w2sel[4];   // 0 data, 1 ones (bias), 2 zero
+  int w2off[5];   // conv2 wgrad B: this wave's output tiles (kcol = tap*8 + c; 200 = bias)
+  int w2sel[5];   // 0 data, 1 ones (bias), 2 zero
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 5; ++i) {
     const int kcol = (n0w + i) * 16 + row, tap = kcol >> 3, c = kcol & 7;
     w2sel[i] = (kcol < 200 && c < 6) ? 0 : (kcol == 200 ? 1 : 2);
-    w2off[i] = w2sel[i] == 0 ? ((tap % 5) * 6 + c) * S::P1P + (tap / 5) * 16 : 0;
+    w2off[i] = w2sel[i] == 0 ? ((tap % 5) * 6 + c) * S::P1P + (tap / 5) * 16 : (w2sel[i] == 1 ? 31 : 30) * S::P1P;
+    if (i >= nw) w2off[i] = 30 * S::P1P;  // unused tile of this wave: zero plane
   }
   int w1off[2], w1sel[2];  // conv1 wgrad B: tiles over kcol = tap (25 = bias)
 #pragma unroll
   for (int nt = 0; nt < 2; ++nt) {
     const int tap = nt * 16 + row;
     w1sel[nt] = tap < 25 ? 0 : (tap == 25 ? 1 : 2);
-    w1off[nt] = tap < 25 ? (tap % 5) * S::XP + (tap / 5) * 32 : 0;
+    w1off[nt] = tap < 25 ? (tap % 5) * S::XP + (tap / 5) * 32 : (tap == 25 ? 6 : 5) * S::XP;
   }
   const Frag ones = ones_frag<T>(), zf = M::zero();
   int doff[D2CH];  // conv2 dgrad A: -(tap row, col) shift of the lane's K-chunk inside the padded DYS
@@ -261,24 +278,68 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     int tap, n0;
     if constexpr (KV == 8) { tap = kc * 2 + (grp >> 1); n0 = (grp & 1) * 8; }
     else { tap = kc; n0 = grp * 4; }
-    doff[kc] = tap < 25 ? (-(tap / 5) * 18 - (tap % 5)) * 16 + n0 : -(1 << 20);
+    const int tp = min(tap, 24);  // tap 25 (bf16 K padding) has zero weights: any finite A will do
+    doff[kc] = (-(tp / 5) * 18 - (tp % 5)) * 16 + n0;
   }
 
-  f32x4 accW2[4], accW1[2];
+  // conv2 dgrad B operand: in registers for bf16 (13 fragments), from LDS (W2) for fp32
+  Frag wreg[WREG ? D2CH : 1];
+  if constexpr (WREG) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) accW2[i] = zero4();
+    for (int kc = 0; kc < D2CH; ++kc) wreg[kc] = M::load(pack + L::C2D + row * 416 + kc * KC + grp * KV);
+  }
+
+  f32x4 accW2[5], accW1[2];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) accW2[i] = zero4();
   accW1[0] = zero4();
   accW1[1] = zero4();
   __syncthreads();
 
+  // ---- software pipeline: every global input of image t+1 is loaded into registers while
+  //      image t computes (phases B and C), so phase A only moves registers into LDS
+  struct Pre {
+    uint32_t u;       // 4 pixels
+    uint4 p[2];       // pool1 position (8 channels of T)
+    uint2 m;          // pool1 codes
+    uint32_t c[2];    // pool2 codes for scatter items tid, tid + 256
+    float g[2];       // pool2 grads
+  };
+  auto fetch = [&](int t) -> Pre {
+    Pre f;
+    f.u = 0; f.p[0] = f.p[1] = make_uint4(0, 0, 0, 0); f.m = make_uint2(0, 0);
+    f.c[0] = f.c[1] = 0; f.g[0] = f.g[1] = 0.f;
+    const int bb = blockIdx.x * ipb + t;
+    if (t >= ipb || bb >= br.B) return f;
+    if (tid < 196) {
+      f.u = *reinterpret_cast<const uint32_t*>(br.images + (size_t)idx[bb] * 784 + tid * 4);
+      const uint4* ps = reinterpret_cast<const uint4*>(p1g + ((size_t)bb * 196 + tid) * 8);
+      f.p[0] = ps[0];
+      if constexpr (sizeof(T) == 4) f.p[1] = ps[1];
+      f.m = *reinterpret_cast<const uint2*>(cb.m1 + ((size_t)bb * 196 + tid) * 8);
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int e = tid + 256 * r;
+      if (e < 400) {
+        const int n = e & 15, p = e >> 4;
+        f.c[r] = cb.m2[(size_t)bb * 400 + n * 25 + p];
+        f.g[r] = to_f(dp2[(size_t)bb * K0P + n * 25 + p]);
+      }
+    }
+    return f;
+  };
+  Pre nxt = fetch(0);
+
   for (int t = 0; t < ipb; ++t) {
     const int b = blockIdx.x * ipb + t;
     const bool valid = b < br.B;
+    const Pre cur = nxt;
+    nxt = fetch(t + 1);
     // ---- phase A: stage input (5 shifted copies), pool1 (5 shifted channel-major copies),
     //      pool1 codes, and the pool2 un-pooling scatter into DYS / DY2T
-    if (tid < 196) {
-      uint32_t u = 0;
-      if (valid) u = *reinterpret_cast<const uint32_t*>(br.images + (size_t)idx[b] * 784 + tid * 4);
+    if (tid < 196 && !(cb.ablate & 8)) {
+      const uint32_t u = cur.u;
       const int k = tid * 4, y = k / 28 + 2, x = k % 28 + 2;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -291,37 +352,31 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
       }
       // pool1 position tid: 8 channels
       T pv[8];
-      if (valid) {
-        if constexpr (sizeof(T) == 2) {
-          *reinterpret_cast<uint4*>(pv) = *reinterpret_cast<const uint4*>(p1g + ((size_t)b * 196 + tid) * 8);
-        } else {
-          *reinterpret_cast<uint4*>(pv) = *reinterpret_cast<const uint4*>(p1g + ((size_t)b * 196 + tid) * 8);
-          *reinterpret_cast<uint4*>(pv + 4) = *reinterpret_cast<const uint4*>(p1g + ((size_t)b * 196 + tid) * 8 + 4);
-        }
-        *reinterpret_cast<uint2*>(m1s + tid * 8) = *reinterpret_cast<const uint2*>(cb.m1 + ((size_t)b * 196 + tid) * 8);
-      } else {
+      *reinterpret_cast<uint4*>(pv) = cur.p[0];
+      if constexpr (sizeof(T) == 4) *reinterpret_cast<uint4*>(pv + 4) = cur.p[1];
+      {
+        const int cy = tid / 14, cx = tid % 14;
+        const uint32_t mm[2] = {cur.m.x, cur.m.y};
 #pragma unroll
-        for (int c = 0; c < 8; ++c) pv[c] = to_t<T>(0.f);
-        *reinterpret_cast<uint2*>(m1s + tid * 8) = make_uint2(0, 0);
+        for (int c = 0; c < 6; ++c) m1s[(c * 14 + cy) * 16 + cx] = (uint8_t)(mm[c >> 2] >> (8 * (c & 3)));
       }
       const int py = tid / 14, px = tid % 14;
 #pragma unroll
       for (int kw = 0; kw < 5; ++kw) {
         const int xx = px - kw;
-        if (xx >= 0) {
+        if (xx >= 0 && !(cb.ablate & 16)) {
 #pragma unroll
           for (int c = 0; c < 6; ++c) p1t[(kw * 6 + c) * S::P1P + py * 16 + xx] = pv[c];
         }
       }
     }
-    for (int e = tid; e < 400; e += 256) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int e = tid + 256 * r;
+      if (e >= 400 || (cb.ablate & 32)) break;
       const int n = e & 15, p = e >> 4, py = p / 5, px = p % 5;  // channel fastest: conflict-free DYS writes
-      uint8_t code = 0;
-      float g = 0.f;
-      if (valid) {
-        code = cb.m2[(size_t)b * 400 + n * 25 + p];
-        g = to_f(dp2[(size_t)b * K0P + n * 25 + p]);
-      }
+      const uint32_t code = cur.c[r];
+      const float g = cur.g[r];
 #pragma unroll
       for (int win = 0; win < 4; ++win) {
         const int oh = 2 * py + (win >> 1), ow = 2 * px + (win & 1);
@@ -333,58 +388,93 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     __syncthreads();
 
     // ---- phase B1: conv2 wgrad  dW2[n][tap*8+c] += sum_pos dY2[pos][n] * pool1[pos + tap][c]
-    for (int kc = 0; kc < W2CH; ++kc) {
+    for (int kc = 0; kc < ((cb.ablate & 64) ? 0 : W2CH); ++kc) {
       const int p0 = kc * KC + grp * KV, oh = p0 >> 4, ow0 = p0 & 15;
       const Frag a = M::load(dy2t + row * S::D2P + p0);
+      // unconditional loads + MFMAs (unused tiles read the zero plane): a lane-divergent branch
+      // around an MFMA on a loop-carried accumulator makes hipcc shuttle it VGPR<->AGPR every chunk
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if (i < nw) {
-          const Frag bf = w2sel[i] == 0 ? M::load(p1t + w2off[i] + oh * 16 + ow0) : (w2sel[i] == 1 ? ones : zf);
-          M::mma(accW2[i], a, bf);
-        }
-      }
+      for (int i = 0; i < 5; ++i) M::mma(accW2[i], a, M::load(p1t + w2off[i] + oh * 16 + ow0));
     }
 
-    // ---- phase B2: conv2 dgrad  dP1[q][c] = sum_{tap,n} dY2[q - tap][n] * W2[n][c][tap],
-    //      epilogue: pool1 un-pooling (argmax + ReLU) straight into DY1T
-    for (int mt = d0; mt < d0 + nd; ++mt) {
-      const int q = min(mt * 16 + row, 195);   // rows >= 196 are computed on a valid row and dropped
-      const int qy = q / 14, qx = q % 14;
-      const T* abase = dys + ((qy + 4) * 18 + qx + 4) * 16;
-      f32x4 acc = zero4();
+    // ---- phase B2: conv2 dgrad  dP1[q][c] = sum_{tap,n} dY2[q - tap][n] * W2[n][c][tap]
+    //      M = pool1 positions laid out [y][16] (one image row per tile, x >= 14 dropped), so lane
+    //      group g owns x = 4g..4g+3 of row y, and the pool1 un-pooling epilogue (argmax + ReLU)
+    //      writes the conv1 pre-activation grad rows 2y and 2y+1 as ONE 16-byte store each.
+    //      Tiles are processed in pairs for ILP.
+    {
+      auto dgrad_tile_epi = [&](int y, const f32x4& acc) {
+        const int c = row;
+        if (c < 6) {
+          const uint32_t codes = *reinterpret_cast<const uint32_t*>(m1s + (c * 14 + y) * 16 + grp * 4);
+          T r0[8], r1[8];
 #pragma unroll
-      for (int kc = 0; kc < D2CH; ++kc) {
-        const Frag a = doff[kc] > -(1 << 19) ? M::load(abase + doff[kc]) : zf;
-        M::mma(acc, a, M::load(w2 + row * S::W2P + kc * KC + grp * KV));
-      }
-      const int c = row;
-      if (c < 6) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int qq = mt * 16 + grp * 4 + i;
-          if (qq < 196) {
-            const uint8_t code = m1s[qq * 8 + c];
-            const int y = qq / 14, x = qq % 14;
-            const float v = (code & 4) ? acc[i] : 0.f;
-            const int am = code & 3;
-#pragma unroll
-            for (int win = 0; win < 4; ++win)
-              dy1t[c * S::D1P + (2 * y + (win >> 1)) * 32 + 2 * x + (win & 1)] = to_t<T>(win == am ? v : 0.f);
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t code = (codes >> (8 * i)) & 255u;
+            const bool ok = (grp * 4 + i) < 14 && (code & 4);
+            const float v = ok ? acc[i] : 0.f;
+            const uint32_t am = code & 3;
+            r0[2 * i] = to_t<T>(am == 0 ? v : 0.f);
+            r0[2 * i + 1] = to_t<T>(am == 1 ? v : 0.f);
+            r1[2 * i] = to_t<T>(am == 2 ? v : 0.f);
+            r1[2 * i + 1] = to_t<T>(am == 3 ? v : 0.f);
+          }
+          T* d = dy1t + c * S::D1P + (2 * y) * 32 + grp * 8;
+          if constexpr (sizeof(T) == 2) {
+            *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(r0);
+            *reinterpret_cast<uint4*>(d + 32) = *reinterpret_cast<const uint4*>(r1);
+          } else {
+            reinterpret_cast<uint4*>(d)[0] = reinterpret_cast<const uint4*>(r0)[0];
+            reinterpret_cast<uint4*>(d)[1] = reinterpret_cast<const uint4*>(r0)[1];
+            reinterpret_cast<uint4*>(d + 32)[0] = reinterpret_cast<const uint4*>(r1)[0];
+            reinterpret_cast<uint4*>(d + 32)[1] = reinterpret_cast<const uint4*>(r1)[1];
           }
         }
+      };
+      const int x = min(row, 13);
+      int m = 0;
+      const int nmt = (cb.ablate & 128) ? 0 : nd;
+      for (; m + 2 <= nmt; m += 2) {
+        const int y0 = d0 + m, y1 = y0 + 1;
+        const T* a0 = dys + ((y0 + 4) * 18 + x + 4) * 16;
+        const T* a1 = dys + ((y1 + 4) * 18 + x + 4) * 16;
+        f32x4 acc0 = zero4(), acc1 = zero4();
+#pragma unroll
+        for (int kc = 0; kc < D2CH; ++kc) {
+          const Frag fa0 = M::load(a0 + doff[kc]);
+          const Frag fa1 = M::load(a1 + doff[kc]);
+          Frag fb;
+          if constexpr (WREG) fb = wreg[kc];
+          else fb = M::load(w2 + row * S::W2P + kc * KC + grp * KV);
+          M::mma(acc0, fa0, fb);
+          M::mma(acc1, fa1, fb);
+        }
+        dgrad_tile_epi(y0, acc0);
+        dgrad_tile_epi(y1, acc1);
+      }
+      for (; m < nmt; ++m) {
+        const int y0 = d0 + m;
+        const T* a0 = dys + ((y0 + 4) * 18 + x + 4) * 16;
+        f32x4 acc0 = zero4();
+#pragma unroll
+        for (int kc = 0; kc < D2CH; ++kc) {
+          const Frag fa0 = M::load(a0 + doff[kc]);
+          Frag fb;
+          if constexpr (WREG) fb = wreg[kc];
+          else fb = M::load(w2 + row * S::W2P + kc * KC + grp * KV);
+          M::mma(acc0, fa0, fb);
+        }
+        dgrad_tile_epi(y0, acc0);
       }
     }
     __syncthreads();
 
     // ---- phase C: conv1 wgrad  dW1[n][tap] += sum_pos dY1[pos][n] * xpad[pos + tap]
-    for (int kc = w; kc < W1CH; kc += 4) {
+    for (int kc = w; kc < ((cb.ablate & 512) ? 0 : W1CH); kc += 4) {
       const int p0 = kc * KC + grp * KV, oh = p0 >> 5, ow0 = p0 & 31;
-      const Frag a = row < 8 ? M::load(dy1t + row * S::D1P + p0) : zf;
+      const Frag a = M::load(dy1t + min(row, 7) * S::D1P + p0);  // rows 6..15: DY1T rows 6/7 are zero
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        const Frag bf = w1sel[nt] == 0 ? M::load(xs + w1off[nt] + oh * 32 + ow0) : (w1sel[nt] == 1 ? ones : zf);
-        M::mma(accW1[nt], a, bf);
-      }
+      for (int nt = 0; nt < 2; ++nt) M::mma(accW1[nt], a, M::load(xs + w1off[nt] + oh * 32 + ow0));
     }
     __syncthreads();
   }
@@ -392,7 +482,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   // ---- write this workgroup's partial gradients (slab row = blockIdx.x)
   float* out = cb.slab + (size_t)blockIdx.x * L::CONV_PARAMS;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 5; ++i) {
     if (i >= nw) break;
     const int kcol = (n0w + i) * 16 + row;
 #pragma unroll

@@ -114,6 +114,11 @@ LenetConvBuffers Trainer::conv_buffers() const {
   cb.m2 = ptr<uint8_t>(p_.m2);
   cb.dp2 = ptr<const void>(p_.dp2);
   cb.slab = ptr<float>(p_.slab_conv);
+  static const int ablate = [] {
+    const char* e = std::getenv("MNIST_AMD_ABLATE");
+    return e ? std::atoi(e) : 0;
+  }();
+  cb.ablate = ablate;
   return cb;
 }
 
