@@ -54,9 +54,18 @@ template <typename T>
 struct FwdSmem {
   static constexpr int XP = 1048;  // plane pitch (32x32 + pad): 2-way worst-case conflicts (was 8-way at 1024)
   static constexpr int OFF_XS = 0;                                        // [8][XP] T
-  static constexpr int OFF_P1 = rup(8 * XP * (int)sizeof(T), 16);         // [196][8] T
-  static constexpr int TOTAL = rup(OFF_P1 + 196 * 8 * (int)sizeof(T), 16);
+  static constexpr int OFF_P1 = rup(8 * XP * (int)sizeof(T), 16);         // [196][8] T   pool1 output
+  static constexpr int OFF_M1 = rup(OFF_P1 + 196 * 8 * (int)sizeof(T), 16);  // [196][8] u8 pool1 codes
+  static constexpr int OFF_P2 = rup(OFF_M1 + 196 * 8, 16);                // [400] T      pool2 output (NCHW)
+  static constexpr int OFF_M2 = rup(OFF_P2 + 400 * (int)sizeof(T), 16);   // [400] u8     pool2 codes
+  static constexpr int TOTAL = rup(OFF_M2 + 400, 16);
 };
+
+// Coalesced 16-byte copy of a staged LDS image to global memory (both 16-byte aligned).
+DEV void copy_out16(void* dst, const void* src, int bytes) {
+  for (int e = threadIdx.x; e < bytes / 16; e += blockDim.x)
+    reinterpret_cast<uint4*>(dst)[e] = reinterpret_cast<const uint4*>(src)[e];
+}
 
 template <typename T, bool TRAIN>
 __global__ __launch_bounds__(256) void conv_fwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
@@ -67,6 +76,9 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(BatchRef br, LenetConvBuf
   __shared__ __attribute__((aligned(16))) char smem[S::TOTAL];
   T* xs = reinterpret_cast<T*>(smem + S::OFF_XS);
   T* p1s = reinterpret_cast<T*>(smem + S::OFF_P1);
+  uint8_t* m1s = reinterpret_cast<uint8_t*>(smem + S::OFF_M1);
+  T* p2s = reinterpret_cast<T*>(smem + S::OFF_P2);
+  uint8_t* m2s = reinterpret_cast<uint8_t*>(smem + S::OFF_M2);
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
   const int32_t* idx = br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride;
   const T* pack = reinterpret_cast<const T*>(cb.pack);
@@ -82,6 +94,67 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(BatchRef br, LenetConvBuf
   const float bias1 = row < 6 ? prm[L::CB1 + row] : 0.f;
   const float bias2 = prm[L::CB2 + row];
 
+  // conv1 tiling: tile (j, w) = pooled row j (0..13) x pooled columns 4w..4w+3 (grid padded 14->16),
+  // M row = pooled column * 4 + window element.  Since 2*4w is a multiple of 8, the shifted-copy
+  // plane and column of every fragment are lane constants: A(j, kc) = c1base[kc] + 64*j.
+  int c1base[C1CH];
+  {
+    const int q = row >> 2, e = row & 3, xt = 2 * q + (e & 1);
+#pragma unroll
+    for (int kc = 0; kc < C1CH; ++kc) {
+      const int k0 = kc * KC + grp * KV;
+      const int kh = min(k0 >> 3, 4), xx = xt + (k0 & 7);
+      c1base[kc] = (xx & 7) * S::XP + ((e >> 1) + kh) * 32 + 8 * w + (xx & ~7);
+    }
+  }
+  const bool c1valid = 4 * w + grp < 14;  // wave 3, lane groups 2-3: padding columns 14, 15
+  auto c1_epi = [&](int j, const f32x4& acc) {  // pool + bias + ReLU, staged in LDS
+    const int n = row, pp = j * 14 + 4 * w + grp;
+    float mx = acc[0];
+    int am = 0;
+#pragma unroll
+    for (int i = 1; i < 4; ++i)
+      if (acc[i] > mx) { mx = acc[i]; am = i; }
+    const float pre = mx + bias1;
+    if (n < 8 && c1valid) {
+      p1s[pp * 8 + n] = to_t<T>(n < 6 ? fmaxf(pre, 0.f) : 0.f);
+      m1s[pp * 8 + n] = (n < 6) ? (uint8_t)(am | (pre > 0.f ? 4 : 0)) : 0;
+    }
+  };
+  auto c2_acc = [&](int mt, f32x4& acc) {
+    const int q = row >> 2, e = row & 3;
+    const int p = min(mt * 4 + q, 24), py = p / 5, px = p % 5;
+    const int base = ((2 * py + (e >> 1)) * 14 + 2 * px + (e & 1)) * 8;
+#pragma unroll
+    for (int kc = 0; kc < C2CH; ++kc) {
+      int pos, c0;
+      if constexpr (KV == 8) { pos = kc * 4 + grp; c0 = 0; }
+      else { pos = kc * 2 + (grp >> 1); c0 = (grp & 1) * 4; }
+      pos = min(pos, 24);
+      const int kh = pos / 5, kw = pos % 5;
+      M::mma(acc, M::load(p1s + base + (kh * 14 + kw) * 8 + c0), b2[kc]);
+    }
+  };
+  auto c2_epi = [&](int mt, const f32x4& acc) {
+    const int n = row, pp = mt * 4 + grp;
+    if (pp < 25) {
+      float mx = acc[0];
+      int am = 0;
+#pragma unroll
+      for (int i = 1; i < 4; ++i)
+        if (acc[i] > mx) { mx = acc[i]; am = i; }
+      const float pre = mx + bias2;
+      p2s[n * 25 + pp] = to_t<T>(fmaxf(pre, 0.f));
+      m2s[n * 25 + pp] = (uint8_t)(am | (pre > 0.f ? 4 : 0));
+    }
+  };
+  auto flush_p2 = [&](int bprev) {  // previous image's pool2 outputs -> HBM (16-byte stores)
+    if (bprev >= 0 && bprev < br.B) {
+      copy_out16(reinterpret_cast<T*>(cb.p2) + (size_t)bprev * K0P, p2s, 400 * (int)sizeof(T));
+      if (TRAIN) copy_out16(cb.m2 + (size_t)bprev * 400, m2s, 400);
+    }
+  };
+
   zero_lds<T>(xs, 8 * S::XP);
   // software pipeline: image t+1's pixels are in flight (registers) while image t computes
   auto fetch = [&](int t) -> uint32_t {
@@ -96,6 +169,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(BatchRef br, LenetConvBuf
     const bool valid = b < br.B;
     const uint32_t u = u_next;
     u_next = fetch(t + 1);
+    flush_p2(t > 0 ? b - 1 : -1);
     // ---- stage: normalise, scattered into the 8 shifted copies
     if (tid < 196 && !(cb.ablate & 1)) {
       const int k = tid * 4, y = k / 28 + 2, x = k % 28 + 2;
@@ -111,68 +185,46 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(BatchRef br, LenetConvBuf
     }
     __syncthreads();
 
-    // ---- conv1 + bias + ReLU + maxpool: 49 M-tiles (4 pooled outputs x 4 window elems each)
-    for (int mt = w; mt < ((cb.ablate & 2) ? 0 : 49); mt += 4) {
-      const int q = row >> 2, e = row & 3;
-      const int p = mt * 4 + q, py = p / 14, px = p % 14;
-      const int oh = 2 * py + (e >> 1), ow = 2 * px + (e & 1);
-      f32x4 acc = zero4();
+    // ---- conv1 + bias + ReLU + maxpool: 14 pooled rows per wave, in pairs
+    if (!(cb.ablate & 2)) {
+#pragma unroll 1
+      for (int j = 0; j < 14; j += 2) {
+        f32x4 accA = zero4(), accB = zero4();
 #pragma unroll
-      for (int kc = 0; kc < C1CH; ++kc) {
-        const int k0 = kc * KC + grp * KV;
-        const int kh = min(k0 >> 3, 4), x = ow + (k0 & 7);
-        M::mma(acc, M::load(xs + (x & 7) * S::XP + (oh + kh) * 32 + (x & ~7)), b1[kc]);
-      }
-      // lane: channel n = row, pooled position pp = mt*4 + grp, window elems in acc[0..3]
-      const int n = row, pp = mt * 4 + grp;
-      float mx = acc[0];
-      int am = 0;
-#pragma unroll
-      for (int i = 1; i < 4; ++i)
-        if (acc[i] > mx) { mx = acc[i]; am = i; }
-      const float pre = mx + bias1;
-      const float v = (n < 6) ? fmaxf(pre, 0.f) : 0.f;
-      if (n < 8) {
-        p1s[pp * 8 + n] = to_t<T>(v);
-        if (TRAIN && valid) {
-          reinterpret_cast<T*>(cb.p1)[((size_t)b * 196 + pp) * 8 + n] = to_t<T>(v);
-          cb.m1[((size_t)b * 196 + pp) * 8 + n] = (n < 6) ? (uint8_t)(am | (pre > 0.f ? 4 : 0)) : 0;
+        for (int kc = 0; kc < C1CH; ++kc) {
+          const Frag fa = M::load(xs + c1base[kc] + j * 64);
+          const Frag fb = M::load(xs + c1base[kc] + j * 64 + 64);
+          M::mma(accA, fa, b1[kc]);
+          M::mma(accB, fb, b1[kc]);
         }
+        c1_epi(j, accA);
+        c1_epi(j + 1, accB);
       }
     }
     __syncthreads();
 
+    // ---- pool1 -> HBM for the backward pass (16-byte stores), overlapped with conv2
+    if (TRAIN && valid) {
+      copy_out16(reinterpret_cast<T*>(cb.p1) + (size_t)b * 196 * 8, p1s, 196 * 8 * (int)sizeof(T));
+      copy_out16(cb.m1 + (size_t)b * 196 * 8, m1s, 196 * 8);
+    }
     // ---- conv2 + bias + ReLU + maxpool: 100 rows (25 pooled x 4) = 7 M-tiles, N = 16
-    for (int mt = w; mt < ((cb.ablate & 4) ? 0 : 7); mt += 4) {
-      const int q = row >> 2, e = row & 3;
-      const int p = min(mt * 4 + q, 24), py = p / 5, px = p % 5;
-      const int base = ((2 * py + (e >> 1)) * 14 + 2 * px + (e & 1)) * 8;
-      f32x4 acc = zero4();
-#pragma unroll
-      for (int kc = 0; kc < C2CH; ++kc) {
-        int pos, c0;
-        if constexpr (KV == 8) { pos = kc * 4 + grp; c0 = 0; }
-        else { pos = kc * 2 + (grp >> 1); c0 = (grp & 1) * 4; }
-        pos = min(pos, 24);
-        const int kh = pos / 5, kw = pos % 5;
-        M::mma(acc, M::load(p1s + base + (kh * 14 + kw) * 8 + c0), b2[kc]);
-      }
-      const int n = row, pp = mt * 4 + grp;
-      if (pp < 25) {
-        float mx = acc[0];
-        int am = 0;
-#pragma unroll
-        for (int i = 1; i < 4; ++i)
-          if (acc[i] > mx) { mx = acc[i]; am = i; }
-        const float pre = mx + bias2;
-        if (valid) {
-          reinterpret_cast<T*>(cb.p2)[(size_t)b * K0P + n * 25 + pp] = to_t<T>(fmaxf(pre, 0.f));
-          if (TRAIN) cb.m2[(size_t)b * 400 + n * 25 + pp] = (uint8_t)(am | (pre > 0.f ? 4 : 0));
-        }
+    if (!(cb.ablate & 4)) {
+      if (w < 3) {  // waves 0-2: tiles (2w, 2w+1) as a pair; wave 3: tile 6
+        f32x4 accA = zero4(), accB = zero4();
+        c2_acc(2 * w, accA);
+        c2_acc(2 * w + 1, accB);
+        c2_epi(2 * w, accA);
+        c2_epi(2 * w + 1, accB);
+      } else {
+        f32x4 acc = zero4();
+        c2_acc(6, acc);
+        c2_epi(6, acc);
       }
     }
     __syncthreads();
   }
+  flush_p2(blockIdx.x * ipb + ipb - 1);
 }
 
 // ====================================================================================
