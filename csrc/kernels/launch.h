@@ -72,6 +72,10 @@ void launch_sgd_pack(ModelKind m, DType t, float* params, const float* grad, flo
                      int nparam, float lr, float momentum, float gscale, int32_t* step_ptr,
                      hipStream_t s);
 void launch_pack(ModelKind m, DType t, const float* params, void* pack, int nparam, hipStream_t s);
+// Fused gradient reduce + SGD + pack + step bump (no all-reduce between them: single-GPU runs).
+void launch_reduce_sgd(ModelKind m, DType t, const float* slab_a, int lda, int na, const float* slab_b, int ldb,
+                       int nb, int split, int n, float scale, float* params, float* grad, float* mom, void* pack,
+                       float lr, float momentum, int32_t* step_ptr, hipStream_t s);
 
 void launch_gather_normalize(DType t, const BatchRef& br, void* out, int ld, hipStream_t s);
 

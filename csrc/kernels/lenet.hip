@@ -18,6 +18,7 @@
 // workgroup; bias gradients come out of the same GEMMs through an all-ones column.
 // Pool code byte: bits 0-1 argmax window element (first max, raster order, as ATen),
 // bit 2 = pooled pre-activation > 0 (ReLU passes the gradient).
+#include <cstdlib>
 #include <algorithm>
 
 #include "common.h"
@@ -567,7 +568,13 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
 }  // namespace
 
 static int fwd_ipb(int B) { return std::max(1, (B + 1023) / 1024); }
-static int bwd_ipb(int B) { return std::max(1, (B + 1023) / 1024); }
+static int bwd_ipb(int B) {
+  static const int div = [] {
+    const char* e = std::getenv("MNIST_AMD_BWD_BLOCKS");  // tuning knob: target block count
+    return e ? std::max(1, std::atoi(e)) : 512;  // 512 = one full round of 2 blocks/CU; 1024/768 measured slower
+  }();
+  return std::max(1, (B + div - 1) / div);
+}
 
 int lenet_conv_bwd_blocks(int B) {
   const int ipb = bwd_ipb(B);

@@ -29,15 +29,16 @@ __global__ __launch_bounds__(NW * 64) void reduce_slabs_kernel(const float* __re
     const int per = (nslab + NW - 1) / NW;
     const int sb = w * per, se = min(nslab, sb + per);
     int k = sb;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-    for (; k + 4 <= se; k += 4) {
-      s0 += slab[(size_t)k * ld + p];
-      s1 += slab[(size_t)(k + 1) * ld + p];
-      s2 += slab[(size_t)(k + 2) * ld + p];
-      s3 += slab[(size_t)(k + 3) * ld + p];
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (; k + 8 <= se; k += 8) {
+      float v[8];  // eight independent loads in flight per lane before the adds
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = slab[(size_t)(k + i) * ld + p];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += v[i];
     }
-    for (; k < se; ++k) s0 += slab[(size_t)k * ld + p];
-    s = (s0 + s1) + (s2 + s3);
+    for (; k < se; ++k) acc[0] += slab[(size_t)k * ld + p];
+    s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   }
   part[w][lane] = s;
   __syncthreads();
@@ -72,6 +73,71 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(float* __restrict__ param
     step_ptr[0] += 1;  // step within epoch (batch addressing)
     step_ptr[1] += 1;  // global step (dropout stream)
   }
+}
+
+// Fused  grad = scale * sum_s slab[s]  ->  SGD(+momentum)  ->  re-pack, for runs without a gradient
+// all-reduce (one GPU): saves two kernel boundaries and the grad round trip per step.  Parameters
+// [0, split) reduce slab_a, [split, n) reduce slab_b (LeNet: conv slab / FC slab).  One block = 64
+// parameters x NW waves over the slab rows (same fixed summation tree as reduce_slabs_kernel).
+template <class Model, typename T, int NW>
+__global__ __launch_bounds__(NW * 64) void reduce_sgd_kernel(const float* __restrict__ slab_a, int lda, int na,
+                                                             const float* __restrict__ slab_b, int ldb, int nb,
+                                                             int split, int n, float scale, float* __restrict__ params,
+                                                             float* __restrict__ grad, float* __restrict__ mom,
+                                                             T* __restrict__ pack, float lr, float mu,
+                                                             int32_t* step_ptr) {
+  __shared__ float part[NW][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int p = blockIdx.x * 64 + lane;
+  float s = 0.f;
+  if (p < n) {
+    const bool a = p < split;
+    const float* slab = a ? slab_a : slab_b;
+    const int ld = a ? lda : ldb, ns = a ? na : nb;
+    const int per = (ns + NW - 1) / NW;
+    const int sb = w * per, se = min(ns, sb + per);
+    int k = sb;
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (; k + 8 <= se; k += 8) {
+      float v[8];  // eight independent loads in flight per lane before the adds
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = slab[(size_t)(k + i) * ld + p];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += v[i];
+    }
+    for (; k < se; ++k) acc[0] += slab[(size_t)k * ld + p];
+    s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  }
+  part[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && p < n) {
+    float g = 0.f;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) g += part[i][lane];
+    g *= scale;
+    grad[p] = g;
+    if (mom) {
+      const float b = mu * mom[p] + g;
+      mom[p] = b;
+      g = b;
+    }
+    const float v = params[p] - lr * g;
+    params[p] = v;
+    Packer<Model, T>::pack(p, v, pack);
+  }
+  if (step_ptr && blockIdx.x == 0 && threadIdx.x == 0) {
+    step_ptr[0] += 1;
+    step_ptr[1] += 1;
+  }
+}
+
+template <class Model, typename T>
+void reduce_sgd_t(const float* sa, int lda, int na, const float* sb, int ldb, int nb, int split, int n, float scale,
+                  float* params, float* grad, float* mom, void* pack, float lr, float mu, int32_t* step_ptr,
+                  hipStream_t s) {
+  const int grid = (n + 63) / 64;
+  hipLaunchKernelGGL((reduce_sgd_kernel<Model, T, 16>), dim3(grid), dim3(1024), 0, s, sa, lda, na, sb, ldb, nb, split,
+                     n, scale, params, grad, mom, reinterpret_cast<T*>(pack), lr, mu, step_ptr);
 }
 
 template <class Model, typename T>
@@ -139,3 +205,16 @@ void launch_gather_normalize(DType t, const BatchRef& br, void* out, int ld, hip
 int model_nparam(ModelKind m) { return m == ModelKind::MLP ? MlpModel::NPARAM : LenetModel::NPARAM; }
 int model_conv_params(ModelKind m) { return m == ModelKind::MLP ? 0 : LenetModel::CONV_PARAMS; }
 int model_pack_size(ModelKind m) { return m == ModelKind::MLP ? MlpModel::PACK_SIZE : LenetModel::PACK_SIZE; }
+
+void launch_reduce_sgd(ModelKind m, DType t, const float* slab_a, int lda, int na, const float* slab_b, int ldb,
+                       int nb, int split, int n, float scale, float* params, float* grad, float* mom, void* pack,
+                       float lr, float momentum, int32_t* step_ptr, hipStream_t s) {
+  float* mb = momentum != 0.f ? mom : nullptr;
+  if (m == ModelKind::MLP) {
+    if (t == DType::F32) reduce_sgd_t<MlpModel, float>(slab_a, lda, na, slab_b, ldb, nb, split, n, scale, params, grad, mb, pack, lr, momentum, step_ptr, s);
+    else reduce_sgd_t<MlpModel, bf16>(slab_a, lda, na, slab_b, ldb, nb, split, n, scale, params, grad, mb, pack, lr, momentum, step_ptr, s);
+  } else {
+    if (t == DType::F32) reduce_sgd_t<LenetModel, float>(slab_a, lda, na, slab_b, ldb, nb, split, n, scale, params, grad, mb, pack, lr, momentum, step_ptr, s);
+    else reduce_sgd_t<LenetModel, bf16>(slab_a, lda, na, slab_b, ldb, nb, split, n, scale, params, grad, mb, pack, lr, momentum, step_ptr, s);
+  }
+}

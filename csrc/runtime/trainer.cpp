@@ -198,6 +198,19 @@ void Trainer::launch_step(int B, hipStream_t s) {
   post_launch(s);
   const int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s);
   post_launch(s);
+  if (!comm_) {
+    // single GPU: conv backward, then ONE fused reduce + SGD + pack kernel (2 boundaries fewer)
+    int nslab = 0;
+    if (model_ == ModelKind::LENET) {
+      launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s);
+      post_launch(s);
+    }
+    launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
+                      nparam_, splits, cp, nparam_, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
+                      ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, ptr<int32_t>(p_.step), s);
+    post_launch(s);
+    return;
+  }
   launch_reduce(ptr<const float>(p_.slab_fc), nparam_, splits, cp, nparam_, scale, ptr<float>(p_.grad), s);
   post_launch(s);
   comm_phase(0, s);
