@@ -16,7 +16,28 @@
 
 namespace {
 
-// One block = 64 consecutive parameters (lane) x NW waves splitting the slab rows; the per-wave
+// Wave w's share of sum_s slab[s][p]: rows [w*per, (w+1)*per), eight independent loads in flight
+// per lane.  Shared by both reduce kernels so the fused single-GPU step and the reduce -> all-reduce
+// -> SGD path produce bitwise-identical gradients.
+constexpr int RNW = 16;  // waves per reduce block, for every slab count (keeps the tree fixed)
+
+__device__ __forceinline__ float slab_partial(const float* __restrict__ slab, int ld, int nslab, int p, int w) {
+  const int per = (nslab + RNW - 1) / RNW;
+  const int sb = w * per, se = min(nslab, sb + per);
+  int k = sb;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (; k + 8 <= se; k += 8) {
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = slab[(size_t)(k + i) * ld + p];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] += v[i];
+  }
+  for (; k < se; ++k) acc[0] += slab[(size_t)k * ld + p];
+  return ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+}
+
+// One block = 64 consecutive parameters (lane) x RNW waves splitting the slab rows; the per-wave
 // partial sums are combined in a fixed tree, so the result is bitwise reproducible.
 template <int NW>
 __global__ __launch_bounds__(NW * 64) void reduce_slabs_kernel(const float* __restrict__ slab, int ld, int nslab,
@@ -26,19 +47,7 @@ __global__ __launch_bounds__(NW * 64) void reduce_slabs_kernel(const float* __re
   const int p = p0 + blockIdx.x * 64 + lane;
   float s = 0.f;
   if (p < p1) {
-    const int per = (nslab + NW - 1) / NW;
-    const int sb = w * per, se = min(nslab, sb + per);
-    int k = sb;
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (; k + 8 <= se; k += 8) {
-      float v[8];  // eight independent loads in flight per lane before the adds
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = slab[(size_t)(k + i) * ld + p];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] += v[i];
-    }
-    for (; k < se; ++k) acc[0] += slab[(size_t)k * ld + p];
-    s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    s = slab_partial(slab, ld, nslab, p, w);
   }
   part[w][lane] = s;
   __syncthreads();
@@ -92,21 +101,7 @@ __global__ __launch_bounds__(NW * 64) void reduce_sgd_kernel(const float* __rest
   float s = 0.f;
   if (p < n) {
     const bool a = p < split;
-    const float* slab = a ? slab_a : slab_b;
-    const int ld = a ? lda : ldb, ns = a ? na : nb;
-    const int per = (ns + NW - 1) / NW;
-    const int sb = w * per, se = min(ns, sb + per);
-    int k = sb;
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (; k + 8 <= se; k += 8) {
-      float v[8];  // eight independent loads in flight per lane before the adds
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = slab[(size_t)(k + i) * ld + p];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] += v[i];
-    }
-    for (; k < se; ++k) acc[0] += slab[(size_t)k * ld + p];
-    s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+    s = a ? slab_partial(slab_a, lda, na, p, w) : slab_partial(slab_b, ldb, nb, p, w);
   }
   part[w][lane] = s;
   __syncthreads();
@@ -136,7 +131,7 @@ void reduce_sgd_t(const float* sa, int lda, int na, const float* sb, int ldb, in
                   float* params, float* grad, float* mom, void* pack, float lr, float mu, int32_t* step_ptr,
                   hipStream_t s) {
   const int grid = (n + 63) / 64;
-  hipLaunchKernelGGL((reduce_sgd_kernel<Model, T, 16>), dim3(grid), dim3(1024), 0, s, sa, lda, na, sb, ldb, nb, split,
+  hipLaunchKernelGGL((reduce_sgd_kernel<Model, T, RNW>), dim3(grid), dim3(RNW * 64), 0, s, sa, lda, na, sb, ldb, nb, split,
                      n, scale, params, grad, mom, reinterpret_cast<T*>(pack), lr, mu, step_ptr);
 }
 
@@ -163,12 +158,8 @@ void launch_reduce(const float* slab, int slab_ld, int nslab, int p0, int p1, fl
                    hipStream_t s) {
   if (p1 <= p0) return;
   const int grid = (p1 - p0 + 63) / 64;
-  if (nslab >= 64)
-    hipLaunchKernelGGL(reduce_slabs_kernel<16>, dim3(grid), dim3(1024), 0, s, slab, slab_ld, nslab, p0, p1, scale, grad);
-  else if (nslab >= 8)
-    hipLaunchKernelGGL(reduce_slabs_kernel<4>, dim3(grid), dim3(256), 0, s, slab, slab_ld, nslab, p0, p1, scale, grad);
-  else
-    hipLaunchKernelGGL(reduce_slabs_kernel<1>, dim3(grid), dim3(64), 0, s, slab, slab_ld, nslab, p0, p1, scale, grad);
+  hipLaunchKernelGGL(reduce_slabs_kernel<RNW>, dim3(grid), dim3(RNW * 64), 0, s, slab, slab_ld, nslab, p0, p1, scale,
+                     grad);
 }
 
 void launch_sgd_pack(ModelKind m, DType t, float* params, const float* grad, float* mom, void* pack, int nparam,

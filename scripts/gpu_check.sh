@@ -7,8 +7,8 @@ TAG=${1:-run}
 mkdir -p "$OUT"
 cd "${GRAFT_REPO_ROOT:-$(pwd)}" || exit 1
 timeout -k 10 600 python -m pytest tests -m gpu -q -x > "$OUT/${TAG}_pytest.log" 2>&1 &&
-timeout -k 10 300 python bench.py --steps 100 --warmup 10 > "$OUT/${TAG}_bench.log" 2>&1 &&
-timeout -k 10 300 python bench.py --model mlp --dtype fp32 --batch 128 --steps 300 --warmup 20 >> "$OUT/${TAG}_bench.log" 2>&1 &&
+timeout -k 10 300 python bench.py --steps 2000 --warmup 50 > "$OUT/${TAG}_bench.log" 2>&1 &&
+timeout -k 10 300 python bench.py --model mlp --dtype fp32 --batch 128 --steps 2000 --warmup 50 >> "$OUT/${TAG}_bench.log" 2>&1 &&
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_prof" -o run --output-format csv -- python3 "$OUT/../bench.py" --steps 20 --warmup 5 > "$OUT/${TAG}_prof.log" 2>&1)
 rc=$?
 echo "rc=$rc"

@@ -5,7 +5,7 @@ TAG=${1:-q}
 mkdir -p "$OUT"
 cd "${GRAFT_REPO_ROOT:-$(pwd)}" || exit 1
 timeout -k 10 600 python -m pytest tests/test_native_gpu.py -q -x > "$OUT/${TAG}_pytest.log" 2>&1 &&
-timeout -k 10 300 python bench.py --steps 100 --warmup 10 > "$OUT/${TAG}_bench.log" 2>&1 &&
+timeout -k 10 300 python bench.py --steps 2000 --warmup 50 --no-eval > "$OUT/${TAG}_bench.log" 2>&1 &&
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_prof" -o run --output-format csv -- python3 "$OUT/../bench.py" --steps 20 --warmup 5 --no-eval > "$OUT/${TAG}_prof.log" 2>&1)
 rc=$?
 echo "rc=$rc"

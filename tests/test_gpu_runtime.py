@@ -53,6 +53,42 @@ def test_rccl_inside_captured_step(native, small_mnist, model_name):
     assert torch.equal(out[0], out[1])
 
 
+@pytest.mark.parametrize("model_name", ["mlp", "lenet5"])
+def test_module_ddp_rccl_on_gpu(native, model_name):
+    """Bring-your-own-model DDP wrapper on cuda:0 with the native RCCL comm (bucket all-reduces on its
+    side stream, world 1) == the same torch model trained without the wrapper."""
+    import torch.nn.functional as F
+    from pytorch_ddp_mnist_amd.models import build_model
+    from pytorch_ddp_mnist_amd.parallel.module_ddp import DistributedDataParallel
+    comm = native.RcclComm(native.RcclComm.make_unique_id(), 0, 1, 0)
+    g = torch.Generator().manual_seed(0)
+    xs = [torch.randn(64, 784, generator=g) for _ in range(3)]
+    ys = [torch.randint(0, 10, (64,), generator=g) for _ in range(3)]
+    out = []
+    for wrap in (False, True):
+        torch.manual_seed(1)
+        m = build_model(model_name).cuda()
+        if model_name == "mlp":
+            m[2].p = 0.0
+        dm = DistributedDataParallel(m, rccl=comm, bucket_cap_mb=0.1, first_bucket_mb=0.05) if wrap else m
+        opt = torch.optim.SGD(dm.parameters(), lr=0.05, momentum=0.9)
+        for x, y in zip(xs, ys):
+            x = x.cuda().view(-1, 1, 28, 28) if model_name == "lenet5" else x.cuda()
+            opt.zero_grad()
+            o = dm(x)
+            (F.nll_loss(o, y.cuda()) if model_name == "lenet5" else F.cross_entropy(o, y.cuda())).backward()
+            opt.step()
+        torch.cuda.synchronize()
+        out.append(torch.cat([p.detach().reshape(-1).cpu() for p in m.parameters()]))
+        if wrap:
+            assert len(dm.buckets) > 1
+    if model_name == "mlp":
+        assert torch.equal(out[0], out[1])
+    else:  # MIOpen's conv weight-gradient kernels are not run-to-run deterministic
+        assert torch.allclose(out[0], out[1], rtol=1e-5, atol=1e-6), (out[0] - out[1]).abs().max()
+    assert comm.async_error() == ""
+
+
 def _run(args, cwd, timeout=600):
     r = subprocess.run([sys.executable] + args, cwd=cwd, env=dict(os.environ, PYTHONPATH=ROOT),
                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=timeout)
