@@ -2,6 +2,7 @@
 // Device buffers are owned by torch (HBM via its caching allocator) and passed as raw
 // addresses; streams are passed as the integer handles of torch.cuda.Stream.cuda_stream.
 #include <pybind11/pybind11.h>
+#include <stdexcept>
 #include <pybind11/stl.h>
 
 #include "kernels/launch.h"
@@ -29,6 +30,18 @@ PYBIND11_MODULE(_C, m) {
     return std::string(p.gcnArchName);
   });
   m.def("rccl_version", &RcclComm::version);
+  // x[r] = normalize(images[idx[r]]) for r < B, fp32 (dtype 0) or bf16 (1), rows ld elements apart.
+  // `zero` is a device int32 holding 0 (the kernel addresses idx through a device step counter).
+  m.def("gather_normalize", [](int dtype, uintptr_t images, uintptr_t idx, uintptr_t zero, int B, uintptr_t out,
+                               int ld, uintptr_t stream) {
+    if (B <= 0) return;
+    if (ld < 784) throw std::invalid_argument("gather_normalize: ld must be >= 784");
+    BatchRef br{reinterpret_cast<const uint8_t*>(images), nullptr, reinterpret_cast<const int32_t*>(idx),
+                reinterpret_cast<const int32_t*>(zero), 0, B};
+    launch_gather_normalize(static_cast<DType>(dtype), br, reinterpret_cast<void*>(out), ld,
+                            reinterpret_cast<hipStream_t>(stream));
+    HIP_CHECK(hipGetLastError());
+  });
 
   py::class_<TrainerPtrs>(m, "TrainerPtrs")
       .def(py::init<>())

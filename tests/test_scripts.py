@@ -54,3 +54,12 @@ def test_launcher_propagates_failure(tmp_path):
     r = subprocess.run([sys.executable, "-m", "pytorch_ddp_mnist_amd.parallel.launch", "-n", "2", "--",
                         sys.executable, "-c", code], cwd=tmp_path, env=ENV, timeout=25)
     assert r.returncode == 3
+
+
+def test_byo_model_example_two_ranks(tmp_path):
+    """examples/byo_model_ddp.py: user model + DistributedDataParallel + device loaders, 2 gloo ranks."""
+    out = _run(["-m", "pytorch_ddp_mnist_amd.parallel.launch", "-n", "2", "--style", "torch", "--timeout", "240",
+                "--", sys.executable, os.path.join(ROOT, "examples", "byo_model_ddp.py"), "--device", "cpu",
+                "--limit", "3000"], tmp_path)
+    m = re.findall(r"^Epoch=0, top1=(\d\.\d+)$", out, re.M)
+    assert len(m) == 1 and float(m[0]) > 0.5, out  # rank 0 prints
