@@ -19,6 +19,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("model_conv_params", [](int model) { return model_conv_params(static_cast<ModelKind>(model)); });
   m.def("model_pack_size", [](int model) { return model_pack_size(static_cast<ModelKind>(model)); });
   m.def("conv_bwd_blocks", &lenet_conv_bwd_blocks);
+  m.attr("L1_KSPLIT") = L1_KSPLIT;
+  m.attr("L1_SPLIT_MAX_B") = L1_SPLIT_MAX_B;
   m.def("device_count", [] {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -47,7 +49,7 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init<>())
 #define RW(f) .def_readwrite(#f, &TrainerPtrs::f)
       RW(images) RW(labels) RW(idx) RW(step) RW(params) RW(grad) RW(mom) RW(pack) RW(slab_fc) RW(slab_conv)
-      RW(metrics) RW(xT) RW(h1T) RW(h2T) RW(dy1T) RW(dy2T) RW(dy3T) RW(p1) RW(m1) RW(p2) RW(m2) RW(dp2);
+      RW(metrics) RW(xT) RW(h1T) RW(h2T) RW(dy1T) RW(dy2T) RW(dy3T) RW(p1) RW(m1) RW(p2) RW(m2) RW(dp2) RW(z1p);
 #undef RW
 
   py::class_<Bucket>(m, "Bucket")

@@ -16,6 +16,7 @@
 // Every product is a 16x16 MFMA tile loop (common.h); epilogues fuse bias, ReLU, dropout
 // masks, padding and the transposed global stores.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "launch.h"
@@ -51,8 +52,8 @@ DEV void store_col4(T* base, float a, float b, float c, float d) {
   }
 }
 
-template <typename T, class H, int MT, bool TRAIN>
-__global__ __launch_bounds__(256) void head_kernel(BatchRef br, HeadBuffers hb) {
+template <typename T, class H, int MT, bool TRAIN, bool PRE, int NWV = 4>
+__global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers hb) {
   using S = HeadSmem<T, H, MT>;
   using M = Mma<T>;
   using Frag = typename M::Frag;
@@ -81,10 +82,12 @@ __global__ __launch_bounds__(256) void head_kernel(BatchRef br, HeadBuffers hb) 
   __syncthreads();
 
   // ---------------------------------------------------------------- stage the input tile
-  if constexpr (H::GATHER) {
+  // (PRE: layer 1 already ran in l1_split_kernel, which also wrote xT; X itself is not needed)
+  if constexpr (PRE) {
+  } else if constexpr (H::GATHER) {
     constexpr int CH = H::K0P / 8;
     T* xT = reinterpret_cast<T*>(hb.xT);
-    for (int e = tid; e < R * CH; e += 256) {
+    for (int e = tid; e < R * CH; e += NWV * 64) {
       const int r = e % R, k = (e / R) * 8;
       const int s = sIdx[r];
       float v[8];
@@ -111,7 +114,7 @@ __global__ __launch_bounds__(256) void head_kernel(BatchRef br, HeadBuffers hb) 
     constexpr int CH = H::K0P / VE;
     const T* xin = reinterpret_cast<const T*>(hb.xin);
     T* xT = reinterpret_cast<T*>(hb.xT);
-    for (int e = tid; e < R * CH; e += 256) {
+    for (int e = tid; e < R * CH; e += NWV * 64) {
       const int r = e % R, k = (e / R) * VE;
       uint4 u = make_uint4(0, 0, 0, 0);
       if (r0 + r < B) u = *reinterpret_cast<const uint4*>(xin + (size_t)(r0 + r) * H::K0P + k);
@@ -129,10 +132,28 @@ __global__ __launch_bounds__(256) void head_kernel(BatchRef br, HeadBuffers hb) 
   const uint32_t drop_thr = H::DROPOUT ? (uint32_t)(hb.drop_p * 4294967295.0f) : 0u;
 
   // ---------------------------------------------------------------- L1: H1 = relu(X W1^T + b1)
-  {
+  if constexpr (PRE) {
+    // sum the L1_KSPLIT partial products in a fixed order, then the same bias/ReLU/dropout epilogue
+    T* h1T = reinterpret_cast<T*>(hb.h1T);
+    const float* zp = hb.z1p;
+    for (int e = tid; e < H::N1P * R; e += NWV * 64) {
+      const int n = e / R, r = e % R, rg = r0 + r;
+      float z = 0.f;
+#pragma unroll
+      for (int q = 0; q < L1_KSPLIT; ++q) z += zp[((size_t)q * H::N1P + n) * ldB + rg];
+      float x = fmaxf(z + (n < H::N1 ? prm[H::B1 + n] : 0.f), 0.f);
+      if constexpr (H::DROPOUT && TRAIN) {
+        const uint32_t h = hash4(hb.seed, (uint32_t)gstep, (uint32_t)rg, (uint32_t)n);
+        x = (h >= drop_thr) ? x * keep_scale : 0.f;
+      }
+      if (n >= H::N1 || rg >= B) x = 0.f;
+      sH1[r * S::P1 + n] = to_t<T>(x);
+      if constexpr (TRAIN) h1T[(size_t)n * ldB + rg] = to_t<T>(x);
+    }
+  } else {
     constexpr int NT = H::N1P / 16, KCH = H::K0P / KC;
     T* h1T = reinterpret_cast<T*>(hb.h1T);
-    for (int nt = w; nt < NT; nt += 4) {
+    for (int nt = w; nt < NT; nt += NWV) {
       f32x4 acc[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = zero4();
@@ -172,7 +193,7 @@ __global__ __launch_bounds__(256) void head_kernel(BatchRef br, HeadBuffers hb) 
   {
     constexpr int NT = H::N2P / 16, KCH = H::N1P / KC;
     T* h2T = reinterpret_cast<T*>(hb.h2T);
-    for (int nt = w; nt < NT; nt += 4) {
+    for (int nt = w; nt < NT; nt += NWV) {
       f32x4 acc[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = zero4();
@@ -207,7 +228,7 @@ __global__ __launch_bounds__(256) void head_kernel(BatchRef br, HeadBuffers hb) 
   // ---------------------------------------------------------------- L3: logits = H2 W3^T (+ b3)
   {
     constexpr int KCH = H::N2P / KC;
-    for (int m = w; m < MT; m += 4) {
+    for (int m = w; m < MT; m += NWV) {
       f32x4 acc = zero4();
       const T* bp = pack + H::F3 + row * H::N2P + grp * KV;
       const T* ap = sH2 + (m * 16 + row) * S::P2 + grp * KV;
@@ -272,7 +293,7 @@ __global__ __launch_bounds__(256) void head_kernel(BatchRef br, HeadBuffers hb) 
   {
     constexpr int NT = H::N2P / 16, KCH = H::NCK / KC;
     T* dy2T = reinterpret_cast<T*>(hb.dy2T);
-    for (int nt = w; nt < NT; nt += 4) {
+    for (int nt = w; nt < NT; nt += NWV) {
       f32x4 acc[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = zero4();
@@ -306,7 +327,7 @@ __global__ __launch_bounds__(256) void head_kernel(BatchRef br, HeadBuffers hb) 
   {
     constexpr int NT = H::N1P / 16, KCH = H::N2P / KC;
     T* dy1T = reinterpret_cast<T*>(hb.dy1T);
-    for (int nt = w; nt < NT; nt += 4) {
+    for (int nt = w; nt < NT; nt += NWV) {
       f32x4 acc[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = zero4();
@@ -340,7 +361,7 @@ __global__ __launch_bounds__(256) void head_kernel(BatchRef br, HeadBuffers hb) 
     __syncthreads();
     constexpr int NT = rup(H::K0, 16) / 16, KCH = H::N1P / KC;
     T* dx = reinterpret_cast<T*>(hb.dx);
-    for (int nt = w; nt < NT; nt += 4) {
+    for (int nt = w; nt < NT; nt += NWV) {
       f32x4 acc[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = zero4();
@@ -363,6 +384,71 @@ __global__ __launch_bounds__(256) void head_kernel(BatchRef br, HeadBuffers hb) 
       }
     }
   }
+}
+
+// ====================================================================================
+// Small-batch layer 1: Z1 partial[q] = X[:, Kq] W1[:, Kq]^T over a (16-row tile, 64-column group,
+// K quarter) grid, so a B=128 step spreads the 784-deep GEMM over 64 workgroups instead of 8.
+// The X tile (gathered + normalised for the MLP, pool2 rows for LeNet) is staged once in LDS and
+// shared by the 4 waves (one 16-column tile each); the n-group-0 blocks also write X^T for the
+// wgrad GEMM.  Partials are stored transposed, [q][n][ldB], one 16-byte store per lane.
+// ====================================================================================
+template <typename T, class H, bool TRAIN>
+__global__ __launch_bounds__(256) void l1_split_kernel(BatchRef br, HeadBuffers hb) {
+  using M = Mma<T>;
+  constexpr int KV = M::KV, KC = M::KC;
+  constexpr int KCH = H::K0P / KC, QCH = (KCH + L1_KSPLIT - 1) / L1_KSPLIT;
+  constexpr int XP = QCH * KC + 8;
+  __shared__ __attribute__((aligned(16))) T sX[16 * XP];
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
+  const int r0 = blockIdx.x * 16, ng = blockIdx.y, q = blockIdx.z;
+  const int c0 = q * QCH, c1 = min(KCH, c0 + QCH);
+  if (c0 >= c1) return;  // uniform per block
+  const int k0 = c0 * KC, klen = (c1 - c0) * KC;
+  const int B = br.B, ldB = hb.ldB;
+  T* xT = reinterpret_cast<T*>(hb.xT);
+  const bool write_xT = TRAIN && ng == 0;
+
+  for (int e = tid; e < 16 * (klen / 8); e += 256) {
+    const int r = e & 15, kk = (e >> 4) * 8, k = k0 + kk, rg = r0 + r;
+    float v[8];
+    if constexpr (H::GATHER) {
+      if (rg < B && k < H::K0) {
+        const int32_t* idx = br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride;
+        const uint2 u = *reinterpret_cast<const uint2*>(br.images + (size_t)idx[rg] * 784 + k);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v[j] = mnist_norm((u.x >> (8 * j)) & 255u);
+          v[j + 4] = mnist_norm((u.y >> (8 * j)) & 255u);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = 0.f;
+      }
+    } else {
+      const T* xin = reinterpret_cast<const T*>(hb.xin);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = rg < B ? to_f(xin[(size_t)rg * H::K0P + k + j]) : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sX[r * XP + kk + j] = to_t<T>(v[j]);
+    if (write_xT) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xT[(size_t)(k + j) * ldB + rg] = to_t<T>(v[j]);
+    }
+  }
+  __syncthreads();
+
+  const int nt = ng * 4 + w;
+  if (nt * 16 >= H::N1P) return;
+  const T* pack = reinterpret_cast<const T*>(hb.pack);
+  const T* bp = pack + H::F1 + (size_t)(nt * 16 + row) * H::K0P + grp * KV;
+  const T* ap = sX + row * XP + grp * KV;
+  f32x4 acc = zero4();
+#pragma unroll 4
+  for (int c = c0; c < c1; ++c) M::mma(acc, M::load(ap + (c - c0) * KC), M::load(bp + c * KC));
+  float* out = hb.z1p + ((size_t)q * H::N1P + nt * 16 + row) * ldB + r0 + grp * 4;
+  *reinterpret_cast<f32x4*>(out) = acc;
 }
 
 // ====================================================================================
@@ -495,14 +581,45 @@ void head_launch_mt(bool train, const BatchRef& br, const HeadBuffers& hb, hipSt
   const int rows = rup(br.B, 32);
   const int grid = (rows + MT * 16 - 1) / (MT * 16);
   if (train)
-    hipLaunchKernelGGL((head_kernel<T, H, MT, true>), dim3(grid), dim3(256), 0, s, br, hb);
+    hipLaunchKernelGGL((head_kernel<T, H, MT, true, false>), dim3(grid), dim3(256), 0, s, br, hb);
   else
-    hipLaunchKernelGGL((head_kernel<T, H, MT, false>), dim3(grid), dim3(256), 0, s, br, hb);
+    hipLaunchKernelGGL((head_kernel<T, H, MT, false, false>), dim3(grid), dim3(256), 0, s, br, hb);
+}
+
+// small-batch path: layer-1 split GEMM, then the head with 16-row tiles consuming the partials;
+// with only B/16 workgroups, each gets SPLIT_NWV waves so every N-tile of a layer has its own wave
+#ifndef SPLIT_NWV
+#define SPLIT_NWV 16  // swept 4 / 8 / 16: 40.8 / 37.4 / 36.7 us per MLP fp32 B=128 step
+#endif
+template <typename T, class H, int NWV>
+void head_launch_split_w(bool train, const BatchRef& br, const HeadBuffers& hb, hipStream_t s) {
+  const int mt = (br.B + 15) / 16;
+  const dim3 g1(mt, (H::N1P / 16 + 3) / 4, L1_KSPLIT);
+  const int grid = (rup(br.B, 32) + 15) / 16;
+  if (train) {
+    hipLaunchKernelGGL((l1_split_kernel<T, H, true>), g1, dim3(256), 0, s, br, hb);
+    hipLaunchKernelGGL((head_kernel<T, H, 1, true, true, NWV>), dim3(grid), dim3(NWV * 64), 0, s, br, hb);
+  } else {
+    hipLaunchKernelGGL((l1_split_kernel<T, H, false>), g1, dim3(256), 0, s, br, hb);
+    hipLaunchKernelGGL((head_kernel<T, H, 1, false, true, NWV>), dim3(grid), dim3(NWV * 64), 0, s, br, hb);
+  }
+}
+
+template <typename T, class H>
+void head_launch_split(bool train, const BatchRef& br, const HeadBuffers& hb, hipStream_t s) {
+  static const int nwv = [] {
+    const char* e = std::getenv("MNIST_AMD_SPLIT_NWV");  // tuning knob: 4 / 8 / 16 waves
+    return e ? std::atoi(e) : SPLIT_NWV;
+  }();
+  if (nwv == 16) head_launch_split_w<T, H, 16>(train, br, hb, s);
+  else if (nwv == 4) head_launch_split_w<T, H, 4>(train, br, hb, s);
+  else head_launch_split_w<T, H, 8>(train, br, hb, s);
 }
 
 template <typename T, class H>
 void head_launch_t(bool train, const BatchRef& br, const HeadBuffers& hb, int rows, hipStream_t s) {
-  if (rows <= 16) head_launch_mt<T, H, 1>(train, br, hb, s);
+  if (hb.z1p && br.B <= L1_SPLIT_MAX_B && !std::getenv("MNIST_AMD_NO_L1_SPLIT")) head_launch_split<T, H>(train, br, hb, s);
+  else if (rows <= 16) head_launch_mt<T, H, 1>(train, br, hb, s);
   else if (rows <= 32 || !HeadSmem<T, H, 4>::FITS) {
     if constexpr (HeadSmem<T, H, 2>::FITS) head_launch_mt<T, H, 2>(train, br, hb, s);
     else head_launch_mt<T, H, 1>(train, br, hb, s);

@@ -31,6 +31,7 @@ struct HeadBuffers {
   void* dy3T;            // [16][ldB]
   void* dx;              // LeNet: dp2 [B][K0P]
   float* metrics;        // [loss_sum, correct, count]
+  float* z1p;            // [L1_KSPLIT][N1P][ldB] fp32 layer-1 partial sums (small-batch split path) or null
   int32_t ldB;
   uint32_t seed;
   float drop_p;
@@ -49,6 +50,10 @@ struct LenetConvBuffers {
 };
 
 int head_rows_per_block(ModelKind m, DType t, int B);
+// Small batches (B <= L1_SPLIT_MAX_B) run layer 1 as a separate many-workgroup GEMM split L1_KSPLIT
+// ways over K (the head kernel alone would put the whole 784-deep GEMM on B/16 CUs).
+constexpr int L1_KSPLIT = 4;
+constexpr int L1_SPLIT_MAX_B = 1024;
 
 void launch_head(ModelKind m, DType t, bool train, const BatchRef& br, const HeadBuffers& hb,
                  int rows_per_block, hipStream_t s);

@@ -98,6 +98,7 @@ HeadBuffers Trainer::head_buffers(float* metrics) const {
   hb.dy3T = ptr<void>(p_.dy3T);
   hb.dx = ptr<void>(p_.dp2);
   hb.metrics = metrics;
+  hb.z1p = ptr<float>(p_.z1p);
   hb.ldB = ldb_;
   hb.seed = seed_;
   hb.drop_p = drop_p_;

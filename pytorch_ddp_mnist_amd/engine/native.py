@@ -94,6 +94,8 @@ class NativeTrainer:
             self.dp2 = z(self.ld_b, 416)
         else:
             self.p1 = self.m1 = self.p2 = self.m2 = self.dp2 = None
+        # layer-1 K-split partials for the small-batch path (csrc/kernels/head.hip l1_split_kernel)
+        self.z1p = z(C.L1_KSPLIT * N1P * self.ld_b, dt=torch.float32) if self.batch <= C.L1_SPLIT_MAX_B else None
 
         P = C.TrainerPtrs()
         ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
@@ -103,6 +105,7 @@ class NativeTrainer:
         P.xT, P.h1T, P.h2T = ptr(self.xT), ptr(self.h1T), ptr(self.h2T)
         P.dy1T, P.dy2T, P.dy3T = ptr(self.dy1T), ptr(self.dy2T), ptr(self.dy3T)
         P.p1, P.m1, P.p2, P.m2, P.dp2 = ptr(self.p1), ptr(self.m1), ptr(self.p2), ptr(self.m2), ptr(self.dp2)
+        P.z1p = ptr(self.z1p)
         self._ptrs = P
         self.rt = C.Trainer(mid, did, self.batch, self.ld_b, fc_splits, P)
         self.rt.set_optimizer(float(lr), float(momentum))
