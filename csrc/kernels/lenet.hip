@@ -51,6 +51,9 @@ DEV typename Mma<T>::Frag ones_frag() {
 // LDS: xs8[s][y][x] = xpad[y][x+s] for s = 0..7 (8 shifted copies of the zero-padded 32x32
 // input) so that any run of KV consecutive taps of one kernel row, starting at any column, is
 // an ALIGNED 16-byte read: conv1's im2col A fragment with k = kh*8 + kw is one ds_read_b128.
+// (Measured alternative: ONE un-shifted copy read with under-aligned ds_read_b128 -- legal on
+// gfx950 -- makes the stage 1 store/thread instead of 32, but conv_fwd goes 50 -> 120 us: the
+// under-aligned 16-byte LDS reads are far slower than the extra stores.)
 template <typename T>
 struct FwdSmem {
   static constexpr int XP = 1048;  // plane pitch (32x32 + pad): 2-way worst-case conflicts (was 8-way at 1024)
@@ -59,7 +62,9 @@ struct FwdSmem {
   static constexpr int OFF_M1 = rup(OFF_P1 + 196 * 8 * (int)sizeof(T), 16);  // [196][8] u8 pool1 codes
   static constexpr int OFF_P2 = rup(OFF_M1 + 196 * 8, 16);                // [400] T      pool2 output (NCHW)
   static constexpr int OFF_M2 = rup(OFF_P2 + 400 * (int)sizeof(T), 16);   // [400] u8     pool2 codes
-  static constexpr int TOTAL = rup(OFF_M2 + 400, 16);
+  static constexpr int W2P = 232;                                          // C2F row pitch (224 + 8)
+  static constexpr int OFF_W2 = rup(OFF_M2 + 400, 16);                     // [16][W2P] T  conv2 B operand
+  static constexpr int TOTAL = rup(OFF_W2 + 16 * W2P * (int)sizeof(T), 16);
 };
 
 // Coalesced 16-byte copy of a staged LDS image to global memory (both 16-byte aligned).
@@ -69,7 +74,7 @@ DEV void copy_out16(void* dst, const void* src, int bytes) {
 }
 
 template <typename T, bool TRAIN>
-__global__ __launch_bounds__(256) void conv_fwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void conv_fwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
   using M = Mma<T>;
   using Frag = typename M::Frag;
   using S = FwdSmem<T>;
@@ -87,11 +92,19 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(BatchRef br, LenetConvBuf
 
   constexpr int C1CH = 64 / KC;                 // conv1 K = 5 rows x 8 (kw padded)
   constexpr int C2CH = (25 * 8 + KC - 1) / KC;  // conv2 K = 25 taps x 8 ch (7 bf16 / 13 f32 chunks)
-  Frag b1[C1CH], b2[C2CH];
+  // conv1's B operand lives in registers; conv2's (7 chunks) is staged once per block in LDS, which
+  // keeps the kernel at <= 128 registers (4 waves per SIMD: the whole 1024-block grid co-resident)
+  T* w2s = reinterpret_cast<T*>(smem + S::OFF_W2);
+  Frag b1[C1CH];
 #pragma unroll
   for (int kc = 0; kc < C1CH; ++kc) b1[kc] = M::load(pack + L::C1 + row * 64 + kc * KC + grp * KV);
-#pragma unroll
-  for (int kc = 0; kc < C2CH; ++kc) b2[kc] = M::load(pack + L::C2F + row * 224 + kc * KC + grp * KV);
+  {
+    constexpr int VE = 16 / (int)sizeof(T);
+    for (int e = tid; e < 16 * 224 / VE; e += 256) {
+      const int r = e / (224 / VE), c = (e % (224 / VE)) * VE;
+      *reinterpret_cast<uint4*>(w2s + r * S::W2P + c) = *reinterpret_cast<const uint4*>(pack + L::C2F + r * 224 + c);
+    }
+  }
   const float bias1 = row < 6 ? prm[L::CB1 + row] : 0.f;
   const float bias2 = prm[L::CB2 + row];
 
@@ -133,7 +146,7 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(BatchRef br, LenetConvBuf
       else { pos = kc * 2 + (grp >> 1); c0 = (grp & 1) * 4; }
       pos = min(pos, 24);
       const int kh = pos / 5, kw = pos % 5;
-      M::mma(acc, M::load(p1s + base + (kh * 14 + kw) * 8 + c0), b2[kc]);
+      M::mma(acc, M::load(p1s + base + (kh * 14 + kw) * 8 + c0), M::load(w2s + row * S::W2P + kc * KC + grp * KV));
     }
   };
   auto c2_epi = [&](int mt, const f32x4& acc) {
@@ -158,29 +171,78 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(BatchRef br, LenetConvBuf
 
   zero_lds<T>(xs, 8 * S::XP);
   // software pipeline: image t+1's pixels are in flight (registers) while image t computes
-  auto fetch = [&](int t) -> uint32_t {
+  // Stage mapping: thread (y, g, h), y = 2..29 padded row, g = 8-column group, h = plane half.
+  // It fetches the dword-aligned 20-byte window [8g-4, 8g+16) of image row y-2 (pixel at padded
+  // column 8g+i is window byte i+2), normalises its 16 pixels once, and writes planes 4h..4h+3 as
+  // ALIGNED 16-byte stores: xs[s][y][8g..8g+7] = xpad[y][8g+s..8g+s+7].  Rows 0,1,30,31 stay zero.
+  struct Raw { uint32_t d[5]; };
+  const int sy = 2 + (tid >> 3), sg = (tid >> 1) & 3, sh = tid & 1;
+  auto fetch = [&](int t) -> Raw {  // software pipeline: image t+1's bytes are in flight during image t
+    Raw r{{0u, 0u, 0u, 0u, 0u}};
     const int bb = blockIdx.x * ipb + t;
-    if (tid >= 196 || t >= ipb || bb >= br.B) return 0u;
-    return *reinterpret_cast<const uint32_t*>(br.images + (size_t)idx[bb] * 784 + tid * 4);
+    if (tid >= 224 || t >= ipb || bb >= br.B) return r;
+    const uint8_t* rowp = br.images + (size_t)idx[bb] * 784 + (sy - 2) * 28;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int c = 8 * sg - 4 + 4 * k;
+      if (c >= 0 && c < 28) r.d[k] = *reinterpret_cast<const uint32_t*>(rowp + c);
+    }
+    return r;
   };
-  uint32_t u_next = fetch(0);
+  Raw u_next = fetch(0);
   __syncthreads();
   for (int t = 0; t < ipb; ++t) {
     const int b = blockIdx.x * ipb + t;
     const bool valid = b < br.B;
-    const uint32_t u = u_next;
+    const Raw u = u_next;
     u_next = fetch(t + 1);
     flush_p2(t > 0 ? b - 1 : -1);
-    // ---- stage: normalise, scattered into the 8 shifted copies
-    if (tid < 196 && !(cb.ablate & 1)) {
-      const int k = tid * 4, y = k / 28 + 2, x = k % 28 + 2;
+    // ---- stage: normalise once, 4 aligned 16-byte plane stores per thread
+    if (tid < 224 && !(cb.ablate & 1)) {
+      float f[16];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const T v = to_t<T>(valid ? mnist_norm((u >> (8 * j)) & 255u) : 0.f);
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t byte = (u.d[(i + 2) >> 2] >> (8 * ((i + 2) & 3))) & 255u;
+        const bool in = valid && (unsigned)(8 * sg - 2 + i) < 28u;  // zero padding is 0 AFTER normalising
+        f[i] = in ? mnist_norm(byte) : 0.f;
+      }
+      T* dst = xs + sy * 32 + 8 * sg;
+      if constexpr (sizeof(T) == 2) {
+        // packed pairs D[k] = (v[2k], v[2k+1]); E = window for this thread's plane half (sh);
+        // even planes are dword-aligned slices of E, odd planes one alignbyte per dword
+        uint32_t D[8], E[6];
 #pragma unroll
-        for (int s8 = 0; s8 < 8; ++s8) {
-          const int xx = x + j - s8;
-          if (xx >= 0) xs[s8 * S::XP + y * 32 + xx] = v;
+        for (int k = 0; k < 8; ++k) {
+          bf16x2 p2v;
+          p2v[0] = (bf16)f[2 * k];
+          p2v[1] = (bf16)f[2 * k + 1];
+          D[k] = __builtin_bit_cast(uint32_t, p2v);
+        }
+        const uint32_t msk = 0u - (uint32_t)sh;  // bit blend: a ?: select here becomes scratch-indexed D
+#pragma unroll
+        for (int j = 0; j < 6; ++j) E[j] = (D[j] & ~msk) | (D[j + 2] & msk);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          uint4 o;
+          uint32_t* ov = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (q == 0) ov[j] = E[j];
+            else if (q == 1) ov[j] = __builtin_amdgcn_alignbyte(E[j + 1], E[j], 2);
+            else if (q == 2) ov[j] = E[j + 1];
+            else ov[j] = __builtin_amdgcn_alignbyte(E[j + 2], E[j + 1], 2);
+          }
+          *reinterpret_cast<uint4*>(dst + (4 * sh + q) * S::XP) = o;
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float o[8];
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] = sh ? f[i + 4 + q] : f[i + q];
+          float* d = reinterpret_cast<float*>(dst) + (4 * sh + q) * S::XP;
+          *reinterpret_cast<f32x4*>(d) = f32x4{o[0], o[1], o[2], o[3]};
+          *reinterpret_cast<f32x4*>(d + 4) = f32x4{o[4], o[5], o[6], o[7]};
         }
       }
     }
@@ -188,19 +250,39 @@ __global__ __launch_bounds__(256) void conv_fwd_kernel(BatchRef br, LenetConvBuf
 
     // ---- conv1 + bias + ReLU + maxpool: 14 pooled rows per wave, in pairs
     if (!(cb.ablate & 2)) {
-#pragma unroll 1
+      // software pipeline: pair j+2's fragments are loaded and pair j's MFMAs issued BEFORE pair
+      // j-2's epilogue (the compiler cannot hoist xs loads over the epilogue's p1s stores itself)
+      Frag fa[C1CH], fb[C1CH];
+#pragma unroll
+      for (int kc = 0; kc < C1CH; ++kc) {
+        fa[kc] = M::load(xs + c1base[kc]);
+        fb[kc] = M::load(xs + c1base[kc] + 64);
+      }
+      f32x4 pA = zero4(), pB = zero4();
+#pragma unroll
       for (int j = 0; j < 14; j += 2) {
         f32x4 accA = zero4(), accB = zero4();
 #pragma unroll
         for (int kc = 0; kc < C1CH; ++kc) {
-          const Frag fa = M::load(xs + c1base[kc] + j * 64);
-          const Frag fb = M::load(xs + c1base[kc] + j * 64 + 64);
-          M::mma(accA, fa, b1[kc]);
-          M::mma(accB, fb, b1[kc]);
+          M::mma(accA, fa[kc], b1[kc]);
+          M::mma(accB, fb[kc], b1[kc]);
         }
-        c1_epi(j, accA);
-        c1_epi(j + 1, accB);
+        if (j + 2 < 14) {
+#pragma unroll
+          for (int kc = 0; kc < C1CH; ++kc) {
+            fa[kc] = M::load(xs + c1base[kc] + (j + 2) * 64);
+            fb[kc] = M::load(xs + c1base[kc] + (j + 2) * 64 + 64);
+          }
+        }
+        if (j > 0) {
+          c1_epi(j - 2, pA);
+          c1_epi(j - 1, pB);
+        }
+        pA = accA;
+        pB = accB;
       }
+      c1_epi(12, pA);
+      c1_epi(13, pB);
     }
     __syncthreads();
 

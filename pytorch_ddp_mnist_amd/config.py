@@ -57,6 +57,7 @@ class TrainConfig:
     local_rank: Optional[int] = None
     shard_eval: bool = False
     sampler: str = "torch"      # "torch" (bit-equal DistributedSampler) | "device"
+    resume: Optional[str] = None  # params + momentum + epoch file: loaded if present, rewritten each epoch
 
     def to_nested(self) -> dict:
         """Nested dict in the reference layout (mnist_cpu_mp.py:223-241)."""
@@ -103,11 +104,13 @@ def _add_extra_flags(p: argparse.ArgumentParser, defaults: TrainConfig) -> None:
     add("--tqdm", action="store_true", help="show progress bars (reference DISABLE_TQDM=True is ignored there)")
     add("--shard_eval", action="store_true", help="shard the test set across ranks (reference: every rank evaluates all)")
     add("--sampler", type=str, default=None, choices=["torch", "device"])
+    add("--resume", type=str, default=None,
+        help="resume file (params + momentum + epoch): loaded when it exists, rewritten after every epoch")
 
 
 def _apply_extra(cfg: TrainConfig, a: argparse.Namespace) -> None:
     for name in ("model", "dtype", "lr", "momentum", "dropout", "seed", "init_seed", "data_format",
-                 "device", "bucket_cap_kb", "comm", "save_path", "metrics_jsonl", "sampler"):
+                 "device", "bucket_cap_kb", "comm", "save_path", "metrics_jsonl", "sampler", "resume"):
         v = getattr(a, name, None)
         if v is not None:
             setattr(cfg, name, v)

@@ -20,6 +20,7 @@ from ..data.datasets import normalize_batch
 from ..data.sampler import batch_slices
 from ..models import build_model
 from ..parallel.ddp import GlooReducer, model_phases, plan_buckets
+from ..utils.fault import FaultInjector
 
 
 @dataclass
@@ -65,6 +66,7 @@ class TorchCPUEngine:
         cap = None if bucket_cap_kb is None else bucket_cap_kb * 1024
         self.reducer = GlooReducer(self.module, world, plan_buckets(model_phases(model), cap))
         self.crit = F.nll_loss if model == "lenet5" else F.cross_entropy
+        self.fault = FaultInjector(int(os.environ.get("RANK", "0")))
 
     def train_epoch(self, indices: torch.Tensor, progress=None) -> EpochResult:
         r = EpochResult()
@@ -80,6 +82,7 @@ class TorchCPUEngine:
             loss.backward()
             self.reducer.sync_grads()
             self.opt.step()
+            self.fault.tick()
             lv = float(loss.item()) * b
             r.loss_sum += lv
             r.correct += float((out.argmax(1) == y).sum())
@@ -116,6 +119,24 @@ class TorchCPUEngine:
 
     def state_dict(self):
         return {k: v.detach().clone() for k, v in self.module.state_dict().items()}
+
+    # resume: flat params (state_dict order) + flat SGD momentum buffers (zeros before the first step)
+    def get_state(self):
+        params = torch.cat([p.detach().reshape(-1) for p in self.module.parameters()])
+        bufs = [self.opt.state.get(p, {}).get("momentum_buffer") for p in self.module.parameters()]
+        mom = torch.cat([(b if b is not None else torch.zeros_like(p)).reshape(-1)
+                         for b, p in zip(bufs, self.module.parameters())])
+        return params, mom
+
+    def set_state(self, params: torch.Tensor, mom) -> None:
+        off = 0
+        with torch.no_grad():
+            for p in self.module.parameters():
+                n = p.numel()
+                p.copy_(params[off:off + n].view_as(p))
+                if mom is not None and self.opt.defaults.get("momentum", 0) != 0:
+                    self.opt.state[p]["momentum_buffer"] = mom[off:off + n].view_as(p).clone()
+                off += n
 
     def finish(self) -> None:
         pass

@@ -20,7 +20,8 @@ from ..data.sampler import epoch_indices
 from ..models import build_model
 from ..parallel.comm import DistContext, init_distributed
 from ..parallel.ddp import model_phases, plan_buckets
-from ..utils.checkpoint import save_model
+from ..utils.checkpoint import load_resume, save_model, save_resume
+from ..utils.fault import FaultInjector, check_finite
 from ..utils.logging import MetricsWriter, banner, epoch_line, reference_epoch_loss
 from ..utils.profiling import enable as enable_roctx, range_
 from .reference import EpochResult, TorchCPUEngine
@@ -52,8 +53,20 @@ class NativeEngine:
             dist.broadcast(self.tr.params, 0)
             self.tr.load_flat(self.tr.params.clone())
         self.use_graph = cfg.graph and not self.torch_comm
+        self.fault = FaultInjector(ctx.rank)
+
+    def get_state(self):
+        self.tr.synchronize()
+        return self.tr.params.detach().cpu().clone(), self.tr.mom.detach().cpu().clone()
+
+    def set_state(self, params: torch.Tensor, mom) -> None:
+        self.tr.load_flat(params)
+        if mom is not None:
+            self.tr.mom.copy_(mom.to(self.tr.mom.device))
+        self.tr.synchronize()
 
     def _step(self, b: int) -> None:
+        self.fault.tick()
         if self.torch_comm:
             import torch.distributed as dist
             self.tr.forward_backward(b)
@@ -166,7 +179,16 @@ def run(cfg: TrainConfig, entry: str = "ddp_tutorial_cpu", show_banner: bool = F
     metrics = MetricsWriter(cfg.metrics_jsonl, ctx.rank)
     ntest = len(yte)
     history = []
-    for i in range(cfg.n_epochs):
+    start = 0
+    if cfg.resume and os.path.exists(cfg.resume):
+        st = load_resume(cfg.resume)
+        if st.get("model") != cfg.model:
+            raise ValueError(f"resume file {cfg.resume} holds a {st.get('model')} model, not {cfg.model}")
+        engine.set_state(st["params"], st.get("momentum"))
+        start = int(st["epoch"]) + 1
+        if ctx.rank == 0:
+            print(f"=> resumed from {cfg.resume} after epoch {st['epoch']}", flush=True)
+    for i in range(start, cfg.n_epochs):
         idx = epoch_indices(len(ytr), ctx.world, ctx.rank, i, cfg.seed)
         with range_(f"epoch{i}.train"):
             tr = engine.train_epoch(idx)
@@ -176,6 +198,7 @@ def run(cfg: TrainConfig, entry: str = "ddp_tutorial_cpu", show_banner: bool = F
             tidx = torch.arange(ntest)
         with range_(f"epoch{i}.eval"):
             ev = engine.evaluate(tidx)
+        check_finite(f"epoch {i} training loss", tr.loss_sum)
         train_loss = reference_epoch_loss(tr.full_sum, tr.n_full, cfg.batch_size, tr.last_sum, tr.last_b)
         val_loss = reference_epoch_loss(ev.full_sum, ev.n_full, cfg.batch_size, ev.last_sum, ev.last_b)
         print(epoch_line(i, train_loss, val_loss), flush=True)
@@ -191,6 +214,10 @@ def run(cfg: TrainConfig, entry: str = "ddp_tutorial_cpu", show_banner: bool = F
                   f"val_loss={rec['val_loss_mean']:.4f} val_acc={rec['val_acc']:.4f} "
                   f"images/s={ips:,.0f} ({engine.name}, world={ctx.world})", flush=True)
         metrics.write(**rec)
+        if cfg.resume:
+            params, mom = engine.get_state()  # every rank holds the same replica
+            if ctx.rank == 0:
+                save_resume(cfg.resume, params, mom, i, cfg.model, cfg.dtype)
     engine.finish()
     sd = engine.state_dict()
     if ctx.rank == 0 and cfg.save_path:

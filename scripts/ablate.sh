@@ -4,7 +4,7 @@ OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out
 TAG=${1:-abl}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-for m in 0 1 2 4 8 16 32 64 128 256 512 1016; do
+for m in ${ABL_SET:-0 1 2 4 8 16 32 64 128 256 512 1016}; do
   MNIST_AMD_ABLATE=$m timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_$m" -o run --output-format csv -- python3 "$OUT/../bench.py" --steps 20 --warmup 3 --no-eval > "$OUT/${TAG}_$m.log" 2>&1 || { echo "fail $m"; exit 1; }
 done
 echo done
