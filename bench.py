@@ -8,8 +8,8 @@ top-1 acc", config "LeNet-5 MNIST DDP 8xMI355X large-batch 8192/GPU bf16".  Weak
 Each timed step is a COMPLETE data-parallel training step through the native path: gather +
 normalise of the step's samples from the HBM-resident uint8 dataset, LeNet-5 forward and
 backward (hand-written CDNA4 MFMA kernels, bf16 inputs / fp32 accumulate / fp32 master
-weights), the gradient all-reduce (native RCCL communicator, two buckets overlapped with the
-convolution backward) and the SGD-momentum update, replayed as one hipGraph per step.
+weights), the gradient all-reduce (native RCCL communicator, two buckets, the conv one overlapped
+with the FC weight gradient) and the SGD-momentum update, replayed as one hipGraph per step.
 Epoch boundaries inside the timed region (new DistributedSampler permutation upload) are
 included.  Data: synthetic 28x28 uint8 images of the MNIST shape (no network), random init.
 
@@ -155,7 +155,7 @@ def main() -> int:
             "image_shape": [1, 28, 28],
             "parallelism": f"dp{W}",
             "optimizer": f"SGD(lr={a.lr}, momentum={a.momentum})",
-            "comm": "native RCCL, 2 buckets overlapped with conv backward" if a.comm == "rccl" else "c10d nccl",
+            "comm": "native RCCL, 2 buckets (conv bucket overlapped with FC wgrad)" if a.comm == "rccl" else "c10d nccl",
             "hipgraph": use_graph,
         },
         "top1": None if top1 is None else round(top1, 4),

@@ -1,11 +1,14 @@
 // Static-schedule step orchestration (see trainer.h).
 //
 // Kernel sequence of one data-parallel step (reference CS5, survey §3; kernel IDs of §2.6):
-//   LeNet : conv_fwd -> head(fwd+loss+dgrad) -> wgrad(FC) -> reduce(FC) -> [RCCL FC bucket on
-//           the comm stream] || conv_bwd -> reduce(conv) -> [RCCL conv bucket] -> join -> sgd_pack
-//   MLP   : head -> wgrad -> reduce -> [RCCL bucket] -> join -> sgd_pack
-// The large FC bucket's all-reduce overlaps the convolution backward (the FLOP-heaviest
-// phase); the last bucket is small, so the exposed tail is one small-message RCCL latency.
+//   LeNet, 1 GPU : conv_fwd -> head(fwd+loss+dgrad) -> wgrad(FC) -> conv_bwd -> reduce+sgd+pack (fused)
+//   LeNet, W > 1 : conv_fwd -> head -> conv_bwd -> reduce(conv) -> [RCCL conv bucket on the comm
+//                  stream] || wgrad(FC) -> reduce(FC) -> [RCCL FC bucket] -> join -> sgd_pack
+//   MLP          : head -> wgrad -> reduce -> [RCCL bucket] -> join -> sgd_pack
+// Why conv_bwd goes first with W > 1: its one-round grid (2 blocks/CU) fills every CU's register
+// file for the kernel's whole life, so no collective can be co-resident with it; the conv bucket's
+// all-reduce instead overlaps the FC wgrad/reduce (320 small blocks leave CUs free), and only the FC
+// bucket (236.5 KB) remains exposed before the update.
 // All launches are allocation- and sync-free; capture() records the sequence (both streams,
 // RCCL included) into one hipGraph, so a training step costs one hipGraphLaunch on the host.
 #include "trainer.h"
@@ -197,6 +200,17 @@ void Trainer::launch_step(int B, hipStream_t s) {
   }
   launch_head(model_, dtype_, true, br, hb, head_rows_per_block(model_, dtype_, batch_), s);
   post_launch(s);
+  if (comm_ && model_ == ModelKind::LENET) {
+    // Multi-GPU order: conv backward FIRST, its (small) bucket all-reduce on the side stream then
+    // overlaps the FC wgrad + reduce below.  conv_bwd's 2 blocks/CU fill every CU's register file
+    // for the kernel's whole life, so a collective queued "behind" it could not start until it ended.
+    int nslab = 0;
+    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s);
+    post_launch(s);
+    launch_reduce(ptr<const float>(p_.slab_conv), cp, nslab, 0, cp, scale, ptr<float>(p_.grad), s);
+    post_launch(s);
+    comm_phase(1, s);
+  }
   const int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s);
   post_launch(s);
   if (!comm_) {
@@ -215,14 +229,6 @@ void Trainer::launch_step(int B, hipStream_t s) {
   launch_reduce(ptr<const float>(p_.slab_fc), nparam_, splits, cp, nparam_, scale, ptr<float>(p_.grad), s);
   post_launch(s);
   comm_phase(0, s);
-  if (model_ == ModelKind::LENET) {
-    int nslab = 0;
-    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s);
-    post_launch(s);
-    launch_reduce(ptr<const float>(p_.slab_conv), cp, nslab, 0, cp, scale, ptr<float>(p_.grad), s);
-    post_launch(s);
-    comm_phase(1, s);
-  }
   if (comm_ && overlap_) {
     HIP_CHECK(hipEventRecord(events_[2], comm_stream_));
     HIP_CHECK(hipStreamWaitEvent(s, events_[2], 0));

@@ -13,8 +13,9 @@ the backward phase that produces it has been reduced.  :func:`plan_buckets` deci
 for the small messages of these models the all-reduce is latency-bound on xGMI (7 point-to-point
 links, ~153 GB/s each — a 473 KB ring step is a few microseconds), so the plan is "as few buckets
 as possible, split only at phase boundaries where the remaining backward work can hide one":
-LeNet-5 gets two buckets (FC head 236.5 KB, overlapped with the convolution backward; conv 10 KB,
-exposed), the MLP one.  ``bucket_cap_kb`` forces further splits (A/B experiments).
+LeNet-5 gets two buckets (conv 10 KB, all-reduced while the FC weight gradient runs; FC head
+236.5 KB, exposed: see csrc/runtime/trainer.cpp for why the convolution backward goes first),
+the MLP one.  ``bucket_cap_kb`` forces further splits (A/B experiments).
 
 :class:`GlooReducer` is the same contract for the CPU path (plumbing / oracle): it broadcasts
 parameters at construction and all-reduces the flattened gradients in the same bucket plan.
