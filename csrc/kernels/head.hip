@@ -576,14 +576,25 @@ int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab
   return splits;
 }
 
-template <typename T, class H, int MT>
-void head_launch_mt(bool train, const BatchRef& br, const HeadBuffers& hb, hipStream_t s) {
+template <typename T, class H, int MT, int NWV>
+void head_launch_mtw(bool train, const BatchRef& br, const HeadBuffers& hb, hipStream_t s) {
   const int rows = rup(br.B, 32);
   const int grid = (rows + MT * 16 - 1) / (MT * 16);
   if (train)
-    hipLaunchKernelGGL((head_kernel<T, H, MT, true, false>), dim3(grid), dim3(256), 0, s, br, hb);
+    hipLaunchKernelGGL((head_kernel<T, H, MT, true, false, NWV>), dim3(grid), dim3(NWV * 64), 0, s, br, hb);
   else
-    hipLaunchKernelGGL((head_kernel<T, H, MT, false, false>), dim3(grid), dim3(256), 0, s, br, hb);
+    hipLaunchKernelGGL((head_kernel<T, H, MT, false, false, NWV>), dim3(grid), dim3(NWV * 64), 0, s, br, hb);
+}
+
+template <typename T, class H, int MT>
+void head_launch_mt(bool train, const BatchRef& br, const HeadBuffers& hb, hipStream_t s) {
+  static const int nwv = [] {
+    const char* e = std::getenv("MNIST_AMD_HEAD_NWV");  // tuning knob: waves per head workgroup
+    return e ? std::atoi(e) : 16;  // swept 4 / 8 / 16 at B=8192: 16 waves (4 per SIMD) best, -3% step time
+  }();
+  if (nwv == 8) head_launch_mtw<T, H, MT, 8>(train, br, hb, s);
+  else if (nwv == 16) head_launch_mtw<T, H, MT, 16>(train, br, hb, s);
+  else head_launch_mtw<T, H, MT, 4>(train, br, hb, s);
 }
 
 // small-batch path: layer-1 split GEMM, then the head with 16-row tiles consuming the partials;
@@ -631,10 +642,17 @@ void head_launch_t(bool train, const BatchRef& br, const HeadBuffers& hb, int ro
 }  // namespace
 
 int head_rows_per_block(ModelKind m, DType t, int B) {
+  static const int forced = [] {
+    const char* e = std::getenv("MNIST_AMD_HEAD_ROWS");  // tuning knob
+    return e ? std::atoi(e) : 0;
+  }();
+  if (forced) return forced;
   if (B <= 256) return 16;
   if (t == DType::F32) return 32;
   if (m == ModelKind::MLP) return B >= 4096 ? 64 : 32;
-  return 32;  // 256+ workgroups at B=8192: one wave per SIMD chip-wide (16-row tiles measured slower: 41 vs 32 us)
+  // LeNet bf16, 16-wave workgroups: 64-row tiles (128 workgroups at B=8192) measured best
+  // (step 0.2004 ms vs 0.2023 at 32 rows, 0.215 at 16 rows)
+  return B >= 4096 ? 64 : 32;
 }
 
 void launch_head(ModelKind m, DType t, bool train, const BatchRef& br, const HeadBuffers& hb, int rows,

@@ -14,6 +14,7 @@ allocator, never re-allocated per step) and exposes epoch-level operations:
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import Dict, Optional, Tuple
 
@@ -69,7 +70,7 @@ class NativeTrainer:
         self.ld_b = _rup(self.batch, 64)
         KC = 16 if dtype == "fp32" else 32
         if fc_splits is None:
-            fc_splits = max(1, min(16, _rup(self.batch, KC) // 512))
+            fc_splits = int(os.environ.get("MNIST_AMD_FC_SPLITS", "0")) or max(1, min(16, _rup(self.batch, KC) // 512))
         K0P, N1P, N2P = HEAD_DIMS[model]
         z = lambda *s, dt=tdt: torch.zeros(*s, dtype=dt, device=dev)  # noqa: E731
         self.params = z(self.nparam, dt=torch.float32)
