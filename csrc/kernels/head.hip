@@ -470,12 +470,15 @@ struct WgArgs {
   float* slab;
 };
 
-template <typename T>
-__global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
+template <typename T, int KS = 1>
+__global__ __launch_bounds__(256 * KS) void wgrad_kernel(WgArgs<T> a) {
   using M = Mma<T>;
   using Frag = typename M::Frag;
   constexpr int KV = M::KV, KC = M::KC;
-  const int lane = threadIdx.x & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
+  // KS wave groups per workgroup split the block's batch range; partial tiles meet in LDS
+  __shared__ f32x4 part[KS > 1 ? (KS - 1) * 4 * 4 * 64 : 1];
+  const int lane = threadIdx.x & 63, wall = wave_id(), w = wall & 3, ks = wall >> 2;
+  const int row = lane & 15, grp = lane >> 4;
   int j = 0;
   while (j + 1 < a.njobs && (int)blockIdx.x >= a.job[j + 1].blk_begin) ++j;
   const WgJob<T>& J = a.job[j];
@@ -483,10 +486,12 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
   const int bn = lb / J.nblk_k, bk = lb % J.nblk_k;
   const int n0 = bn * 64 + (w >> 1) * 32, k0 = bk * 64 + (w & 1) * 32;
   const int Kb = J.K + (J.bias ? 1 : 0);
-  if (n0 >= J.N || k0 >= Kb) return;
+  const bool active = n0 < J.N && k0 < Kb;  // no early return: KS > 1 meets at a barrier
   const bool nv1 = n0 + 16 < J.NP;
-  const int rs = blockIdx.y * a.rlen;
-  const int re = min(rs + a.rlen, a.Bp);
+  const int sub = rup((a.rlen + KS - 1) / KS, KC);
+  const int rb = blockIdx.y * a.rlen, rend = min(rb + a.rlen, a.Bp);
+  const int rs = min(rb + ks * sub, rend);
+  const int re = active ? min(rs + sub, rend) : rs;
 
   f32x4 acc[2][2];
 #pragma unroll
@@ -531,6 +536,23 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
     M::mma(acc[1][1], a1, b1);
   }
 
+  if constexpr (KS > 1) {
+    if (ks > 0) {
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) part[(((ks - 1) * 4 + w) * 4 + mi * 2 + ni) * 64 + lane] = acc[mi][ni];
+    }
+    __syncthreads();
+    if (ks > 0) return;
+#pragma unroll
+    for (int q = 1; q < KS; ++q)  // fixed order: bitwise reproducible
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) acc[mi][ni] += part[(((q - 1) * 4 + w) * 4 + mi * 2 + ni) * 64 + lane];
+  }
+  if (!active) return;
   float* out = a.slab + (size_t)blockIdx.y * a.slab_ld + J.out_off;
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
@@ -572,7 +594,13 @@ int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab
   splits = (a.Bp + a.rlen - 1) / a.rlen;
   a.slab = slab;
   a.slab_ld = slab_ld;
-  hipLaunchKernelGGL(wgrad_kernel<T>, dim3(blk, splits), dim3(256), 0, s, a);
+  static const int ksplit = [] {
+    const char* e = std::getenv("MNIST_AMD_WGRAD_KS");  // tuning knob: wave groups per workgroup
+    return e ? std::atoi(e) : 1;
+  }();
+  if (ksplit == 4) hipLaunchKernelGGL((wgrad_kernel<T, 4>), dim3(blk, splits), dim3(1024), 0, s, a);
+  else if (ksplit == 2) hipLaunchKernelGGL((wgrad_kernel<T, 2>), dim3(blk, splits), dim3(512), 0, s, a);
+  else hipLaunchKernelGGL((wgrad_kernel<T, 1>), dim3(blk, splits), dim3(256), 0, s, a);
   return splits;
 }
 

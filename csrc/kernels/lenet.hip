@@ -327,7 +327,8 @@ template <typename T>
 struct BwdSmem {
   // pitches padded so the fragment reads and the un-pooling scatters are <= 2-way bank
   // conflicted (measured 60% conflict cycles with the unpadded 1024/224/160/896 pitches)
-  static constexpr int W2P = 424, XP = 1048, P1P = 240, D2P = 176, D1P = 912;
+  // W2R: conv2 dgrad B operand for TWO output rows per tile, [16 = (r, c)][30 taps x 16 ch + pad]
+  static constexpr int W2P = 488, XP = 1048, P1P = 240, D2P = 176, D1P = 912;
   // XS has 7 planes (5 shifted copies + an all-zero + an all-ones plane) and P1T 32 (30 + zero +
   // ones): padding / bias-gradient columns read a constant plane instead of branching per lane
   static constexpr int XPL = 7, PPL = 32;
@@ -365,10 +366,10 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   const T* p1g = reinterpret_cast<const T*>(cb.p1);
 
   constexpr int W2CH = 160 / KC;              // conv2 wgrad: 10 rows x 16 positions
-  constexpr int D2CH = (400 + KC - 1) / KC;   // conv2 dgrad K = 25 taps x 16 ch (13 bf16 / 25 f32)
+  constexpr int D2CH = 480 / KC;              // conv2 dgrad K = 30 taps (kh' = -1..4) x 16 ch (15 bf16 / 30 f32)
   constexpr int W1CH = 896 / KC;              // conv1 wgrad: 28 rows x 32 positions (28 bf16 / 56 f32)
-  constexpr bool WREG = false;  // register-resident dgrad B (52 VGPRs) pushed the kernel to 245 VGPRs and
-                                // made hipcc shuttle accumulators VGPR<->AGPR around every MFMA
+  // (measured: a register-resident dgrad B operand pushed the kernel to 245 VGPRs and made hipcc
+  //  shuttle accumulators VGPR<->AGPR around every MFMA -- the B operand is read from LDS)
 
   // ---- once per workgroup: zero every padded image, stage C2d
   zero_lds<T>(xs, 6 * S::XP);
@@ -378,22 +379,24 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   zero_lds<T>(dy2t, 16 * S::D2P);
   zero_lds<T>(dy1t, 8 * S::D1P);
   zero_lds<T>(dys, 18 * 18 * 16);
-  if constexpr (!WREG) {
-    constexpr int VE = 16 / (int)sizeof(T);
-    for (int e = tid; e < 16 * 416 / VE; e += 256) {
-      const int r = e / (416 / VE), c = (e % (416 / VE)) * VE;
-      *reinterpret_cast<uint4*>(w2 + r * S::W2P + c) = *reinterpret_cast<const uint4*>(pack + L::C2D + r * 416 + c);
-    }
+  // conv2 dgrad, two output rows per tile: out (Y = y + r, x, c) = sum over kh' in [-1, 4], kw, n of
+  // dY2[y - kh'][x - kw][n] * W2[n][c][kh' + r][kw]  ->  B[(kh'+1)*5 + kw, n][(r, c)], zero where
+  // kh' + r is outside 0..4.  N = (r, c) holds 12 live columns of 16 (was 6 with one row per tile).
+  for (int e = tid; e < 16 * 480; e += 256) {
+    const int nr = e / 480, k = e % 480, r = nr >> 3, c = nr & 7;
+    const int tp = k >> 4, n = k & 15, kh = tp / 5 - 1 + r, kw = tp % 5;
+    w2[nr * S::W2P + k] = (c < 6 && kh >= 0 && kh <= 4) ? pack[L::C2D + c * 416 + (kh * 5 + kw) * 16 + n] : to_t<T>(0.f);
   }
-  // ---- static cost-balanced work split of phase B (dgrad tile = 13 K-chunks, wgrad tile = 5):
-  //      dgrad image rows {4,4,3,3}, wgrad tiles {2,2,4,5}  ->  62/62/59/64 chunks per wave
-  const int nd = w < 2 ? 4 : 3, d0 = w < 2 ? 4 * w : 8 + 3 * (w - 2);   // dgrad rows [d0, d0 + nd)
-  const int nw = w < 2 ? 2 : (w == 2 ? 4 : 5), n0w = w < 2 ? 2 * w : (w == 2 ? 4 : 8);
+  // ---- static work split of phase B (dgrad row-pair tile = 15 K-chunks, wgrad tile = 5):
+  //      dgrad pairs {2,2,2,1}, wgrad tiles {3,3,3,4}  ->  45/45/45/35 chunks per wave
+  const int np = w < 3 ? 2 : 1, q0 = 2 * w;              // dgrad row pairs [q0, q0 + np)
+  const int nw = w < 3 ? 3 : 4, n0w = 3 * w;
+  constexpr int NWT = 4;  // wgrad accumulators per wave
   // ---- per-lane operand offsets (loop invariant)
-  int w2off[5];   // conv2 wgrad B: this wave's output tiles (kcol = tap*8 + c; 200 = bias)
-  int w2sel[5];   // 0 data, 1 ones (bias), 2 zero
+  int w2off[NWT];   // conv2 wgrad B: this wave's output tiles (kcol = tap*8 + c; 200 = bias)
+  int w2sel[NWT];   // 0 data, 1 ones (bias), 2 zero
 #pragma unroll
-  for (int i = 0; i < 5; ++i) {
+  for (int i = 0; i < NWT; ++i) {
     const int kcol = (n0w + i) * 16 + row, tap = kcol >> 3, c = kcol & 7;
     w2sel[i] = (kcol < 200 && c < 6) ? 0 : (kcol == 200 ? 1 : 2);
     w2off[i] = w2sel[i] == 0 ? ((tap % 5) * 6 + c) * S::P1P + (tap / 5) * 16 : (w2sel[i] == 1 ? 31 : 30) * S::P1P;
@@ -413,20 +416,13 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     int tap, n0;
     if constexpr (KV == 8) { tap = kc * 2 + (grp >> 1); n0 = (grp & 1) * 8; }
     else { tap = kc; n0 = grp * 4; }
-    const int tp = min(tap, 24);  // tap 25 (bf16 K padding) has zero weights: any finite A will do
-    doff[kc] = (-(tp / 5) * 18 - (tp % 5)) * 16 + n0;
+    const int khp = tap / 5 - 1, kw = tap % 5;  // A row y - kh' (pair base y <= 12: DYS rows <= 17)
+    doff[kc] = (-khp * 18 - kw) * 16 + n0;
   }
 
-  // conv2 dgrad B operand: in registers for bf16 (13 fragments), from LDS (W2) for fp32
-  Frag wreg[WREG ? D2CH : 1];
-  if constexpr (WREG) {
+  f32x4 accW2[NWT], accW1[2];
 #pragma unroll
-    for (int kc = 0; kc < D2CH; ++kc) wreg[kc] = M::load(pack + L::C2D + row * 416 + kc * KC + grp * KV);
-  }
-
-  f32x4 accW2[5], accW1[2];
-#pragma unroll
-  for (int i = 0; i < 5; ++i) accW2[i] = zero4();
+  for (int i = 0; i < NWT; ++i) accW2[i] = zero4();
   accW1[0] = zero4();
   accW1[1] = zero4();
   __syncthreads();
@@ -529,19 +525,19 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
       // unconditional loads + MFMAs (unused tiles read the zero plane): a lane-divergent branch
       // around an MFMA on a loop-carried accumulator makes hipcc shuttle it VGPR<->AGPR every chunk
 #pragma unroll
-      for (int i = 0; i < 5; ++i) M::mma(accW2[i], a, M::load(p1t + w2off[i] + oh * 16 + ow0));
+      for (int i = 0; i < NWT; ++i) M::mma(accW2[i], a, M::load(p1t + w2off[i] + oh * 16 + ow0));
     }
 
-    // ---- phase B2: conv2 dgrad  dP1[q][c] = sum_{tap,n} dY2[q - tap][n] * W2[n][c][tap]
-    //      M = pool1 positions laid out [y][16] (one image row per tile, x >= 14 dropped), so lane
-    //      group g owns x = 4g..4g+3 of row y, and the pool1 un-pooling epilogue (argmax + ReLU)
-    //      writes the conv1 pre-activation grad rows 2y and 2y+1 as ONE 16-byte store each.
-    //      Tiles are processed in pairs for ILP.
+    // ---- phase B2: conv2 dgrad, one tile = image rows (y, y+1) x 16 columns x (r, c):
+    //      dP1[y+r][x][c] = sum_{kh',kw,n} dY2[y-kh'][x-kw][n] * W2R[kh',kw,n][(r,c)]
+    //      Lane group g owns x = 4g..4g+3; the pool1 un-pooling epilogue (argmax + ReLU) writes the
+    //      conv1 pre-activation grad rows 2Y and 2Y+1 (Y = y + r) as ONE 16-byte store each.
+    //      A wave's (up to 2) tiles share every B fragment.
     {
       auto dgrad_tile_epi = [&](int y, const f32x4& acc) {
-        const int c = row;
+        const int c = row & 7, Y = y + (row >> 3);
         if (c < 6) {
-          const uint32_t codes = *reinterpret_cast<const uint32_t*>(m1s + (c * 14 + y) * 16 + grp * 4);
+          const uint32_t codes = *reinterpret_cast<const uint32_t*>(m1s + (c * 14 + Y) * 16 + grp * 4);
           T r0[8], r1[8];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -554,7 +550,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
             r1[2 * i] = to_t<T>(am == 2 ? v : 0.f);
             r1[2 * i + 1] = to_t<T>(am == 3 ? v : 0.f);
           }
-          T* d = dy1t + c * S::D1P + (2 * y) * 32 + grp * 8;
+          T* d = dy1t + c * S::D1P + (2 * Y) * 32 + grp * 8;
           if constexpr (sizeof(T) == 2) {
             *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(r0);
             *reinterpret_cast<uint4*>(d + 32) = *reinterpret_cast<const uint4*>(r1);
@@ -567,39 +563,29 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
         }
       };
       const int x = min(row, 13);
-      int m = 0;
-      const int nmt = (cb.ablate & 128) ? 0 : nd;
-      for (; m + 2 <= nmt; m += 2) {
-        const int y0 = d0 + m, y1 = y0 + 1;
-        const T* a0 = dys + ((y0 + 4) * 18 + x + 4) * 16;
-        const T* a1 = dys + ((y1 + 4) * 18 + x + 4) * 16;
-        f32x4 acc0 = zero4(), acc1 = zero4();
+      const T* bq = w2 + row * S::W2P + grp * KV;
+      if (!(cb.ablate & 128)) {
+        if (np == 2) {
+          const int y0 = 2 * q0, y1 = y0 + 2;
+          const T* a0 = dys + ((y0 + 4) * 18 + x + 4) * 16;
+          const T* a1 = dys + ((y1 + 4) * 18 + x + 4) * 16;
+          f32x4 acc0 = zero4(), acc1 = zero4();
 #pragma unroll
-        for (int kc = 0; kc < D2CH; ++kc) {
-          const Frag fa0 = M::load(a0 + doff[kc]);
-          const Frag fa1 = M::load(a1 + doff[kc]);
-          Frag fb;
-          if constexpr (WREG) fb = wreg[kc];
-          else fb = M::load(w2 + row * S::W2P + kc * KC + grp * KV);
-          M::mma(acc0, fa0, fb);
-          M::mma(acc1, fa1, fb);
-        }
-        dgrad_tile_epi(y0, acc0);
-        dgrad_tile_epi(y1, acc1);
-      }
-      for (; m < nmt; ++m) {
-        const int y0 = d0 + m;
-        const T* a0 = dys + ((y0 + 4) * 18 + x + 4) * 16;
-        f32x4 acc0 = zero4();
+          for (int kc = 0; kc < D2CH; ++kc) {
+            const Frag fb = M::load(bq + kc * KC);
+            M::mma(acc0, M::load(a0 + doff[kc]), fb);
+            M::mma(acc1, M::load(a1 + doff[kc]), fb);
+          }
+          dgrad_tile_epi(y0, acc0);
+          dgrad_tile_epi(y1, acc1);
+        } else {
+          const int y0 = 2 * q0;
+          const T* a0 = dys + ((y0 + 4) * 18 + x + 4) * 16;
+          f32x4 acc0 = zero4();
 #pragma unroll
-        for (int kc = 0; kc < D2CH; ++kc) {
-          const Frag fa0 = M::load(a0 + doff[kc]);
-          Frag fb;
-          if constexpr (WREG) fb = wreg[kc];
-          else fb = M::load(w2 + row * S::W2P + kc * KC + grp * KV);
-          M::mma(acc0, fa0, fb);
+          for (int kc = 0; kc < D2CH; ++kc) M::mma(acc0, M::load(a0 + doff[kc]), M::load(bq + kc * KC));
+          dgrad_tile_epi(y0, acc0);
         }
-        dgrad_tile_epi(y0, acc0);
       }
     }
     __syncthreads();
@@ -617,7 +603,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   // ---- write this workgroup's partial gradients (slab row = blockIdx.x)
   float* out = cb.slab + (size_t)blockIdx.x * L::CONV_PARAMS;
 #pragma unroll
-  for (int i = 0; i < 5; ++i) {
+  for (int i = 0; i < NWT; ++i) {
     if (i >= nw) break;
     const int kcol = (n0w + i) * 16 + row;
 #pragma unroll
