@@ -58,7 +58,8 @@ template <typename T>
 struct FwdSmem {
   static constexpr int XP = 1048;  // plane pitch (32x32 + pad): 2-way worst-case conflicts (was 8-way at 1024)
   static constexpr int OFF_XS = 0;                                        // [8][XP] T
-  static constexpr int OFF_P1 = rup(8 * XP * (int)sizeof(T), 16);         // [196][8] T   pool1 output
+  static constexpr int XTAIL = 64;  // zeroed tail: conv1's all-zero kernel row kh' = 7 reads 1 row past plane 7
+  static constexpr int OFF_P1 = rup((8 * XP + XTAIL) * (int)sizeof(T), 16);  // [196][8] T   pool1 output
   static constexpr int OFF_M1 = rup(OFF_P1 + 196 * 8 * (int)sizeof(T), 16);  // [196][8] u8 pool1 codes
   static constexpr int OFF_P2 = rup(OFF_M1 + 196 * 8, 16);                // [400] T      pool2 output (NCHW)
   static constexpr int OFF_M2 = rup(OFF_P2 + 400 * (int)sizeof(T), 16);   // [400] u8     pool2 codes
@@ -95,9 +96,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   // conv1's B operand lives in registers; conv2's (7 chunks) is staged once per block in LDS, which
   // keeps the kernel at <= 128 registers (4 waves per SIMD: the whole 1024-block grid co-resident)
   T* w2s = reinterpret_cast<T*>(smem + S::OFF_W2);
+  // conv1 B operand for TWO pooled rows per tile: column (r, c) = (row >> 3, row & 7), k = kh'*8 + kw
+  // with kh' = kh + 2r in 0..7, so B[(kh', kw)][(r, c)] = W1[c][kh' - 2r][kw] (zero outside 0..4)
   Frag b1[C1CH];
+  {
+    const int r1 = row >> 3, c1 = row & 7;
 #pragma unroll
-  for (int kc = 0; kc < C1CH; ++kc) b1[kc] = M::load(pack + L::C1 + row * 64 + kc * KC + grp * KV);
+    for (int kc = 0; kc < C1CH; ++kc) {
+#pragma unroll
+      for (int jj = 0; jj < KV; ++jj) {
+        const int k = kc * KC + grp * KV + jj, kh = (k >> 3) - 2 * r1, kw = k & 7;
+        M::set(b1[kc], jj, (c1 < 6 && kh >= 0 && kh <= 4) ? to_f(pack[L::C1 + c1 * 64 + kh * 8 + kw]) : 0.f);
+      }
+    }
+  }
   {
     constexpr int VE = 16 / (int)sizeof(T);
     for (int e = tid; e < 16 * 224 / VE; e += 256) {
@@ -105,32 +117,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
       *reinterpret_cast<uint4*>(w2s + r * S::W2P + c) = *reinterpret_cast<const uint4*>(pack + L::C2F + r * 224 + c);
     }
   }
-  const float bias1 = row < 6 ? prm[L::CB1 + row] : 0.f;
+  const float bias1 = (row & 7) < 6 ? prm[L::CB1 + (row & 7)] : 0.f;
   const float bias2 = prm[L::CB2 + row];
 
-  // conv1 tiling: tile (j, w) = pooled row j (0..13) x pooled columns 4w..4w+3 (grid padded 14->16),
-  // M row = pooled column * 4 + window element.  Since 2*4w is a multiple of 8, the shifted-copy
-  // plane and column of every fragment are lane constants: A(j, kc) = c1base[kc] + 64*j.
+  // conv1 tiling: tile (t, w) = pooled rows 2t, 2t+1 (t = 0..6) x pooled columns 4w..4w+3 (grid padded
+  // 14->16); M row = pooled column * 4 + window element, N = (pooled-row parity r, channel c) -- 12 of
+  // 16 columns live instead of 6 -- and K = 7 kernel-row offsets x 8 taps (2 bf16 chunks, as before).
+  // Since 2*4w is a multiple of 8, the shifted-copy plane and column of every fragment are lane
+  // constants: A(t, kc) = c1base[kc] + 128*t.
   int c1base[C1CH];
   {
     const int q = row >> 2, e = row & 3, xt = 2 * q + (e & 1);
 #pragma unroll
     for (int kc = 0; kc < C1CH; ++kc) {
       const int k0 = kc * KC + grp * KV;
-      const int kh = min(k0 >> 3, 4), xx = xt + (k0 & 7);
-      c1base[kc] = (xx & 7) * S::XP + ((e >> 1) + kh) * 32 + 8 * w + (xx & ~7);
+      const int khp = k0 >> 3, xx = xt + (k0 & 7);
+      c1base[kc] = (xx & 7) * S::XP + ((e >> 1) + khp) * 32 + 8 * w + (xx & ~7);
     }
   }
   const bool c1valid = 4 * w + grp < 14;  // wave 3, lane groups 2-3: padding columns 14, 15
-  auto c1_epi = [&](int j, const f32x4& acc) {  // pool + bias + ReLU, staged in LDS
-    const int n = row, pp = j * 14 + 4 * w + grp;
+  auto c1_epi = [&](int t, const f32x4& acc) {  // pool + bias + ReLU, staged in LDS
+    const int n = row & 7, pp = (2 * t + (row >> 3)) * 14 + 4 * w + grp;
     float mx = acc[0];
     int am = 0;
 #pragma unroll
     for (int i = 1; i < 4; ++i)
       if (acc[i] > mx) { mx = acc[i]; am = i; }
     const float pre = mx + bias1;
-    if (n < 8 && c1valid) {
+    if (c1valid) {
       p1s[pp * 8 + n] = to_t<T>(n < 6 ? fmaxf(pre, 0.f) : 0.f);
       m1s[pp * 8 + n] = (n < 6) ? (uint8_t)(am | (pre > 0.f ? 4 : 0)) : 0;
     }
@@ -169,7 +183,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
     }
   };
 
-  zero_lds<T>(xs, 8 * S::XP);
+  zero_lds<T>(xs, 8 * S::XP + S::XTAIL);
   // software pipeline: image t+1's pixels are in flight (registers) while image t computes
   // Stage mapping: thread (y, g, h), y = 2..29 padded row, g = 8-column group, h = plane half.
   // It fetches the dword-aligned 20-byte window [8g-4, 8g+16) of image row y-2 (pixel at padded
@@ -248,41 +262,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
     }
     __syncthreads();
 
-    // ---- conv1 + bias + ReLU + maxpool: 14 pooled rows per wave, in pairs
+    // ---- conv1 + bias + ReLU + maxpool: 7 two-row tiles per wave
     if (!(cb.ablate & 2)) {
-      // software pipeline: pair j+2's fragments are loaded and pair j's MFMAs issued BEFORE pair
-      // j-2's epilogue (the compiler cannot hoist xs loads over the epilogue's p1s stores itself)
-      Frag fa[C1CH], fb[C1CH];
+      // software pipeline: tile t+1's fragments are loaded and tile t's MFMAs issued BEFORE tile
+      // t-1's epilogue (the compiler cannot hoist xs loads over the epilogue's p1s stores itself)
+      Frag fa[C1CH];
 #pragma unroll
-      for (int kc = 0; kc < C1CH; ++kc) {
-        fa[kc] = M::load(xs + c1base[kc]);
-        fb[kc] = M::load(xs + c1base[kc] + 64);
+      for (int kc = 0; kc < C1CH; ++kc) fa[kc] = M::load(xs + c1base[kc]);
+      f32x4 prev = zero4();
+#pragma unroll
+      for (int t = 0; t < 7; ++t) {
+        f32x4 acc = zero4();
+#pragma unroll
+        for (int kc = 0; kc < C1CH; ++kc) M::mma(acc, fa[kc], b1[kc]);
+        if (t + 1 < 7) {
+#pragma unroll
+          for (int kc = 0; kc < C1CH; ++kc) fa[kc] = M::load(xs + c1base[kc] + (t + 1) * 128);
+        }
+        if (t > 0) c1_epi(t - 1, prev);
+        prev = acc;
       }
-      f32x4 pA = zero4(), pB = zero4();
-#pragma unroll
-      for (int j = 0; j < 14; j += 2) {
-        f32x4 accA = zero4(), accB = zero4();
-#pragma unroll
-        for (int kc = 0; kc < C1CH; ++kc) {
-          M::mma(accA, fa[kc], b1[kc]);
-          M::mma(accB, fb[kc], b1[kc]);
-        }
-        if (j + 2 < 14) {
-#pragma unroll
-          for (int kc = 0; kc < C1CH; ++kc) {
-            fa[kc] = M::load(xs + c1base[kc] + (j + 2) * 64);
-            fb[kc] = M::load(xs + c1base[kc] + (j + 2) * 64 + 64);
-          }
-        }
-        if (j > 0) {
-          c1_epi(j - 2, pA);
-          c1_epi(j - 1, pB);
-        }
-        pA = accA;
-        pB = accB;
-      }
-      c1_epi(12, pA);
-      c1_epi(13, pB);
+      c1_epi(6, prev);
     }
     __syncthreads();
 
