@@ -382,10 +382,18 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   // conv2 dgrad, two output rows per tile: out (Y = y + r, x, c) = sum over kh' in [-1, 4], kw, n of
   // dY2[y - kh'][x - kw][n] * W2[n][c][kh' + r][kw]  ->  B[(kh'+1)*5 + kw, n][(r, c)], zero where
   // kh' + r is outside 0..4.  N = (r, c) holds 12 live columns of 16 (was 6 with one row per tile).
-  for (int e = tid; e < 16 * 480; e += 256) {
-    const int nr = e / 480, k = e % 480, r = nr >> 3, c = nr & 7;
-    const int tp = k >> 4, n = k & 15, kh = tp / 5 - 1 + r, kw = tp % 5;
-    w2[nr * S::W2P + k] = (c < 6 && kh >= 0 && kh <= 4) ? pack[L::C2D + c * 416 + (kh * 5 + kw) * 16 + n] : to_t<T>(0.f);
+  // Row (r, c) is C2D row c shifted by 5 taps: r = 0 -> [80 zeros | C2D[c][0..400)], r = 1 ->
+  // [C2D[c][0..400) | 80 zeros]; copied as 16-byte vectors (rows c >= 6 are all zero).
+  {
+    constexpr int VE = 16 / (int)sizeof(T), RV = 480 / VE, SH = 80 / VE;
+    for (int e = tid; e < 16 * RV; e += 256) {
+      const int nr = e / RV, v = e % RV, r = nr >> 3, c = nr & 7;
+      const int src = r == 0 ? v - SH : v;  // source vector within C2D row c
+      uint4 val = make_uint4(0, 0, 0, 0);
+      if (c < 6 && src >= 0 && src < 400 / VE)
+        val = *reinterpret_cast<const uint4*>(pack + L::C2D + c * 416 + src * VE);
+      *reinterpret_cast<uint4*>(w2 + nr * S::W2P + v * VE) = val;
+    }
   }
   // ---- static work split of phase B (dgrad row-pair tile = 15 K-chunks, wgrad tile = 5):
   //      dgrad pairs {2,2,2,1}, wgrad tiles {3,3,3,4}  ->  45/45/45/35 chunks per wave
