@@ -98,16 +98,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   T* w2s = reinterpret_cast<T*>(smem + S::OFF_W2);
   // conv1 B operand for TWO pooled rows per tile: column (r, c) = (row >> 3, row & 7), k = kh'*8 + kw
   // with kh' = kh + 2r in 0..7, so B[(kh', kw)][(r, c)] = W1[c][kh' - 2r][kw] (zero outside 0..4)
+  // (a lane's KV k-values never straddle a kernel row, so each fragment is one 16-byte load or zero)
   Frag b1[C1CH];
   {
     const int r1 = row >> 3, c1 = row & 7;
 #pragma unroll
     for (int kc = 0; kc < C1CH; ++kc) {
-#pragma unroll
-      for (int jj = 0; jj < KV; ++jj) {
-        const int k = kc * KC + grp * KV + jj, kh = (k >> 3) - 2 * r1, kw = k & 7;
-        M::set(b1[kc], jj, (c1 < 6 && kh >= 0 && kh <= 4) ? to_f(pack[L::C1 + c1 * 64 + kh * 8 + kw]) : 0.f);
-      }
+      const int k0 = kc * KC + grp * KV, kh = (k0 >> 3) - 2 * r1;
+      b1[kc] = (c1 < 6 && kh >= 0 && kh <= 4) ? M::load(pack + L::C1 + c1 * 64 + kh * 8 + (k0 & 7)) : M::zero();
     }
   }
   {
