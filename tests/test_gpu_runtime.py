@@ -29,8 +29,9 @@ def test_rccl_world1_collectives(native):
     assert (comm.rank, comm.world) == (0, 1)
 
 
+@pytest.mark.parametrize("overlap", [True, False])
 @pytest.mark.parametrize("model_name", ["mlp", "lenet5"])
-def test_rccl_inside_captured_step(native, small_mnist, model_name):
+def test_rccl_inside_captured_step(native, small_mnist, model_name, overlap):
     """The step graph with the RCCL bucket all-reduces captured on the side stream == eager without comm."""
     from pytorch_ddp_mnist_amd.engine.native import NativeTrainer
     from pytorch_ddp_mnist_amd.models import build_model
@@ -43,7 +44,7 @@ def test_rccl_inside_captured_step(native, small_mnist, model_name):
         tr = NativeTrainer(model_name, "bf16", 128, torch.from_numpy(x.reshape(-1, 784)), torch.from_numpy(y),
                            dropout=0.0, init=m)
         if with_comm:
-            tr.attach_comm(native.RcclComm(native.RcclComm.make_unique_id(), 0, 1, 0), 1, overlap=True)
+            tr.attach_comm(native.RcclComm(native.RcclComm.make_unique_id(), 0, 1, 0), 1, overlap=overlap)
             tr.broadcast_params(0)
         tr.set_epoch_indices(idx)
         for _ in range(3):
