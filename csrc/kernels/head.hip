@@ -467,31 +467,50 @@ template <typename T>
 struct WgArgs {
   WgJob<T> job[3];
   int njobs, ldB, rlen, Bp, slab_ld;
+  // XCD-aware mode (xcd_ch > 0): 1-D grid; workgroup L runs on XCD L % 8 (round-robin dispatch) and
+  // reads only the batch rows the head kernel wrote from that XCD -- row chunks c = x, x+8, ... of
+  // xcd_ch rows (= head rows per workgroup) -- so its operands hit the XCD's own L2.
+  int xcd_ch, nch, sx;  // chunk rows, chunk count, splits per XCD
   float* slab;
 };
 
-template <typename T, int KS = 1>
-__global__ __launch_bounds__(256 * KS) void wgrad_kernel(WgArgs<T> a) {
+template <typename T>
+__global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
   using M = Mma<T>;
   using Frag = typename M::Frag;
   constexpr int KV = M::KV, KC = M::KC;
-  // KS wave groups per workgroup split the block's batch range; partial tiles meet in LDS
-  __shared__ f32x4 part[KS > 1 ? (KS - 1) * 4 * 4 * 64 : 1];
-  const int lane = threadIdx.x & 63, wall = wave_id(), w = wall & 3, ks = wall >> 2;
-  const int row = lane & 15, grp = lane >> 4;
+  const int lane = threadIdx.x & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
+  int tile, split, nsteps, x = 0, m0 = 0, spc = 1, rs = 0;
+  if (a.xcd_ch == 0) {
+    tile = blockIdx.x;
+    split = blockIdx.y;
+    rs = split * a.rlen;
+    nsteps = (min(rs + a.rlen, a.Bp) - rs + KC - 1) / KC;
+  } else {
+    const int L = blockIdx.x, q = L >> 3;
+    x = L & 7;
+    tile = q / a.sx;
+    const int sub = q % a.sx;
+    split = x * a.sx + sub;
+    const int mx = x < a.nch ? (a.nch - x + 7) / 8 : 0;  // chunks owned by XCD x
+    m0 = sub * mx / a.sx;
+    const int m1 = (sub + 1) * mx / a.sx;
+    spc = a.xcd_ch / KC;
+    nsteps = (m1 - m0) * spc;
+  }
+  auto step_row = [&](int st) -> int {  // first batch row of step st (may be >= Bp: skipped)
+    if (a.xcd_ch == 0) return rs + st * KC;
+    return (x + 8 * (m0 + st / spc)) * a.xcd_ch + (st % spc) * KC;
+  };
   int j = 0;
-  while (j + 1 < a.njobs && (int)blockIdx.x >= a.job[j + 1].blk_begin) ++j;
+  while (j + 1 < a.njobs && tile >= a.job[j + 1].blk_begin) ++j;
   const WgJob<T>& J = a.job[j];
-  const int lb = blockIdx.x - J.blk_begin;
+  const int lb = tile - J.blk_begin;
   const int bn = lb / J.nblk_k, bk = lb % J.nblk_k;
   const int n0 = bn * 64 + (w >> 1) * 32, k0 = bk * 64 + (w & 1) * 32;
   const int Kb = J.K + (J.bias ? 1 : 0);
-  const bool active = n0 < J.N && k0 < Kb;  // no early return: KS > 1 meets at a barrier
+  if (n0 >= J.N || k0 >= Kb) return;
   const bool nv1 = n0 + 16 < J.NP;
-  const int sub = rup((a.rlen + KS - 1) / KS, KC);
-  const int rb = blockIdx.y * a.rlen, rend = min(rb + a.rlen, a.Bp);
-  const int rs = min(rb + ks * sub, rend);
-  const int re = active ? min(rs + sub, rend) : rs;
 
   f32x4 acc[2][2];
 #pragma unroll
@@ -514,46 +533,29 @@ __global__ __launch_bounds__(256 * KS) void wgrad_kernel(WgArgs<T> a) {
 
   // software pipeline: the next K-chunk's four fragments are in flight while this one computes
   Frag na0, na1, nb0, nb1;
-  if (rs < re) {
-    na0 = M::load(ap0 + rs);
-    na1 = nv1 ? M::load(ap1 + rs) : zf;
-    nb0 = M::load(bp0 + rs);
-    nb1 = M::load(bp1 + rs);
-  }
-  for (int rc = rs; rc < re; rc += KC) {
+  auto fetch = [&](int rc) {
+    na0 = M::load(ap0 + rc);
+    na1 = nv1 ? M::load(ap1 + rc) : zf;
+    nb0 = M::load(bp0 + rc);
+    nb1 = M::load(bp1 + rc);
+  };
+  int rc = nsteps > 0 ? step_row(0) : a.Bp;
+  if (rc < a.Bp) fetch(rc);
+  for (int st = 0; st < nsteps; ++st) {
+    if (rc >= a.Bp) break;  // rows past the (padded) batch: nothing left in this sequence
     const Frag a0 = na0, a1 = na1;
     const Frag b0 = sel0 == 0 ? nb0 : (sel0 == 1 ? ones : zf);
     const Frag b1 = sel1 == 0 ? nb1 : (sel1 == 1 ? ones : zf);
-    if (rc + KC < re) {
-      na0 = M::load(ap0 + rc + KC);
-      na1 = nv1 ? M::load(ap1 + rc + KC) : zf;
-      nb0 = M::load(bp0 + rc + KC);
-      nb1 = M::load(bp1 + rc + KC);
-    }
+    const int rn = st + 1 < nsteps ? step_row(st + 1) : a.Bp;
+    if (rn < a.Bp) fetch(rn);
     M::mma(acc[0][0], a0, b0);
     M::mma(acc[0][1], a0, b1);
     M::mma(acc[1][0], a1, b0);
     M::mma(acc[1][1], a1, b1);
+    rc = rn;
   }
 
-  if constexpr (KS > 1) {
-    if (ks > 0) {
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) part[(((ks - 1) * 4 + w) * 4 + mi * 2 + ni) * 64 + lane] = acc[mi][ni];
-    }
-    __syncthreads();
-    if (ks > 0) return;
-#pragma unroll
-    for (int q = 1; q < KS; ++q)  // fixed order: bitwise reproducible
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) acc[mi][ni] += part[(((q - 1) * 4 + w) * 4 + mi * 2 + ni) * 64 + lane];
-  }
-  if (!active) return;
-  float* out = a.slab + (size_t)blockIdx.y * a.slab_ld + J.out_off;
+  float* out = a.slab + (size_t)split * a.slab_ld + J.out_off;
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -570,7 +572,7 @@ __global__ __launch_bounds__(256 * KS) void wgrad_kernel(WgArgs<T> a) {
 }
 
 template <typename T, class H>
-int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab_ld, hipStream_t s) {
+int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab_ld, int xcd_ch, hipStream_t s) {
   WgArgs<T> a{};
   auto mk = [&](int i, const void* dy, const void* x, int N, int K, int NP, bool bias, int off, int& blk) {
     WgJob<T>& J = a.job[i];
@@ -594,13 +596,17 @@ int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab
   splits = (a.Bp + a.rlen - 1) / a.rlen;
   a.slab = slab;
   a.slab_ld = slab_ld;
-  static const int ksplit = [] {
-    const char* e = std::getenv("MNIST_AMD_WGRAD_KS");  // tuning knob: wave groups per workgroup
-    return e ? std::atoi(e) : 1;
-  }();
-  if (ksplit == 4) hipLaunchKernelGGL((wgrad_kernel<T, 4>), dim3(blk, splits), dim3(1024), 0, s, a);
-  else if (ksplit == 2) hipLaunchKernelGGL((wgrad_kernel<T, 2>), dim3(blk, splits), dim3(512), 0, s, a);
-  else hipLaunchKernelGGL((wgrad_kernel<T, 1>), dim3(blk, splits), dim3(256), 0, s, a);
+  a.xcd_ch = 0;
+  static const bool xcd_off = std::getenv("MNIST_AMD_NO_XCD") != nullptr;  // A/B knob
+  // XCD-aware mapping when the head's row tiling is known and the split count divides over 8 XCDs
+  if (!xcd_off && xcd_ch > 0 && xcd_ch % KC == 0 && splits % 8 == 0) {
+    a.xcd_ch = xcd_ch;
+    a.nch = (a.Bp + xcd_ch - 1) / xcd_ch;
+    a.sx = splits / 8;
+    hipLaunchKernelGGL(wgrad_kernel<T>, dim3(blk * splits), dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL(wgrad_kernel<T>, dim3(blk, splits), dim3(256), 0, s, a);
+  }
   return splits;
 }
 
@@ -655,16 +661,28 @@ void head_launch_split(bool train, const BatchRef& br, const HeadBuffers& hb, hi
   else head_launch_split_w<T, H, 8>(train, br, hb, s);
 }
 
+// returns the batch rows per workgroup actually used (the wgrad kernel's XCD-aware mapping needs it)
 template <typename T, class H>
-void head_launch_t(bool train, const BatchRef& br, const HeadBuffers& hb, int rows, hipStream_t s) {
-  if (hb.z1p && br.B <= L1_SPLIT_MAX_B && !std::getenv("MNIST_AMD_NO_L1_SPLIT")) head_launch_split<T, H>(train, br, hb, s);
-  else if (rows <= 16) head_launch_mt<T, H, 1>(train, br, hb, s);
-  else if (rows <= 32 || !HeadSmem<T, H, 4>::FITS) {
-    if constexpr (HeadSmem<T, H, 2>::FITS) head_launch_mt<T, H, 2>(train, br, hb, s);
-    else head_launch_mt<T, H, 1>(train, br, hb, s);
-  } else {
-    if constexpr (HeadSmem<T, H, 4>::FITS) head_launch_mt<T, H, 4>(train, br, hb, s);
+int head_launch_t(bool train, const BatchRef& br, const HeadBuffers& hb, int rows, hipStream_t s) {
+  if (hb.z1p && br.B <= L1_SPLIT_MAX_B && !std::getenv("MNIST_AMD_NO_L1_SPLIT")) {
+    head_launch_split<T, H>(train, br, hb, s);
+    return 16;
   }
+  if (rows <= 16) {
+    head_launch_mt<T, H, 1>(train, br, hb, s);
+    return 16;
+  }
+  if (rows <= 32 || !HeadSmem<T, H, 4>::FITS) {
+    if constexpr (HeadSmem<T, H, 2>::FITS) {
+      head_launch_mt<T, H, 2>(train, br, hb, s);
+      return 32;
+    } else {
+      head_launch_mt<T, H, 1>(train, br, hb, s);
+      return 16;
+    }
+  }
+  if constexpr (HeadSmem<T, H, 4>::FITS) head_launch_mt<T, H, 4>(train, br, hb, s);
+  return 64;
 }
 
 }  // namespace
@@ -683,23 +701,23 @@ int head_rows_per_block(ModelKind m, DType t, int B) {
   return B >= 4096 ? 64 : 32;
 }
 
-void launch_head(ModelKind m, DType t, bool train, const BatchRef& br, const HeadBuffers& hb, int rows,
-                 hipStream_t s) {
+int launch_head(ModelKind m, DType t, bool train, const BatchRef& br, const HeadBuffers& hb, int rows,
+                hipStream_t s) {
   if (m == ModelKind::MLP) {
-    if (t == DType::F32) head_launch_t<float, MlpModel::Head>(train, br, hb, rows, s);
-    else head_launch_t<bf16, MlpModel::Head>(train, br, hb, rows, s);
-  } else {
-    if (t == DType::F32) head_launch_t<float, LenetModel::Head>(train, br, hb, rows, s);
-    else head_launch_t<bf16, LenetModel::Head>(train, br, hb, rows, s);
+    if (t == DType::F32) return head_launch_t<float, MlpModel::Head>(train, br, hb, rows, s);
+    return head_launch_t<bf16, MlpModel::Head>(train, br, hb, rows, s);
   }
+  if (t == DType::F32) return head_launch_t<float, LenetModel::Head>(train, br, hb, rows, s);
+  return head_launch_t<bf16, LenetModel::Head>(train, br, hb, rows, s);
 }
 
 int launch_head_wgrad(ModelKind m, DType t, const HeadBuffers& hb, int B, int splits, float* slab,
-                      int slab_ld, hipStream_t s) {
+                      int slab_ld, hipStream_t s, int head_rows) {
+  // head_rows: batch rows per head workgroup for this B (0 = unknown: contiguous split mapping)
   if (m == ModelKind::MLP) {
-    if (t == DType::F32) return wgrad_launch<float, MlpModel::Head>(hb, B, splits, slab, slab_ld, s);
-    return wgrad_launch<bf16, MlpModel::Head>(hb, B, splits, slab, slab_ld, s);
+    if (t == DType::F32) return wgrad_launch<float, MlpModel::Head>(hb, B, splits, slab, slab_ld, head_rows, s);
+    return wgrad_launch<bf16, MlpModel::Head>(hb, B, splits, slab, slab_ld, head_rows, s);
   }
-  if (t == DType::F32) return wgrad_launch<float, LenetModel::Head>(hb, B, splits, slab, slab_ld, s);
-  return wgrad_launch<bf16, LenetModel::Head>(hb, B, splits, slab, slab_ld, s);
+  if (t == DType::F32) return wgrad_launch<float, LenetModel::Head>(hb, B, splits, slab, slab_ld, head_rows, s);
+  return wgrad_launch<bf16, LenetModel::Head>(hb, B, splits, slab, slab_ld, head_rows, s);
 }

@@ -55,12 +55,13 @@ int head_rows_per_block(ModelKind m, DType t, int B);
 constexpr int L1_KSPLIT = 4;
 constexpr int L1_SPLIT_MAX_B = 1024;
 
-void launch_head(ModelKind m, DType t, bool train, const BatchRef& br, const HeadBuffers& hb,
+// returns the batch rows per workgroup it used
+int launch_head(ModelKind m, DType t, bool train, const BatchRef& br, const HeadBuffers& hb,
                  int rows_per_block, hipStream_t s);
 
 // Grouped weight-gradient GEMM over the batch (split-K over rows): writes S slabs, returns S.
 int launch_head_wgrad(ModelKind m, DType t, const HeadBuffers& hb, int B, int splits, float* slab,
-                       int slab_ld, hipStream_t s);
+                       int slab_ld, hipStream_t s, int head_rows = 0);
 
 void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetConvBuffers& cb,
                            hipStream_t s);

@@ -140,9 +140,9 @@ void Trainer::forward_backward(int B, uintptr_t stream) {
     launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(), s);
     post_launch(s);
   }
-  launch_head(model_, dtype_, true, br, hb, head_rows_per_block(model_, dtype_, batch_), s);
+  const int hrows = launch_head(model_, dtype_, true, br, hb, head_rows_per_block(model_, dtype_, batch_), s);
   post_launch(s);
-  launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s);
+  launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s, hrows);
   post_launch(s);
   if (model_ == ModelKind::LENET) {
     launch_lenet_conv_bwd(dtype_, br, conv_buffers(), nullptr, s);
@@ -198,7 +198,7 @@ void Trainer::launch_step(int B, hipStream_t s) {
     launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(), s);
     post_launch(s);
   }
-  launch_head(model_, dtype_, true, br, hb, head_rows_per_block(model_, dtype_, batch_), s);
+  const int hrows = launch_head(model_, dtype_, true, br, hb, head_rows_per_block(model_, dtype_, batch_), s);
   post_launch(s);
   if (comm_ && model_ == ModelKind::LENET) {
     // Multi-GPU order: conv backward FIRST, its (small) bucket all-reduce on the side stream then
@@ -211,7 +211,7 @@ void Trainer::launch_step(int B, hipStream_t s) {
     post_launch(s);
     comm_phase(1, s);
   }
-  const int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s);
+  const int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s, hrows);
   post_launch(s);
   if (!comm_) {
     // single GPU: conv backward, then ONE fused reduce + SGD + pack kernel (2 boundaries fewer)

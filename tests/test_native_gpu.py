@@ -53,12 +53,13 @@ def rel_err(a, b):
 
 @pytest.mark.parametrize("model_name", ["mlp", "lenet5"])
 @pytest.mark.parametrize("dtype,tol", [("fp32", 2e-4), ("bf16", 5e-2)])
-@pytest.mark.parametrize("batch", [2048, 1024, 128, 96, 16])
+@pytest.mark.parametrize("batch", [4096, 2048, 1024, 128, 96, 16])
 def test_grads_match_torch(native, small_mnist, model_name, dtype, tol, batch):
     x, y, _, _ = small_mnist
     torch.manual_seed(0)
     module = build_model(model_name)
-    # trainer batch <= 1024 takes the layer-1 split path (l1_split_kernel), 2048 the fused head
+    # trainer batch <= 1024 takes the layer-1 split path (l1_split_kernel), 2048 the fused head,
+    # 4096 (8 wgrad splits) the XCD-aware wgrad mapping
     tr = make_trainer(model_name, dtype, max(128, batch), x, y, module)
     idx = torch.arange(batch, dtype=torch.int32) * 3 % len(y)
     tr.set_epoch_indices(idx)
