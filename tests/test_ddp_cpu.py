@@ -52,10 +52,11 @@ def _worker(rank, world, port, model_name, q):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("model_name", ["mlp", "lenet5"])
-def test_ddp_equivalence_w2(model_name):
+def test_ddp_equivalence(model_name, world):
     """W ranks x B samples == 1 rank x W*B samples (mean loss), starting from rank 0's weights."""
-    world, port = 2, _port()
+    port = _port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     ps = [ctx.Process(target=_worker, args=(r, world, port, model_name, q)) for r in range(world)]
@@ -66,10 +67,11 @@ def test_ddp_equivalence_w2(model_name):
         p.join(60)
         assert p.exitcode == 0
     sd0, g0 = res[0][1], res[0][2]
-    sd1, g1 = res[1][1], res[1][2]
-    for k in sd0:
-        assert torch.equal(sd0[k], sd1[k]), "parameters must be broadcast from rank 0 at construction"
-    assert torch.allclose(g0, g1)
+    for r in range(1, world):
+        sdr, gr = res[r][1], res[r][2]
+        for k in sd0:
+            assert torch.equal(sd0[k], sdr[k]), "parameters must be broadcast from rank 0 at construction"
+        assert torch.allclose(g0, gr)
     # single-process oracle on the full batch from rank 0's initial weights
     torch.manual_seed(100)
     m = build_model(model_name)
