@@ -137,7 +137,7 @@ def test_mlp_loss_trajectory_matches_torch(native, small_mnist):
             loss = F.cross_entropy(out, torch.from_numpy(y[b].astype(np.int64)))
             loss.backward()
             opt.step()
-            losses_t.append(float(loss))
+            losses_t.append(float(loss.detach()))
             if len(losses_n) == 100:
                 break
         if len(losses_n) == 100:
