@@ -47,7 +47,10 @@ def _worker(rank, world, port, model_name, q):
     loss = F.nll_loss(out, y[rank * 8:(rank + 1) * 8]) if model_name == "lenet5" else F.cross_entropy(out, y[rank * 8:(rank + 1) * 8])
     loss.backward()
     red.sync_grads()
-    q.put((rank, {k: v.clone() for k, v in m.state_dict().items()}, flatten_grads(m)))
+    # numpy, not torch tensors: torch's queue pickler shares storage through fds/shm that can
+    # vanish when this process exits before the parent has unpickled them (flaky at W=4)
+    q.put((rank, {k: v.detach().numpy().copy() for k, v in m.state_dict().items()},
+           flatten_grads(m).detach().numpy().copy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -66,6 +69,7 @@ def test_ddp_equivalence(model_name, world):
     for p in ps:
         p.join(60)
         assert p.exitcode == 0
+    res = [(r, {k: torch.from_numpy(v) for k, v in sd.items()}, torch.from_numpy(g)) for r, sd, g in res]
     sd0, g0 = res[0][1], res[0][2]
     for r in range(1, world):
         sdr, gr = res[r][1], res[r][2]
