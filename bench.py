@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--comm", default="rccl", choices=["rccl", "torch"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--comm-world1", action="store_true",
+                    help="attach the RCCL communicator at world size 1 (runs the multi-GPU step schedule on one GPU)")
     ap.add_argument("--eval", action="store_true", default=True)
     ap.add_argument("--no-eval", dest="eval", action="store_false")
     ap.add_argument("--json-out", default=None)
@@ -76,9 +78,14 @@ def main() -> int:
     torch.manual_seed(0)
     tr = NativeTrainer(a.model, a.dtype, a.batch, images, labels, device=dev, lr=a.lr, momentum=a.momentum,
                        dropout=0.0, init=build_model(a.model), max_indices=num_samples(N, W))
-    if W > 1:
+    if W > 1 or a.comm_world1:
         if a.comm == "rccl":
-            tr.attach_comm(ctx.rccl, W, overlap=not a.no_overlap)
+            comm = ctx.rccl
+            if comm is None:  # --comm-world1: a world-1 RCCL communicator, no rendezvous needed
+                from pytorch_ddp_mnist_amd.ops.native import load_c
+                C = load_c()
+                comm = C.RcclComm(bytes(C.RcclComm.make_unique_id()), 0, 1, ctx.local_rank)
+            tr.attach_comm(comm, W, overlap=not a.no_overlap)
             tr.broadcast_params(0)
         else:
             import torch.distributed as dist

@@ -1,20 +1,24 @@
 // Static-schedule step orchestration (see trainer.h).
 //
 // Kernel sequence of one data-parallel step (reference CS5, survey §3; kernel IDs of §2.6):
-//   LeNet, 1 GPU : conv_fwd -> head(fwd+loss+dgrad) -> wgrad(FC) -> conv_bwd -> reduce+sgd+pack (fused)
-//   LeNet, W > 1 : conv_fwd -> head -> conv_bwd -> reduce(conv) -> [RCCL conv bucket on the comm
-//                  stream] || wgrad(FC) -> reduce(FC) -> [RCCL FC bucket] -> join -> sgd_pack
+//   LeNet, 1 GPU : conv_fwd -> head(fwd+loss+dgrad) -> { conv_bwd  ||  wgrad(FC) on the aux stream }
+//                  -> reduce+sgd+pack (fused)
+//   LeNet, W > 1 : conv_fwd -> head -> { conv_bwd -> reduce(conv)  ||  wgrad(FC) -> reduce(FC) }
+//                  -> ONE all-reduce of the whole grad slab (RCCL) -> sgd_pack
 //   MLP          : head -> wgrad -> reduce -> [RCCL bucket] -> join -> sgd_pack
-// Why conv_bwd goes first with W > 1: its one-round grid (2 blocks/CU) fills every CU's register
-// file for the kernel's whole life, so no collective can be co-resident with it; the conv bucket's
-// all-reduce instead overlaps the FC wgrad/reduce (320 small blocks leave CUs free), and only the FC
-// bucket (236.5 KB) remains exposed before the update.
+// conv_bwd's one-round grid (2 blocks/CU) is LDS-bound and leaves VGPR room on every SIMD, which the
+// FC wgrad (no LDS) fills: running the two concurrently hides most of the wgrad (-6% step time on
+// one MI355X).  MNIST_AMD_CONCURRENT=0 restores the serial schedule (W > 1: conv bucket overlapped
+// with the FC wgrad, FC bucket exposed); MNIST_AMD_MG_SCHED=split sends the FC bucket as soon as it
+// is reduced (see launch_step_concurrent_comm).
 // All launches are allocation- and sync-free; capture() records the sequence (both streams,
 // RCCL included) into one hipGraph, so a training step costs one hipGraphLaunch on the host.
 #include "trainer.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
+#include <string>
 
 #include "hip_check.h"
 
@@ -33,6 +37,14 @@ void post_launch(hipStream_t s) {
     HIP_CHECK(hipStreamIsCapturing(s, &st));
     if (st == hipStreamCaptureStatusNone) HIP_CHECK(hipStreamSynchronize(s));
   }
+}
+// MNIST_AMD_CONCURRENT: 0 = serial step, otherwise (default) FC wgrad || conv_bwd (see launch_step)
+int concurrent_mode() {
+  static const int m = [] {
+    const char* e = std::getenv("MNIST_AMD_CONCURRENT");
+    return e ? std::atoi(e) : 1;
+  }();
+  return m;
 }
 inline hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 template <typename P> P* ptr(uintptr_t v) { return reinterpret_cast<P*>(v); }
@@ -54,7 +66,8 @@ Trainer::Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const
     buckets_.push_back({0, nparam_, 0});
   }
   HIP_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
-  events_.resize(4);
+  HIP_CHECK(hipStreamCreateWithFlags(&aux_stream_, hipStreamNonBlocking));
+  events_.resize(6);
   for (auto& e : events_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_CHECK(hipMalloc(&zero_counter_, 2 * sizeof(int32_t)));
   HIP_CHECK(hipMemset(zero_counter_, 0, 2 * sizeof(int32_t)));
@@ -65,6 +78,7 @@ Trainer::~Trainer() {
   if (graph_) hipGraphDestroy(graph_);
   for (auto& e : events_) hipEventDestroy(e);
   if (comm_stream_) hipStreamDestroy(comm_stream_);
+  if (aux_stream_) hipStreamDestroy(aux_stream_);
   if (zero_counter_) hipFree(zero_counter_);
 }
 
@@ -200,16 +214,43 @@ void Trainer::launch_step(int B, hipStream_t s) {
   }
   const int hrows = launch_head(model_, dtype_, true, br, hb, head_rows_per_block(model_, dtype_, batch_), s);
   post_launch(s);
+  if (comm_ && model_ == ModelKind::LENET && concurrent_mode() != 0) {
+    launch_step_concurrent_comm(B, hrows, s);
+    return;
+  }
   if (comm_ && model_ == ModelKind::LENET) {
-    // Multi-GPU order: conv backward FIRST, its (small) bucket all-reduce on the side stream then
-    // overlaps the FC wgrad + reduce below.  conv_bwd's 2 blocks/CU fill every CU's register file
-    // for the kernel's whole life, so a collective queued "behind" it could not start until it ended.
+    // Serial multi-GPU order (MNIST_AMD_CONCURRENT=0): conv backward FIRST, its (small) bucket
+    // all-reduce on the side stream then overlaps the FC wgrad + reduce below.  conv_bwd's 2 blocks/CU
+    // fill every CU's LDS for the kernel's whole life, so a collective queued "behind" it could not
+    // start until it ended.
     int nslab = 0;
     launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s);
     post_launch(s);
     launch_reduce(ptr<const float>(p_.slab_conv), cp, nslab, 0, cp, scale, ptr<float>(p_.grad), s);
     post_launch(s);
     comm_phase(1, s);
+  }
+  if (!comm_ && model_ == ModelKind::LENET && concurrent_mode() != 0) {
+    // single GPU, concurrent branches: the FC wgrad (no LDS, 320 small blocks) runs on the aux stream
+    // beside conv_bwd (LDS-bound, 2 blocks/CU, 2 waves/SIMD: VGPR room is left for wgrad waves), then
+    // both join before the fused reduce + SGD + pack.  conv_bwd is enqueued first so its one-round
+    // grid is dispatched whole (measured: wgrad enqueued first 0.1692 ms/step, conv_bwd first 0.1565,
+    // serial 0.1671).
+    HIP_CHECK(hipEventRecord(events_[4], s));
+    HIP_CHECK(hipStreamWaitEvent(aux_stream_, events_[4], 0));
+    int nslab = 0;
+    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s);
+    post_launch(s);
+    const int splits =
+        launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, aux_stream_, hrows);
+    post_launch(aux_stream_);
+    HIP_CHECK(hipEventRecord(events_[5], aux_stream_));
+    HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));
+    launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
+                      nparam_, splits, cp, nparam_, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
+                      ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, ptr<int32_t>(p_.step), s);
+    post_launch(s);
+    return;
   }
   const int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s, hrows);
   post_launch(s);
@@ -236,6 +277,73 @@ void Trainer::launch_step(int B, hipStream_t s) {
   launch_sgd_pack(model_, dtype_, ptr<float>(p_.params), ptr<const float>(p_.grad), ptr<float>(p_.mom),
                   ptr<void>(p_.pack), nparam_, lr_, momentum_, 1.0f / float(world_), ptr<int32_t>(p_.step), s);
   post_launch(s);
+}
+
+// LeNet with a communicator, concurrent branches:
+//   main : conv_bwd -> reduce(conv)                      \
+//   aux  : wgrad(FC) -> reduce(FC)   (beside conv_bwd)    > join -> all-reduce -> sgd_pack
+// MNIST_AMD_MG_SCHED=join (default): after the join, adjacent buckets of different backward phases are
+//   coalesced, so the default plan is ONE all-reduce of the whole 246,824-byte slab -- the exchange is
+//   latency-bound on xGMI, and one call pays the ring latency once instead of twice.
+// MNIST_AMD_MG_SCHED=split: the FC buckets go out on the comm stream as soon as reduce(FC) is done
+//   (they can only overlap conv_bwd where a CU has room beside its 2 LDS-heavy blocks), the conv
+//   buckets after reduce(conv).
+void Trainer::launch_step_concurrent_comm(int B, int hrows, hipStream_t s) {
+  static const bool split = [] {
+    const char* e = std::getenv("MNIST_AMD_MG_SCHED");
+    return e && std::string(e) == "split";
+  }();
+  const BatchRef br = batch_ref(B);
+  const HeadBuffers hb = head_buffers(ptr<float>(p_.metrics));
+  const float scale = 1.0f / float(B);
+  const int cp = model_conv_params(model_);
+  HIP_CHECK(hipEventRecord(events_[4], s));
+  HIP_CHECK(hipStreamWaitEvent(aux_stream_, events_[4], 0));
+  int nslab = 0;
+  launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s);
+  post_launch(s);
+  const int splits =
+      launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, aux_stream_, hrows);
+  post_launch(aux_stream_);
+  launch_reduce(ptr<const float>(p_.slab_fc), nparam_, splits, cp, nparam_, scale, ptr<float>(p_.grad), aux_stream_);
+  post_launch(aux_stream_);
+  HIP_CHECK(hipEventRecord(events_[5], aux_stream_));
+  launch_reduce(ptr<const float>(p_.slab_conv), cp, nslab, 0, cp, scale, ptr<float>(p_.grad), s);
+  post_launch(s);
+  float* g = ptr<float>(p_.grad);
+  if (split) {
+    HIP_CHECK(hipStreamWaitEvent(comm_stream_, events_[5], 0));
+    for (const Bucket& b : buckets_)
+      if (b.phase == 0) comm_->all_reduce_sum_f32(g + b.p0, size_t(b.p1 - b.p0), comm_stream_);
+    HIP_CHECK(hipEventRecord(events_[1], s));
+    HIP_CHECK(hipStreamWaitEvent(comm_stream_, events_[1], 0));
+    for (const Bucket& b : buckets_)
+      if (b.phase != 0) comm_->all_reduce_sum_f32(g + b.p0, size_t(b.p1 - b.p0), comm_stream_);
+    HIP_CHECK(hipEventRecord(events_[2], comm_stream_));
+    HIP_CHECK(hipStreamWaitEvent(s, events_[2], 0));
+  } else {
+    HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));
+    for (const Bucket& b : coalesced_buckets()) comm_->all_reduce_sum_f32(g + b.p0, size_t(b.p1 - b.p0), s);
+  }
+  launch_sgd_pack(model_, dtype_, ptr<float>(p_.params), ptr<const float>(p_.grad), ptr<float>(p_.mom),
+                  ptr<void>(p_.pack), nparam_, lr_, momentum_, 1.0f / float(world_), ptr<int32_t>(p_.step), s);
+  post_launch(s);
+}
+
+std::vector<Bucket> Trainer::coalesced_buckets() const {
+  // buckets sorted by offset; a bucket that starts where the previous one ends and belongs to a
+  // different backward phase is merged into it (splits within a phase came from an explicit cap)
+  std::vector<Bucket> b = buckets_, out;
+  std::sort(b.begin(), b.end(), [](const Bucket& x, const Bucket& y) { return x.p0 < y.p0; });
+  for (const Bucket& x : b) {
+    if (!out.empty() && out.back().p1 == x.p0 && out.back().phase != x.phase) {
+      out.back().p1 = x.p1;
+      out.back().phase = x.phase;
+    } else {
+      out.push_back(x);
+    }
+  }
+  return out;
 }
 
 void Trainer::train_step(int B, uintptr_t stream) { launch_step(B, S(stream)); }

@@ -69,6 +69,8 @@ class Trainer {
   HeadBuffers head_buffers(float* metrics) const;
   LenetConvBuffers conv_buffers() const;
   void launch_step(int B, hipStream_t s);
+  void launch_step_concurrent_comm(int B, int hrows, hipStream_t s);
+  std::vector<Bucket> coalesced_buckets() const;
   void comm_phase(int phase, hipStream_t s);
 
   ModelKind model_;
@@ -82,6 +84,7 @@ class Trainer {
   std::shared_ptr<RcclComm> comm_;
   std::vector<Bucket> buckets_;
   hipStream_t comm_stream_ = nullptr;
+  hipStream_t aux_stream_ = nullptr;  // concurrent FC wgrad branch (fork/join inside the step graph)
   std::vector<hipEvent_t> events_;
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t exec_ = nullptr;

@@ -97,6 +97,7 @@ def _run(args, cwd, timeout=600):
     return r.stdout
 
 
+@pytest.mark.timeout(600)  # spawns fresh interpreters (torch import + GPU init)
 def test_multi_gpu_tutorial_single_rank(tmp_path):
     out = _run(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1", "--master-addr", "127.0.0.1",
                 "--master-port", "29617", os.path.join(ROOT, "ddp_tutorial_multi_gpu.py"), "--epochs", "2",
@@ -110,6 +111,7 @@ def test_multi_gpu_tutorial_single_rank(tmp_path):
     assert acc > 0.5
 
 
+@pytest.mark.timeout(600)  # spawns fresh interpreters (torch import + GPU init)
 def test_reference_mlp_on_gpu_matches_cpu_engine(tmp_path):
     """Same script, same seed, fp32, dropout 0: native GPU and torch-CPU epochs agree closely."""
     args = [os.path.join(ROOT, "mnist_cpu_mp.py"), "--data_limit", "4096", "--synthetic", "--dropout", "0",
