@@ -49,7 +49,7 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init<>())
 #define RW(f) .def_readwrite(#f, &TrainerPtrs::f)
       RW(images) RW(labels) RW(idx) RW(step) RW(params) RW(grad) RW(mom) RW(pack) RW(slab_fc) RW(slab_conv)
-      RW(metrics) RW(xT) RW(h1T) RW(h2T) RW(dy1T) RW(dy2T) RW(dy3T) RW(p1) RW(m1) RW(p2) RW(m2) RW(dp2) RW(z1p);
+      RW(metrics) RW(xT) RW(h1T) RW(h2T) RW(dy1T) RW(dy2T) RW(dy3T) RW(p1) RW(m1) RW(p2) RW(m2) RW(dp2) RW(z1p) RW(stamps);
 #undef RW
 
   py::class_<Bucket>(m, "Bucket")

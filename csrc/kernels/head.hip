@@ -37,7 +37,21 @@ struct HeadSmem {
   static constexpr int OFF_D = rup(OFF_H2 + R * P2 * (int)sizeof(T), 16);
   static constexpr int OFF_L = rup(OFF_D + R * PD * (int)sizeof(T), 16);
   static constexpr int OFF_I = OFF_L + R * 16 * 4;
-  static constexpr int TOTAL = rup(OFF_I + R * 4, 16);
+  static constexpr int OFF_LAB = OFF_I + R * 4;                       // [R] int labels of the tile
+  static constexpr int OFF_B = OFF_LAB + R * 4;                       // fp32 biases b1 [N1P] | b2 [N2P] | b3 [16]
+  static constexpr int OFF_PART = OFF_B + (H::N1P + H::N2P + 16) * 4;  // [16 waves][4] f32 metric partials
+  static constexpr int BASE_END = rup(OFF_PART + 16 * 4 * 4, 16);
+  // Layer-2/3 weights (forward and dgrad operand images) staged once per workgroup, rows padded by 8
+  // elements (<= 2-way ds_read_b128 conflicts), when they fit beside the activations: every phase
+  // after L1 then reads its B operand from LDS instead of waiting on an L2/MALL round trip.
+  static constexpr int PW2 = H::N1P + 8, PW2T = H::N2P + 8, PW3 = H::N2P + 8, PW3T = H::NCK + 8;
+  static constexpr int OFF_W2 = BASE_END;                                          // [N2P][PW2]
+  static constexpr int OFF_W2T = rup(OFF_W2 + H::N2P * PW2 * (int)sizeof(T), 16);  // [N1P][PW2T]
+  static constexpr int OFF_W3 = rup(OFF_W2T + H::N1P * PW2T * (int)sizeof(T), 16); // [16][PW3]
+  static constexpr int OFF_W3T = rup(OFF_W3 + 16 * PW3 * (int)sizeof(T), 16);      // [N2P][PW3T]
+  static constexpr int W_END = rup(OFF_W3T + H::N2P * PW3T * (int)sizeof(T), 16);
+  static constexpr bool WLDS = W_END <= 160 * 1024;
+  static constexpr int TOTAL = WLDS ? W_END : BASE_END;
   static constexpr bool FITS = TOTAL <= 160 * 1024;
 };
 
@@ -52,12 +66,28 @@ DEV void store_col4(T* base, float a, float b, float c, float d) {
   }
 }
 
+// copy a [rows][cols] T matrix (cols a multiple of 16 B) into LDS with row pitch `pitch`
+template <typename T, int NT>
+DEV void stage_rows(T* dst, const T* src, int rows, int cols, int pitch, int tid) {
+  constexpr int VE = 16 / (int)sizeof(T);
+  const int cv = cols / VE;
+  for (int e = tid; e < rows * cv; e += NT) {
+    const int r = e / cv, c = (e % cv) * VE;
+    *reinterpret_cast<uint4*>(dst + r * pitch + c) = *reinterpret_cast<const uint4*>(src + r * cols + c);
+  }
+}
+
+// Phase timeline of one workgroup (measured with MNIST_AMD_STAMPS, LeNet bf16 B=8192, 64-row tiles,
+// 16 waves; before this layout every phase was dominated by its B-operand fetch from L2/MALL):
+//   stage X + W2/W3 images + biases (one barrier; idx and the first L1 operands are in flight with it)
+//   L1 -> L2 -> L3 -> softmax-CE -> dH2 -> dH1 -> dX, one barrier each; the dX operands (W1^T, the
+//   largest) are fetched into registers while softmax, dH2 and dH1 run.
 template <typename T, class H, int MT, bool TRAIN, bool PRE, int NWV = 4>
 __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers hb) {
   using S = HeadSmem<T, H, MT>;
   using M = Mma<T>;
   using Frag = typename M::Frag;
-  constexpr int R = S::R, KV = M::KV, KC = M::KC;
+  constexpr int R = S::R, KV = M::KV, KC = M::KC, NTH = NWV * 64;
   static_assert(S::FITS, "head tile does not fit in LDS");
   __shared__ __attribute__((aligned(16))) char smem[S::TOTAL];
   T* sX = reinterpret_cast<T*>(smem + S::OFF_X);
@@ -66,6 +96,11 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   T* sD = reinterpret_cast<T*>(smem + S::OFF_D);
   float* sLog = reinterpret_cast<float*>(smem + S::OFF_L);
   int* sIdx = reinterpret_cast<int*>(smem + S::OFF_I);
+  int* sLab = reinterpret_cast<int*>(smem + S::OFF_LAB);
+  float* sB1 = reinterpret_cast<float*>(smem + S::OFF_B);
+  float* sB2 = sB1 + H::N1P;
+  float* sB3 = sB2 + H::N2P;
+  float* sPart = reinterpret_cast<float*>(smem + S::OFF_PART);
 
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int row = lane & 15, grp = lane >> 4;
@@ -78,8 +113,50 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   const float* prm = hb.params;
   const int ldB = hb.ldB;
 
+  // optional per-phase wall-clock stamps (MNIST_AMD_STAMPS; thread 0, one vector store each)
+  auto stamp = [&](int k) {
+    if (hb.stamps && tid == 0) hb.stamps[blockIdx.x * 16 + k] = wall_clock64();
+  };
+  stamp(0);
+
+  // B operands of each phase: LDS images when they fit (WLDS), else the packed global copies
+  const T* bW2 = S::WLDS ? reinterpret_cast<const T*>(smem + S::OFF_W2) : pack + H::F2;
+  const T* bW2T = S::WLDS ? reinterpret_cast<const T*>(smem + S::OFF_W2T) : pack + H::F2T;
+  const T* bW3 = S::WLDS ? reinterpret_cast<const T*>(smem + S::OFF_W3) : pack + H::F3;
+  const T* bW3T = S::WLDS ? reinterpret_cast<const T*>(smem + S::OFF_W3T) : pack + H::F3T;
+  constexpr int LW2 = S::WLDS ? S::PW2 : H::N1P, LW2T = S::WLDS ? S::PW2T : H::N2P;
+  constexpr int LW3 = S::WLDS ? S::PW3 : H::N2P, LW3T = S::WLDS ? S::PW3T : H::NCK;
+
+  // ---- L1 operands of this wave's first n-tile: issued first, in flight during the staging
+  constexpr int NT1 = H::N1P / 16, KCH1 = H::K0P / KC;
+  constexpr bool PF1 = !PRE && KCH1 <= 16;  // <= 64 VGPRs of prefetched fragments (LeNet bf16: 13 chunks)
+  Frag b1pre[PF1 ? KCH1 : 1];
+  if constexpr (PF1) {
+    if (w < NT1) {
+      const T* bp = pack + H::F1 + (w * 16 + row) * H::K0P + grp * KV;
+#pragma unroll
+      for (int kc = 0; kc < KCH1; ++kc) b1pre[kc] = M::load(bp + kc * KC);
+    }
+  }
+
+  // ---- staging: indices, weights, biases (+ the input tile; the MLP gather needs sIdx first)
   if (tid < R) sIdx[tid] = (r0 + tid < B) ? idx[r0 + tid] : -1;
-  __syncthreads();
+  if constexpr (S::WLDS) {
+    stage_rows<T, NTH>(reinterpret_cast<T*>(smem + S::OFF_W2), pack + H::F2, H::N2P, H::N1P, S::PW2, tid);
+    if constexpr (TRAIN) {
+      stage_rows<T, NTH>(reinterpret_cast<T*>(smem + S::OFF_W2T), pack + H::F2T, H::N1P, H::N2P, S::PW2T, tid);
+      stage_rows<T, NTH>(reinterpret_cast<T*>(smem + S::OFF_W3T), pack + H::F3T, H::N2P, H::NCK, S::PW3T, tid);
+    }
+    stage_rows<T, NTH>(reinterpret_cast<T*>(smem + S::OFF_W3), pack + H::F3, 16, H::N2P, S::PW3, tid);
+  }
+  for (int e = tid; e < H::N1P + H::N2P + 16; e += NTH) {
+    float v = 0.f;
+    if (e < H::N1P) v = e < H::N1 ? prm[H::B1 + e] : 0.f;
+    else if (e < H::N1P + H::N2P) v = (e - H::N1P) < H::N2 ? prm[H::B2 + e - H::N1P] : 0.f;
+    else v = (H::BIAS3 && e - H::N1P - H::N2P < H::NC) ? prm[H::B3 + e - H::N1P - H::N2P] : 0.f;
+    sB1[e] = v;
+  }
+  if constexpr (H::GATHER && !PRE) __syncthreads();
 
   // ---------------------------------------------------------------- stage the input tile
   // (PRE: layer 1 already ran in l1_split_kernel, which also wrote xT; X itself is not needed)
@@ -87,7 +164,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   } else if constexpr (H::GATHER) {
     constexpr int CH = H::K0P / 8;
     T* xT = reinterpret_cast<T*>(hb.xT);
-    for (int e = tid; e < R * CH; e += NWV * 64) {
+    for (int e = tid; e < R * CH; e += NTH) {
       const int r = e % R, k = (e / R) * 8;
       const int s = sIdx[r];
       float v[8];
@@ -114,7 +191,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
     constexpr int CH = H::K0P / VE;
     const T* xin = reinterpret_cast<const T*>(hb.xin);
     T* xT = reinterpret_cast<T*>(hb.xT);
-    for (int e = tid; e < R * CH; e += NWV * 64) {
+    for (int e = tid; e < R * CH; e += NTH) {
       const int r = e % R, k = (e / R) * VE;
       uint4 u = make_uint4(0, 0, 0, 0);
       if (r0 + r < B) u = *reinterpret_cast<const uint4*>(xin + (size_t)(r0 + r) * H::K0P + k);
@@ -127,6 +204,12 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
     }
   }
   __syncthreads();
+  stamp(1);
+  // labels: fetched by the LAST threads of the block (idle in L1 when NWV > NT1), used after 3 barriers
+  {
+    const int t = tid - (NTH - R);
+    if (t >= 0) sLab[t] = sIdx[t] >= 0 ? (int)br.labels[sIdx[t]] : 0;
+  }
 
   const float keep_scale = H::DROPOUT ? 1.0f / (1.0f - hb.drop_p) : 1.0f;
   const uint32_t drop_thr = H::DROPOUT ? (uint32_t)(hb.drop_p * 4294967295.0f) : 0u;
@@ -136,12 +219,12 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
     // sum the L1_KSPLIT partial products in a fixed order, then the same bias/ReLU/dropout epilogue
     T* h1T = reinterpret_cast<T*>(hb.h1T);
     const float* zp = hb.z1p;
-    for (int e = tid; e < H::N1P * R; e += NWV * 64) {
+    for (int e = tid; e < H::N1P * R; e += NTH) {
       const int n = e / R, r = e % R, rg = r0 + r;
       float z = 0.f;
 #pragma unroll
       for (int q = 0; q < L1_KSPLIT; ++q) z += zp[((size_t)q * H::N1P + n) * ldB + rg];
-      float x = fmaxf(z + (n < H::N1 ? prm[H::B1 + n] : 0.f), 0.f);
+      float x = fmaxf(z + sB1[n], 0.f);
       if constexpr (H::DROPOUT && TRAIN) {
         const uint32_t h = hash4(hb.seed, (uint32_t)gstep, (uint32_t)rg, (uint32_t)n);
         x = (h >= drop_thr) ? x * keep_scale : 0.f;
@@ -151,22 +234,24 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       if constexpr (TRAIN) h1T[(size_t)n * ldB + rg] = to_t<T>(x);
     }
   } else {
-    constexpr int NT = H::N1P / 16, KCH = H::K0P / KC;
     T* h1T = reinterpret_cast<T*>(hb.h1T);
-    for (int nt = w; nt < NT; nt += NWV) {
+    const T* ap = sX + row * S::PX + grp * KV;
+#pragma unroll
+    for (int j = 0; j < (NT1 + NWV - 1) / NWV; ++j) {
+      const int nt = w + j * NWV;
+      if (nt >= NT1) break;
       f32x4 acc[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = zero4();
       const T* bp = pack + H::F1 + (nt * 16 + row) * H::K0P + grp * KV;
-      const T* ap = sX + row * S::PX + grp * KV;
 #pragma unroll
-      for (int kc = 0; kc < KCH; ++kc) {
-        const Frag b = M::load(bp + kc * KC);
+      for (int kc = 0; kc < KCH1; ++kc) {
+        const Frag b = (PF1 && j == 0) ? b1pre[PF1 ? kc : 0] : M::load(bp + kc * KC);
 #pragma unroll
         for (int m = 0; m < MT; ++m) M::mma(acc[m], M::load(ap + m * 16 * S::PX + kc * KC), b);
       }
       const int n = nt * 16 + row;
-      const float bias = n < H::N1 ? prm[H::B1 + n] : 0.f;
+      const float bias = sB1[n];
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         float v[4];
@@ -188,6 +273,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
     }
   }
   __syncthreads();
+  stamp(2);
 
   // ---------------------------------------------------------------- L2: H2 = relu(H1 W2^T + b2)
   {
@@ -197,7 +283,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       f32x4 acc[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = zero4();
-      const T* bp = pack + H::F2 + (nt * 16 + row) * H::N1P + grp * KV;
+      const T* bp = bW2 + (nt * 16 + row) * LW2 + grp * KV;
       const T* ap = sH1 + row * S::P1 + grp * KV;
 #pragma unroll
       for (int kc = 0; kc < KCH; ++kc) {
@@ -206,7 +292,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
         for (int m = 0; m < MT; ++m) M::mma(acc[m], M::load(ap + m * 16 * S::P1 + kc * KC), b);
       }
       const int n = nt * 16 + row;
-      const float bias = n < H::N2 ? prm[H::B2 + n] : 0.f;
+      const float bias = sB2[n];
 #pragma unroll
       for (int m = 0; m < MT; ++m) {
         float v[4];
@@ -224,70 +310,107 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
     }
   }
   __syncthreads();
+  stamp(3);
 
   // ---------------------------------------------------------------- L3: logits = H2 W3^T (+ b3)
   {
     constexpr int KCH = H::N2P / KC;
     for (int m = w; m < MT; m += NWV) {
       f32x4 acc = zero4();
-      const T* bp = pack + H::F3 + row * H::N2P + grp * KV;
+      const T* bp = bW3 + row * LW3 + grp * KV;
       const T* ap = sH2 + (m * 16 + row) * S::P2 + grp * KV;
       for (int kc = 0; kc < KCH; ++kc) M::mma(acc, M::load(ap + kc * KC), M::load(bp + kc * KC));
       const int c = row;
-      const float bias = (H::BIAS3 && c < H::NC) ? prm[H::B3 + c] : 0.f;
+      const float bias = sB3[c];
 #pragma unroll
       for (int i = 0; i < 4; ++i) sLog[(m * 16 + grp * 4 + i) * 16 + c] = acc[i] + bias;
     }
   }
   __syncthreads();
+  stamp(4);
+
+  // ---- dX operands (W1^T, [K0 rows][N1P]): the first two n-tiles of this wave, fetched now so the
+  //      L2/MALL latency hides behind softmax, dH2 and dH1
+  constexpr int NTX = rup(H::K0, 16) / 16, KCHX = H::N1P / KC, PXT = KCHX <= 4 ? 2 : 1;  // <= 32 VGPRs
+  Frag bx[H::DX && TRAIN ? PXT : 1][KCHX];
+  auto prefetch_dx = [&] {
+    if constexpr (H::DX && TRAIN) {
+#pragma unroll
+      for (int j = 0; j < PXT; ++j) {
+        const int nt = w + j * NWV;
+        if (nt < NTX) {
+          const T* bp = pack + H::F1T + (nt * 16 + row) * H::N1P + grp * KV;
+#pragma unroll
+          for (int kc = 0; kc < KCHX; ++kc) bx[j][kc] = M::load(bp + kc * KC);
+        }
+      }
+    }
+  };
+
+  prefetch_dx();
 
   // ---------------------------------------------------------------- softmax cross-entropy
-  if (w == 0) {
+  // Every thread takes one (row, class) pair: t -> r = t >> 4, c = t & 15, so a row is one 16-lane
+  // group and its max / first argmax (ATen tie order) / exp-sum are xor-shuffle reductions.  dZ goes
+  // to LDS here; its transposed copy for the wgrad GEMM is stored in the dH2 phase.
+  {
     float loss = 0.f, corr = 0.f, cnt = 0.f;
-    T* dy3T = reinterpret_cast<T*>(hb.dy3T);
-    for (int r = lane; r < R; r += 64) {
-      const int rg = r0 + r;
+    for (int t = tid; t < R * 16; t += NTH) {
+      const int r = t >> 4, c = t & 15, rg = r0 + r;
       const bool valid = rg < B;
-      float z[H::NC];
-      float mx = -INFINITY;
-      int am = 0;
+      const float z = c < H::NC ? sLog[r * 16 + c] : -INFINITY;
+      float mx = z;
 #pragma unroll
-      for (int c = 0; c < H::NC; ++c) {
-        z[c] = sLog[r * 16 + c];
-        if (z[c] > mx) { mx = z[c]; am = c; }
-      }
-      float se = 0.f;
+      for (int o = 8; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 16));
+      int am = z == mx ? c : 16;
 #pragma unroll
-      for (int c = 0; c < H::NC; ++c) se += __expf(z[c] - mx);
-      const int y = valid ? (int)br.labels[sIdx[r]] : 0;
-      const float lse = mx + __logf(se);
-      if (valid) {
-        loss += lse - z[y];
+      for (int o = 8; o > 0; o >>= 1) am = min(am, __shfl_xor(am, o, 16));
+      const float e = c < H::NC ? __expf(z - mx) : 0.f;
+      float se = e;
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) se += __shfl_xor(se, o, 16);
+      const int y = sLab[r];
+      const float zy = __shfl(z, (lane & 48) | y, 64);
+      if (c == 0 && valid) {
+        loss += mx + __logf(se) - zy;
         corr += (am == y) ? 1.f : 0.f;
         cnt += 1.f;
       }
       if constexpr (TRAIN) {
-        const float inv = 1.f / se;
-#pragma unroll
-        for (int c = 0; c < H::NCK; ++c) {
-          float d = 0.f;
-          if (valid && c < H::NC) d = __expf(z[c] - mx) * inv - (c == y ? 1.f : 0.f);
-          sD[r * S::PD + c] = to_t<T>(d);
-          if (c < H::NCP) dy3T[(size_t)c * ldB + rg] = to_t<T>(d);
-        }
+        const float d = (valid && c < H::NC) ? e / se - (c == y ? 1.f : 0.f) : 0.f;
+        sD[r * S::PD + c] = to_t<T>(d);
+        sD[r * S::PD + 16 + c] = to_t<T>(0.f);  // K padding of the dH2 product (NCK = 32)
       }
     }
     loss = wave_sum(loss);
     corr = wave_sum(corr);
     cnt = wave_sum(cnt);
     if (lane == 0) {
-      atomicAdd(hb.metrics + 0, loss);
-      atomicAdd(hb.metrics + 1, corr);
-      atomicAdd(hb.metrics + 2, cnt);
+      sPart[w * 4 + 0] = loss;
+      sPart[w * 4 + 1] = corr;
+      sPart[w * 4 + 2] = cnt;
     }
   }
-  if constexpr (!TRAIN) return;
+  // tile totals -> hb.metrics at the very end (contended float atomics kept off the phases)
+  auto flush_metrics = [&] {
+    if (tid == 0) {
+      float a = 0.f, b = 0.f, c = 0.f;
+      for (int i = 0; i < NWV; ++i) {
+        a += sPart[i * 4 + 0];
+        b += sPart[i * 4 + 1];
+        c += sPart[i * 4 + 2];
+      }
+      atomicAdd(hb.metrics + 0, a);
+      atomicAdd(hb.metrics + 1, b);
+      atomicAdd(hb.metrics + 2, c);
+    }
+  };
   __syncthreads();
+  stamp(5);
+  if constexpr (!TRAIN) {
+    flush_metrics();
+    return;
+  }
 
   // ---------------------------------------------------------------- dH2 = (dZ W3) * [H2 > 0]
   {
@@ -297,7 +420,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       f32x4 acc[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = zero4();
-      const T* bp = pack + H::F3T + (nt * 16 + row) * H::NCK + grp * KV;
+      const T* bp = bW3T + (nt * 16 + row) * LW3T + grp * KV;
       const T* ap = sD + row * S::PD + grp * KV;
 #pragma unroll
       for (int kc = 0; kc < KCH; ++kc) {
@@ -320,8 +443,15 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
         store_col4<T>(dy2T + (size_t)n * ldB + r0 + m * 16 + grp * 4, v[0], v[1], v[2], v[3]);
       }
     }
+    // dZ^T for the wgrad GEMM (coalesced along the batch; waves without a dH2 tile go first)
+    T* dy3T = reinterpret_cast<T*>(hb.dy3T);
+    for (int e = tid; e < H::NCP * R; e += NTH) {
+      const int c = e / R, r = e % R;
+      dy3T[(size_t)c * ldB + r0 + r] = sD[r * S::PD + c];
+    }
   }
   __syncthreads();
+  stamp(6);
 
   // ---------------------------------------------------------------- dH1 = (dH2 W2) * [H1 > 0] / keep
   {
@@ -331,7 +461,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       f32x4 acc[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = zero4();
-      const T* bp = pack + H::F2T + (nt * 16 + row) * H::N2P + grp * KV;
+      const T* bp = bW2T + (nt * 16 + row) * LW2T + grp * KV;
       const T* ap = sH2 + row * S::P2 + grp * KV;
 #pragma unroll
       for (int kc = 0; kc < KCH; ++kc) {
@@ -359,17 +489,20 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   // ---------------------------------------------------------------- dX = dH1 W1 (LeNet: into pool2 grads)
   if constexpr (H::DX) {
     __syncthreads();
-    constexpr int NT = rup(H::K0, 16) / 16, KCH = H::N1P / KC;
+    stamp(7);
     T* dx = reinterpret_cast<T*>(hb.dx);
-    for (int nt = w; nt < NT; nt += NWV) {
+    const T* ap = sH1 + row * S::P1 + grp * KV;
+#pragma unroll
+    for (int j = 0; j < (NTX + NWV - 1) / NWV; ++j) {
+      const int nt = w + j * NWV;
+      if (nt >= NTX) break;
       f32x4 acc[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = zero4();
       const T* bp = pack + H::F1T + (nt * 16 + row) * H::N1P + grp * KV;
-      const T* ap = sH1 + row * S::P1 + grp * KV;
 #pragma unroll
-      for (int kc = 0; kc < KCH; ++kc) {
-        const Frag b = M::load(bp + kc * KC);
+      for (int kc = 0; kc < KCHX; ++kc) {
+        const Frag b = j < PXT ? bx[j < PXT ? j : 0][kc] : M::load(bp + kc * KC);
 #pragma unroll
         for (int m = 0; m < MT; ++m) M::mma(acc[m], M::load(ap + m * 16 * S::P1 + kc * KC), b);
       }
@@ -384,6 +517,8 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       }
     }
   }
+  stamp(8);
+  flush_metrics();
 }
 
 // ====================================================================================

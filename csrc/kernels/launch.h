@@ -32,6 +32,7 @@ struct HeadBuffers {
   void* dx;              // LeNet: dp2 [B][K0P]
   float* metrics;        // [loss_sum, correct, count]
   float* z1p;            // [L1_KSPLIT][N1P][ldB] fp32 layer-1 partial sums (small-batch split path) or null
+  unsigned long long* stamps;  // optional phase timestamps [block][16] (MNIST_AMD_STAMPS profiling) or null
   int32_t ldB;
   uint32_t seed;
   float drop_p;

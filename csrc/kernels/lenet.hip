@@ -285,7 +285,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
     __syncthreads();
 
     // ---- pool1 -> HBM for the backward pass (16-byte stores), overlapped with conv2
-    if (TRAIN && valid) {
+    if (TRAIN && valid && !(cb.ablate & 1024)) {
       copy_out16(reinterpret_cast<T*>(cb.p1) + (size_t)b * 196 * 8, p1s, 196 * 8 * (int)sizeof(T));
       copy_out16(cb.m1 + (size_t)b * 196 * 8, m1s, 196 * 8);
     }

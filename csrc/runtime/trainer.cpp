@@ -116,6 +116,7 @@ HeadBuffers Trainer::head_buffers(float* metrics) const {
   hb.dx = ptr<void>(p_.dp2);
   hb.metrics = metrics;
   hb.z1p = ptr<float>(p_.z1p);
+  hb.stamps = ptr<unsigned long long>(p_.stamps);
   hb.ldB = ldb_;
   hb.seed = seed_;
   hb.drop_p = drop_p_;

@@ -20,6 +20,7 @@ struct TrainerPtrs {
   uintptr_t xT = 0, h1T = 0, h2T = 0, dy1T = 0, dy2T = 0, dy3T = 0;
   uintptr_t p1 = 0, m1 = 0, p2 = 0, m2 = 0, dp2 = 0;
   uintptr_t z1p = 0;  // optional: enables the small-batch layer-1 split path
+  uintptr_t stamps = 0;  // optional: per-block phase timestamps of the head kernel (profiling)
 };
 
 // A gradient bucket = contiguous range of the flat grad slab, all-reduced as one RCCL call as

@@ -107,6 +107,9 @@ class NativeTrainer:
         P.dy1T, P.dy2T, P.dy3T = ptr(self.dy1T), ptr(self.dy2T), ptr(self.dy3T)
         P.p1, P.m1, P.p2, P.m2, P.dp2 = ptr(self.p1), ptr(self.m1), ptr(self.p2), ptr(self.m2), ptr(self.dp2)
         P.z1p = ptr(self.z1p)
+        # MNIST_AMD_STAMPS=1: per-block phase timestamps (wall clock, 100 MHz) of the head kernel
+        self.stamps = z(4096 * 16, dt=torch.int64) if os.environ.get("MNIST_AMD_STAMPS") else None
+        P.stamps = ptr(self.stamps)
         self._ptrs = P
         self.rt = C.Trainer(mid, did, self.batch, self.ld_b, fc_splits, P)
         self.rt.set_optimizer(float(lr), float(momentum))
