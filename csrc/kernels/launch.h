@@ -48,6 +48,7 @@ struct LenetConvBuffers {
   const void* dp2;       // [B][416] T   (backward input)
   float* slab;           // conv partial grads, row per workgroup: [G][2572]
   int ablate = 0;        // diagnostics only: bitmask of phases to skip (timing ablation, wrong results)
+  unsigned long long* stamps = nullptr;  // optional phase timestamps (profiling): fwd [block][16], bwd [block][16]
 };
 
 int head_rows_per_block(ModelKind m, DType t, int B);

@@ -90,6 +90,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   const int32_t* idx = br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride;
   const T* pack = reinterpret_cast<const T*>(cb.pack);
   const float* prm = cb.params;
+  // optional wall-clock stamps (profiling): [0] start, [1] setup, 3 per image for images 0..3, [14] loop end
+  auto stamp = [&](int k) {
+    if (cb.stamps && tid == 0) cb.stamps[(1024 + blockIdx.x) * 16 + k] = wall_clock64();
+  };
+  stamp(0);
 
   constexpr int C1CH = 64 / KC;                 // conv1 K = 5 rows x 8 (kw padded)
   constexpr int C2CH = (25 * 8 + KC - 1) / KC;  // conv2 K = 25 taps x 8 ch (7 bf16 / 13 f32 chunks)
@@ -203,6 +208,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   };
   Raw u_next = fetch(0);
   __syncthreads();
+  stamp(1);
   for (int t = 0; t < ipb; ++t) {
     const int b = blockIdx.x * ipb + t;
     const bool valid = b < br.B;
@@ -259,6 +265,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
       }
     }
     __syncthreads();
+    if (t < 4) stamp(2 + 3 * t);
 
     // ---- conv1 + bias + ReLU + maxpool: 7 two-row tiles per wave
     if (!(cb.ablate & 2)) {
@@ -283,6 +290,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
       c1_epi(6, prev);
     }
     __syncthreads();
+    if (t < 4) stamp(3 + 3 * t);
 
     // ---- pool1 -> HBM for the backward pass (16-byte stores), overlapped with conv2
     if (TRAIN && valid && !(cb.ablate & 1024)) {
@@ -304,7 +312,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
       }
     }
     __syncthreads();
+    if (t < 4) stamp(4 + 3 * t);
   }
+  stamp(14);
   flush_p2(blockIdx.x * ipb + ipb - 1);
 }
 
@@ -362,6 +372,12 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   const T* pack = reinterpret_cast<const T*>(cb.pack);
   const T* dp2 = reinterpret_cast<const T*>(cb.dp2);
   const T* p1g = reinterpret_cast<const T*>(cb.p1);
+  // optional wall-clock stamps (profiling): [0] start, [1] setup, 3 per image for images 0..3,
+  // [14] loop end, [15] slab written
+  auto stamp = [&](int k) {
+    if (cb.stamps && tid == 0) cb.stamps[blockIdx.x * 16 + k] = wall_clock64();
+  };
+  stamp(0);
 
   constexpr int W2CH = 160 / KC;              // conv2 wgrad: 10 rows x 16 positions
   constexpr int D2CH = 480 / KC;              // conv2 dgrad K = 30 taps (kh' = -1..4) x 16 ch (15 bf16 / 30 f32)
@@ -432,6 +448,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   accW1[0] = zero4();
   accW1[1] = zero4();
   __syncthreads();
+  stamp(1);
 
   // ---- software pipeline: every global input of image t+1 is loaded into registers while
   //      image t computes (phases B and C), so phase A only moves registers into LDS
@@ -523,6 +540,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
       }
     }
     __syncthreads();
+    if (t < 4) stamp(2 + 3 * t);
 
     // ---- phase B1: conv2 wgrad  dW2[n][tap*8+c] += sum_pos dY2[pos][n] * pool1[pos + tap][c]
     for (int kc = 0; kc < ((cb.ablate & 64) ? 0 : W2CH); ++kc) {
@@ -595,6 +613,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
       }
     }
     __syncthreads();
+    if (t < 4) stamp(3 + 3 * t);
 
     // ---- phase C: conv1 wgrad  dW1[n][tap] += sum_pos dY1[pos][n] * xpad[pos + tap]
     for (int kc = w; kc < ((cb.ablate & 512) ? 0 : W1CH); kc += 4) {
@@ -604,7 +623,9 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
       for (int nt = 0; nt < 2; ++nt) M::mma(accW1[nt], a, M::load(xs + w1off[nt] + oh * 32 + ow0));
     }
     __syncthreads();
+    if (t < 4) stamp(4 + 3 * t);
   }
+  stamp(14);
 
   // ---- write this workgroup's partial gradients (slab row = blockIdx.x)
   float* out = cb.slab + (size_t)blockIdx.x * L::CONV_PARAMS;
@@ -637,6 +658,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
       else if (kcol == 25) out[L::CB1 + n] = v;
     }
   }
+  stamp(15);
 }
 
 }  // namespace

@@ -138,6 +138,8 @@ LenetConvBuffers Trainer::conv_buffers() const {
     return e ? std::atoi(e) : 0;
   }();
   cb.ablate = ablate;
+  // stamps layout (16 slots per workgroup): head blocks [0, 1024), conv_bwd [1024, 2048), conv_fwd [2048, 4096)
+  cb.stamps = p_.stamps ? ptr<unsigned long long>(p_.stamps) + 1024 * 16 : nullptr;
   return cb;
 }
 

@@ -28,14 +28,33 @@ tr.reset_metrics()
 for _ in range(6):
     tr.step(B, use_graph=True)
 tr.synchronize()
+allst = tr.stamps.view(-1, 16).cpu().numpy().astype(np.int64)
+
+
+def report(title, st, names, last):
+    """st: [blocks][16] stamps; names[k] = phase between stamp k and k+1; `last` = final stamp slot."""
+    t0 = st[:, 0].min()
+    print(f"{title}: {len(st)} workgroups; start spread {(st[:, 0].max() - t0) * 10 / 1000:.2f} us; "
+          f"span {(st[:, last].max() - t0) * 10 / 1000:.2f} us")
+    for k, n in enumerate(names):
+        if n is None:
+            continue
+        d = (st[:, k + 1] - st[:, k]) * 10 / 1000.0
+        print(f"  {n:16s} mean {d.mean():7.2f} us  min {d.min():7.2f}  max {d.max():7.2f}")
+    tot = (st[:, last] - st[:, 0]) * 10 / 1000.0
+    print(f"  {'total':16s} mean {tot.mean():7.2f} us  min {tot.min():7.2f}  max {tot.max():7.2f}")
+
+
 nblk = (B + 63) // 64
-st = tr.stamps.view(-1, 16)[:nblk].cpu().numpy().astype(np.int64)
-names = ["idx+stage X", "L1", "L2", "L3", "softmax", "dH2", "dH1", "dX"]
-t0 = st[:, 0].min()
-print(f"head workgroups: {nblk}; start spread {(st[:, 0].max() - t0) * 10 / 1000:.2f} us; "
-      f"kernel span {(st[:, 8].max() - t0) * 10 / 1000:.2f} us")
-for k, n in enumerate(names):
-    d = (st[:, k + 1] - st[:, k]) * 10 / 1000.0
-    print(f"  {n:12s} mean {d.mean():7.2f} us  min {d.min():7.2f}  max {d.max():7.2f}")
-tot = (st[:, 8] - st[:, 0]) * 10 / 1000.0
-print(f"  {'total':12s} mean {tot.mean():7.2f} us  min {tot.min():7.2f}  max {tot.max():7.2f}")
+report("head", allst[:nblk], ["idx+stage X", "L1", "L2", "L3", "softmax", "dH2", "dH1", "dX"], 8)
+if model == "lenet5":
+    per_img = []
+    for t in range(4):
+        per_img += [f"img{t} stage" if t == 0 else f"img{t} stage(+prev)", f"img{t} conv1", f"img{t} conv2"]
+    nf = (B + 7) // 8 if B >= 1024 else B
+    report("conv_fwd", allst[2048:2048 + min(nf, 1024)], ["setup"] + per_img, 14)
+    nb = 512 if B >= 512 else B
+    bnames = ["setup"]
+    for t in range(4):
+        bnames += [f"img{t} A (stage)", f"img{t} B (w2+dgrad)", f"img{t} C (w1)"]
+    report("conv_bwd", allst[1024:1024 + nb], bnames + [None, "slab write"], 15)
