@@ -67,8 +67,9 @@ int launch_head_wgrad(ModelKind m, DType t, const HeadBuffers& hb, int B, int sp
 
 void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetConvBuffers& cb,
                            hipStream_t s);
+// mode 0: full backward; 1: conv2 dgrad + conv1 wgrad half; 2: conv2 wgrad half (lenet.hip MODE)
 void launch_lenet_conv_bwd(DType t, const BatchRef& br, const LenetConvBuffers& cb, int* nslab_out,
-                           hipStream_t s);
+                           hipStream_t s, int mode = 0);
 int lenet_conv_bwd_blocks(int B);
 
 // grad[p] = scale * sum_s slab[s][p]  for p in [p0, p1)
@@ -82,8 +83,8 @@ void launch_sgd_pack(ModelKind m, DType t, float* params, const float* grad, flo
 void launch_pack(ModelKind m, DType t, const float* params, void* pack, int nparam, hipStream_t s);
 // Fused gradient reduce + SGD + pack + step bump (no all-reduce between them: single-GPU runs).
 void launch_reduce_sgd(ModelKind m, DType t, const float* slab_a, int lda, int na, const float* slab_b, int ldb,
-                       int nb, int split, int n, float scale, float* params, float* grad, float* mom, void* pack,
-                       float lr, float momentum, int32_t* step_ptr, hipStream_t s);
+                       int nb, int split, int p0, int n, float scale, float* params, float* grad, float* mom,
+                       void* pack, float lr, float momentum, int32_t* step_ptr, hipStream_t s);  // params [p0, n)
 
 void launch_gather_normalize(DType t, const BatchRef& br, void* out, int ld, hipStream_t s);
 

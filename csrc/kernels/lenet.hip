@@ -331,8 +331,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
 // The pool1 un-pooling (argmax + ReLU) is fused into the conv2-dgrad epilogue, which writes DY1T
 // directly; pool2 un-pooling is a cooperative scatter.  Both scatters write every position of
 // their map (2x2 windows tile it), so nothing but the padding is ever zero-filled.
-template <typename T>
+// MODE splits the kernel into two independent halves that run CONCURRENTLY on two streams, with the
+// block -> images mapping and per-block accumulation order of MODE 0 (so the slab rows are bitwise
+// those of the full kernel; each half writes its own columns):
+//   MODE 0 full | MODE 1 dgrad side (XS, DYS, W2R, DY1T, M1: conv2 dgrad, pool1 un-pooling, conv1
+//   wgrad) | MODE 2 conv2-wgrad side (P1T, DY2T: 21 KB of LDS, fills the room MODE 1 leaves per CU)
+template <typename T, int MODE = 0>
 struct BwdSmem {
+  static constexpr bool HD = MODE != 2, HW = MODE != 1;  // dgrad side / conv2-wgrad side present
   // pitches padded so the fragment reads and the un-pooling scatters are <= 2-way bank
   // conflicted (measured 60% conflict cycles with the unpadded 1024/224/160/896 pitches)
   // W2R: conv2 dgrad B operand for TWO output rows per tile, [16 = (r, c)][30 taps x 16 ch + pad]
@@ -341,22 +347,23 @@ struct BwdSmem {
   // ones): padding / bias-gradient columns read a constant plane instead of branching per lane
   static constexpr int XPL = 7, PPL = 32;
   static constexpr int OFF_XS = 0;
-  static constexpr int OFF_P1T = rup(OFF_XS + XPL * XP * (int)sizeof(T), 16);
-  static constexpr int OFF_DY2T = rup(OFF_P1T + PPL * P1P * (int)sizeof(T), 16);
-  static constexpr int OFF_DYS = rup(OFF_DY2T + 16 * D2P * (int)sizeof(T), 16);   // [18][18][16] zero-padded
-  static constexpr int OFF_W2 = rup(OFF_DYS + 18 * 18 * 16 * (int)sizeof(T), 16);
-  static constexpr int OFF_DY1T = rup(OFF_W2 + 16 * W2P * (int)sizeof(T), 16);
-  static constexpr int OFF_M1 = rup(OFF_DY1T + 8 * D1P * (int)sizeof(T), 16);   // [6][14][16] u8 pool1 codes
-  static constexpr int TOTAL = rup(OFF_M1 + 6 * 14 * 16, 16);
-  static constexpr int OFF_RED = OFF_XS;  // [4][2][256] f32 scratch after the image loop
-  static_assert(4 * 2 * 256 * 4 <= OFF_P1T, "reduction scratch must fit in the aliased XS region");
+  static constexpr int OFF_P1T = rup(OFF_XS + (HD ? XPL * XP * (int)sizeof(T) : 0), 16);
+  static constexpr int OFF_DY2T = rup(OFF_P1T + (HW ? PPL * P1P * (int)sizeof(T) : 0), 16);
+  static constexpr int OFF_DYS = rup(OFF_DY2T + (HW ? 16 * D2P * (int)sizeof(T) : 0), 16);  // [18][18][16] zero-padded
+  static constexpr int OFF_W2 = rup(OFF_DYS + (HD ? 18 * 18 * 16 * (int)sizeof(T) : 0), 16);
+  static constexpr int OFF_DY1T = rup(OFF_W2 + (HD ? 16 * W2P * (int)sizeof(T) : 0), 16);
+  static constexpr int OFF_M1 = rup(OFF_DY1T + (HD ? 8 * D1P * (int)sizeof(T) : 0), 16);  // [6][14][16] u8 pool1 codes
+  static constexpr int TOTAL = rup(OFF_M1 + (HD ? 6 * 14 * 16 : 0), 16);
+  static constexpr int OFF_RED = OFF_XS;  // [4][2][256] f32 scratch after the image loop (dgrad side)
+  static_assert(!HD || 4 * 2 * 256 * 4 <= XPL * XP * (int)sizeof(T), "reduction scratch must fit in the aliased XS region");
 };
 
-template <typename T>
+template <typename T, int MODE>
 __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
   using M = Mma<T>;
   using Frag = typename M::Frag;
-  using S = BwdSmem<T>;
+  using S = BwdSmem<T, MODE>;
+  constexpr bool HD = S::HD, HW = S::HW;
   constexpr int KV = M::KV, KC = M::KC;
   __shared__ __attribute__((aligned(16))) char smem[S::TOTAL];
   T* xs = reinterpret_cast<T*>(smem + S::OFF_XS);
@@ -375,7 +382,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   // optional wall-clock stamps (profiling): [0] start, [1] setup, 3 per image for images 0..3,
   // [14] loop end, [15] slab written
   auto stamp = [&](int k) {
-    if (cb.stamps && tid == 0) cb.stamps[blockIdx.x * 16 + k] = wall_clock64();
+    if (cb.stamps && tid == 0) cb.stamps[(blockIdx.x + (MODE == 2 ? 512 : 0)) * 16 + k] = wall_clock64();
   };
   stamp(0);
 
@@ -386,19 +393,23 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   //  shuttle accumulators VGPR<->AGPR around every MFMA -- the B operand is read from LDS)
 
   // ---- once per workgroup: zero every padded image, stage C2d
-  zero_lds<T>(xs, 6 * S::XP);
-  zero_lds<T>(p1t, 31 * S::P1P);
-  for (int e = tid; e < S::XP; e += 256) xs[6 * S::XP + e] = to_t<T>(1.f);
-  for (int e = tid; e < S::P1P; e += 256) p1t[31 * S::P1P + e] = to_t<T>(1.f);
-  zero_lds<T>(dy2t, 16 * S::D2P);
-  zero_lds<T>(dy1t, 8 * S::D1P);
-  zero_lds<T>(dys, 18 * 18 * 16);
+  if constexpr (HD) {
+    zero_lds<T>(xs, 6 * S::XP);
+    for (int e = tid; e < S::XP; e += 256) xs[6 * S::XP + e] = to_t<T>(1.f);
+    zero_lds<T>(dy1t, 8 * S::D1P);
+    zero_lds<T>(dys, 18 * 18 * 16);
+  }
+  if constexpr (HW) {
+    zero_lds<T>(p1t, 31 * S::P1P);
+    for (int e = tid; e < S::P1P; e += 256) p1t[31 * S::P1P + e] = to_t<T>(1.f);
+    zero_lds<T>(dy2t, 16 * S::D2P);
+  }
   // conv2 dgrad, two output rows per tile: out (Y = y + r, x, c) = sum over kh' in [-1, 4], kw, n of
   // dY2[y - kh'][x - kw][n] * W2[n][c][kh' + r][kw]  ->  B[(kh'+1)*5 + kw, n][(r, c)], zero where
   // kh' + r is outside 0..4.  N = (r, c) holds 12 live columns of 16 (was 6 with one row per tile).
   // Row (r, c) is C2D row c shifted by 5 taps: r = 0 -> [80 zeros | C2D[c][0..400)], r = 1 ->
   // [C2D[c][0..400) | 80 zeros]; copied as 16-byte vectors (rows c >= 6 are all zero).
-  {
+  if constexpr (HD) {
     constexpr int VE = 16 / (int)sizeof(T), RV = 480 / VE, SH = 80 / VE;
     for (int e = tid; e < 16 * RV; e += 256) {
       const int nr = e / RV, v = e % RV, r = nr >> 3, c = nr & 7;
@@ -466,11 +477,15 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     const int bb = blockIdx.x * ipb + t;
     if (t >= ipb || bb >= br.B) return f;
     if (tid < 196) {
-      f.u = *reinterpret_cast<const uint32_t*>(br.images + (size_t)idx[bb] * 784 + tid * 4);
-      const uint4* ps = reinterpret_cast<const uint4*>(p1g + ((size_t)bb * 196 + tid) * 8);
-      f.p[0] = ps[0];
-      if constexpr (sizeof(T) == 4) f.p[1] = ps[1];
-      f.m = *reinterpret_cast<const uint2*>(cb.m1 + ((size_t)bb * 196 + tid) * 8);
+      if constexpr (HD) {
+        f.u = *reinterpret_cast<const uint32_t*>(br.images + (size_t)idx[bb] * 784 + tid * 4);
+        f.m = *reinterpret_cast<const uint2*>(cb.m1 + ((size_t)bb * 196 + tid) * 8);
+      }
+      if constexpr (HW) {
+        const uint4* ps = reinterpret_cast<const uint4*>(p1g + ((size_t)bb * 196 + tid) * 8);
+        f.p[0] = ps[0];
+        if constexpr (sizeof(T) == 4) f.p[1] = ps[1];
+      }
     }
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
@@ -492,7 +507,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     nxt = fetch(t + 1);
     // ---- phase A: stage input (5 shifted copies), pool1 (5 shifted channel-major copies),
     //      pool1 codes, and the pool2 un-pooling scatter into DYS / DY2T
-    if (tid < 196 && !(cb.ablate & 8)) {
+    if (HD && tid < 196 && !(cb.ablate & 8)) {
       const uint32_t u = cur.u;
       const int k = tid * 4, y = k / 28 + 2, x = k % 28 + 2;
 #pragma unroll
@@ -504,16 +519,16 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
           if (xx >= 0) xs[kw * S::XP + y * 32 + xx] = v;
         }
       }
+      const int cy = tid / 14, cx = tid % 14;
+      const uint32_t mm[2] = {cur.m.x, cur.m.y};
+#pragma unroll
+      for (int c = 0; c < 6; ++c) m1s[(c * 14 + cy) * 16 + cx] = (uint8_t)(mm[c >> 2] >> (8 * (c & 3)));
+    }
+    if (HW && tid < 196 && !(cb.ablate & 8)) {
       // pool1 position tid: 8 channels
       T pv[8];
       *reinterpret_cast<uint4*>(pv) = cur.p[0];
       if constexpr (sizeof(T) == 4) *reinterpret_cast<uint4*>(pv + 4) = cur.p[1];
-      {
-        const int cy = tid / 14, cx = tid % 14;
-        const uint32_t mm[2] = {cur.m.x, cur.m.y};
-#pragma unroll
-        for (int c = 0; c < 6; ++c) m1s[(c * 14 + cy) * 16 + cx] = (uint8_t)(mm[c >> 2] >> (8 * (c & 3)));
-      }
       const int py = tid / 14, px = tid % 14;
 #pragma unroll
       for (int kw = 0; kw < 5; ++kw) {
@@ -535,15 +550,15 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
       for (int win = 0; win < 4; ++win) {
         const int oh = 2 * py + (win >> 1), ow = 2 * px + (win & 1);
         const T v = to_t<T>(((code & 4) && (code & 3) == win) ? g : 0.f);
-        dys[((oh + 4) * 18 + ow + 4) * 16 + n] = v;
-        dy2t[n * S::D2P + oh * 16 + ow] = v;
+        if constexpr (HD) dys[((oh + 4) * 18 + ow + 4) * 16 + n] = v;
+        if constexpr (HW) dy2t[n * S::D2P + oh * 16 + ow] = v;
       }
     }
     __syncthreads();
     if (t < 4) stamp(2 + 3 * t);
 
     // ---- phase B1: conv2 wgrad  dW2[n][tap*8+c] += sum_pos dY2[pos][n] * pool1[pos + tap][c]
-    for (int kc = 0; kc < ((cb.ablate & 64) ? 0 : W2CH); ++kc) {
+    for (int kc = 0; kc < ((!HW || (cb.ablate & 64)) ? 0 : W2CH); ++kc) {
       const int p0 = kc * KC + grp * KV, oh = p0 >> 4, ow0 = p0 & 15;
       const Frag a = M::load(dy2t + row * S::D2P + p0);
       // unconditional loads + MFMAs (unused tiles read the zero plane): a lane-divergent branch
@@ -588,7 +603,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
       };
       const int x = min(row, 13);
       const T* bq = w2 + row * S::W2P + grp * KV;
-      if (!(cb.ablate & 128)) {
+      if (HD && !(cb.ablate & 128)) {
         if (np == 2) {
           const int y0 = 2 * q0, y1 = y0 + 2;
           const T* a0 = dys + ((y0 + 4) * 18 + x + 4) * 16;
@@ -616,14 +631,16 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     if (t < 4) stamp(3 + 3 * t);
 
     // ---- phase C: conv1 wgrad  dW1[n][tap] += sum_pos dY1[pos][n] * xpad[pos + tap]
-    for (int kc = w; kc < ((cb.ablate & 512) ? 0 : W1CH); kc += 4) {
-      const int p0 = kc * KC + grp * KV, oh = p0 >> 5, ow0 = p0 & 31;
-      const Frag a = M::load(dy1t + min(row, 7) * S::D1P + p0);  // rows 6..15: DY1T rows 6/7 are zero
+    if constexpr (HD) {
+      for (int kc = w; kc < ((cb.ablate & 512) ? 0 : W1CH); kc += 4) {
+        const int p0 = kc * KC + grp * KV, oh = p0 >> 5, ow0 = p0 & 31;
+        const Frag a = M::load(dy1t + min(row, 7) * S::D1P + p0);  // rows 6..15: DY1T rows 6/7 are zero
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) M::mma(accW1[nt], a, M::load(xs + w1off[nt] + oh * 32 + ow0));
+        for (int nt = 0; nt < 2; ++nt) M::mma(accW1[nt], a, M::load(xs + w1off[nt] + oh * 32 + ow0));
+      }
+      __syncthreads();
+      if (t < 4) stamp(4 + 3 * t);
     }
-    __syncthreads();
-    if (t < 4) stamp(4 + 3 * t);
   }
   stamp(14);
 
@@ -631,7 +648,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   float* out = cb.slab + (size_t)blockIdx.x * L::CONV_PARAMS;
 #pragma unroll
   for (int i = 0; i < NWT; ++i) {
-    if (i >= nw) break;
+    if (!HW || i >= nw) break;
     const int kcol = (n0w + i) * 16 + row;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -644,18 +661,20 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
       }
     }
   }
+  if constexpr (HD) {
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt)
+    for (int nt = 0; nt < 2; ++nt)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) red[(w * 2 + nt) * 256 + (grp * 4 + r) * 16 + row] = accW1[nt][r];
-  __syncthreads();
-  for (int e = tid; e < 512; e += 256) {
-    const int nt = e >> 8, ix = e & 255, n = ix >> 4, kcol = nt * 16 + (ix & 15);
-    const float v = (red[(0 * 2 + nt) * 256 + ix] + red[(1 * 2 + nt) * 256 + ix]) +
-                    (red[(2 * 2 + nt) * 256 + ix] + red[(3 * 2 + nt) * 256 + ix]);
-    if (n < 6) {
-      if (kcol < 25) out[L::CW1 + n * 25 + kcol] = v;
-      else if (kcol == 25) out[L::CB1 + n] = v;
+      for (int r = 0; r < 4; ++r) red[(w * 2 + nt) * 256 + (grp * 4 + r) * 16 + row] = accW1[nt][r];
+    __syncthreads();
+    for (int e = tid; e < 512; e += 256) {
+      const int nt = e >> 8, ix = e & 255, n = ix >> 4, kcol = nt * 16 + (ix & 15);
+      const float v = (red[(0 * 2 + nt) * 256 + ix] + red[(1 * 2 + nt) * 256 + ix]) +
+                      (red[(2 * 2 + nt) * 256 + ix] + red[(3 * 2 + nt) * 256 + ix]);
+      if (n < 6) {
+        if (kcol < 25) out[L::CW1 + n * 25 + kcol] = v;
+        else if (kcol == 25) out[L::CB1 + n] = v;
+      }
     }
   }
   stamp(15);
@@ -689,10 +708,18 @@ void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetC
   }
 }
 
-void launch_lenet_conv_bwd(DType t, const BatchRef& br, const LenetConvBuffers& cb, int* nslab_out, hipStream_t s) {
+void launch_lenet_conv_bwd(DType t, const BatchRef& br, const LenetConvBuffers& cb, int* nslab_out, hipStream_t s,
+                           int mode) {
   const int ipb = bwd_ipb(br.B), grid = (br.B + ipb - 1) / ipb;
   if (nslab_out) *nslab_out = grid;
   if (br.B <= 0) return;
-  if (t == DType::F32) hipLaunchKernelGGL(conv_bwd_kernel<float>, dim3(grid), dim3(256), 0, s, br, cb, ipb);
-  else hipLaunchKernelGGL(conv_bwd_kernel<bf16>, dim3(grid), dim3(256), 0, s, br, cb, ipb);
+  if (t == DType::F32) {
+    if (mode == 1) hipLaunchKernelGGL((conv_bwd_kernel<float, 1>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
+    else if (mode == 2) hipLaunchKernelGGL((conv_bwd_kernel<float, 2>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
+    else hipLaunchKernelGGL((conv_bwd_kernel<float, 0>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
+  } else {
+    if (mode == 1) hipLaunchKernelGGL((conv_bwd_kernel<bf16, 1>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
+    else if (mode == 2) hipLaunchKernelGGL((conv_bwd_kernel<bf16, 2>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
+    else hipLaunchKernelGGL((conv_bwd_kernel<bf16, 0>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
+  }
 }

@@ -26,6 +26,17 @@ __device__ __forceinline__ float slab_partial(const float* __restrict__ slab, in
   const int sb = w * per, se = min(nslab, sb + per);
   int k = sb;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  // 32 rows per round, all loads issued before the first add (the 512-row conv slab is one round per
+  // wave instead of four dependent ones); same per-accumulator addition order as the 8-row loop below
+  for (; k + 32 <= se; k += 32) {
+    float v[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) v[i] = slab[(size_t)(k + i) * ld + p];
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += v[g * 8 + i];
+  }
   for (; k + 8 <= se; k += 8) {
     float v[8];
 #pragma unroll
@@ -86,18 +97,19 @@ __global__ __launch_bounds__(256) void sgd_pack_kernel(float* __restrict__ param
 
 // Fused  grad = scale * sum_s slab[s]  ->  SGD(+momentum)  ->  re-pack, for runs without a gradient
 // all-reduce (one GPU): saves two kernel boundaries and the grad round trip per step.  Parameters
-// [0, split) reduce slab_a, [split, n) reduce slab_b (LeNet: conv slab / FC slab).  One block = 64
+// [p0, n): below `split` from slab_a, the rest from slab_b (LeNet: conv slab / FC slab; the concurrent
+// schedule updates the FC range right after the FC wgrad, the conv range after conv_bwd).  One block = 64
 // parameters x NW waves over the slab rows (same fixed summation tree as reduce_slabs_kernel).
 template <class Model, typename T, int NW>
 __global__ __launch_bounds__(NW * 64) void reduce_sgd_kernel(const float* __restrict__ slab_a, int lda, int na,
                                                              const float* __restrict__ slab_b, int ldb, int nb,
-                                                             int split, int n, float scale, float* __restrict__ params,
+                                                             int split, int p0, int n, float scale, float* __restrict__ params,
                                                              float* __restrict__ grad, float* __restrict__ mom,
                                                              T* __restrict__ pack, float lr, float mu,
                                                              int32_t* step_ptr) {
   __shared__ float part[NW][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int p = blockIdx.x * 64 + lane;
+  const int p = p0 + blockIdx.x * 64 + lane;
   float s = 0.f;
   if (p < n) {
     const bool a = p < split;
@@ -127,12 +139,13 @@ __global__ __launch_bounds__(NW * 64) void reduce_sgd_kernel(const float* __rest
 }
 
 template <class Model, typename T>
-void reduce_sgd_t(const float* sa, int lda, int na, const float* sb, int ldb, int nb, int split, int n, float scale,
+void reduce_sgd_t(const float* sa, int lda, int na, const float* sb, int ldb, int nb, int split, int p0, int n, float scale,
                   float* params, float* grad, float* mom, void* pack, float lr, float mu, int32_t* step_ptr,
                   hipStream_t s) {
-  const int grid = (n + 63) / 64;
+  const int grid = (n - p0 + 63) / 64;
+  if (grid <= 0) return;
   hipLaunchKernelGGL((reduce_sgd_kernel<Model, T, RNW>), dim3(grid), dim3(RNW * 64), 0, s, sa, lda, na, sb, ldb, nb, split,
-                     n, scale, params, grad, mom, reinterpret_cast<T*>(pack), lr, mu, step_ptr);
+                     p0, n, scale, params, grad, mom, reinterpret_cast<T*>(pack), lr, mu, step_ptr);
 }
 
 template <class Model, typename T>
@@ -198,14 +211,14 @@ int model_conv_params(ModelKind m) { return m == ModelKind::MLP ? 0 : LenetModel
 int model_pack_size(ModelKind m) { return m == ModelKind::MLP ? MlpModel::PACK_SIZE : LenetModel::PACK_SIZE; }
 
 void launch_reduce_sgd(ModelKind m, DType t, const float* slab_a, int lda, int na, const float* slab_b, int ldb,
-                       int nb, int split, int n, float scale, float* params, float* grad, float* mom, void* pack,
-                       float lr, float momentum, int32_t* step_ptr, hipStream_t s) {
+                       int nb, int split, int p0, int n, float scale, float* params, float* grad, float* mom,
+                       void* pack, float lr, float momentum, int32_t* step_ptr, hipStream_t s) {
   float* mb = momentum != 0.f ? mom : nullptr;
   if (m == ModelKind::MLP) {
-    if (t == DType::F32) reduce_sgd_t<MlpModel, float>(slab_a, lda, na, slab_b, ldb, nb, split, n, scale, params, grad, mb, pack, lr, momentum, step_ptr, s);
-    else reduce_sgd_t<MlpModel, bf16>(slab_a, lda, na, slab_b, ldb, nb, split, n, scale, params, grad, mb, pack, lr, momentum, step_ptr, s);
+    if (t == DType::F32) reduce_sgd_t<MlpModel, float>(slab_a, lda, na, slab_b, ldb, nb, split, p0, n, scale, params, grad, mb, pack, lr, momentum, step_ptr, s);
+    else reduce_sgd_t<MlpModel, bf16>(slab_a, lda, na, slab_b, ldb, nb, split, p0, n, scale, params, grad, mb, pack, lr, momentum, step_ptr, s);
   } else {
-    if (t == DType::F32) reduce_sgd_t<LenetModel, float>(slab_a, lda, na, slab_b, ldb, nb, split, n, scale, params, grad, mb, pack, lr, momentum, step_ptr, s);
-    else reduce_sgd_t<LenetModel, bf16>(slab_a, lda, na, slab_b, ldb, nb, split, n, scale, params, grad, mb, pack, lr, momentum, step_ptr, s);
+    if (t == DType::F32) reduce_sgd_t<LenetModel, float>(slab_a, lda, na, slab_b, ldb, nb, split, p0, n, scale, params, grad, mb, pack, lr, momentum, step_ptr, s);
+    else reduce_sgd_t<LenetModel, bf16>(slab_a, lda, na, slab_b, ldb, nb, split, p0, n, scale, params, grad, mb, pack, lr, momentum, step_ptr, s);
   }
 }

@@ -46,6 +46,17 @@ int concurrent_mode() {
   }();
   return m;
 }
+// MNIST_AMD_SPLIT_BWD=1 (concurrent schedule only): conv_bwd runs as its two halves, the dgrad side on
+// the main stream and the conv2-wgrad side on the aux stream (lenet.hip MODE 1 / 2).  Bitwise equal to
+// the full kernel (tests/test_schedules_gpu.py) but measured SLOWER (0.184 vs 0.157 ms/step: the two
+// halves contend for the same LDS bandwidth and the dgrad half alone is only 15% shorter), so off.
+bool split_bwd() {
+  static const bool on = [] {
+    const char* e = std::getenv("MNIST_AMD_SPLIT_BWD");
+    return e ? std::atoi(e) != 0 : false;
+  }();
+  return on;
+}
 inline hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 template <typename P> P* ptr(uintptr_t v) { return reinterpret_cast<P*>(v); }
 }  // namespace
@@ -242,15 +253,25 @@ void Trainer::launch_step(int B, hipStream_t s) {
     HIP_CHECK(hipEventRecord(events_[4], s));
     HIP_CHECK(hipStreamWaitEvent(aux_stream_, events_[4], 0));
     int nslab = 0;
-    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s);
+    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s, split_bwd() ? 1 : 0);
     post_launch(s);
+    if (split_bwd()) {
+      launch_lenet_conv_bwd(dtype_, br, conv_buffers(), nullptr, aux_stream_, 2);
+      post_launch(aux_stream_);
+    }
     const int splits =
         launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, aux_stream_, hrows);
+    post_launch(aux_stream_);
+    // the FC update follows the FC wgrad on the aux stream (it touches only FC parameters and FC
+    // operand images); the conv update + step bump follows the join
+    launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
+                      nparam_, splits, cp, cp, nparam_, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
+                      ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, nullptr, aux_stream_);
     post_launch(aux_stream_);
     HIP_CHECK(hipEventRecord(events_[5], aux_stream_));
     HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));
     launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
-                      nparam_, splits, cp, nparam_, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
+                      nparam_, splits, cp, 0, cp, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
                       ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, ptr<int32_t>(p_.step), s);
     post_launch(s);
     return;
@@ -265,7 +286,7 @@ void Trainer::launch_step(int B, hipStream_t s) {
       post_launch(s);
     }
     launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
-                      nparam_, splits, cp, nparam_, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
+                      nparam_, splits, cp, 0, nparam_, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
                       ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, ptr<int32_t>(p_.step), s);
     post_launch(s);
     return;
@@ -303,14 +324,19 @@ void Trainer::launch_step_concurrent_comm(int B, int hrows, hipStream_t s) {
   HIP_CHECK(hipEventRecord(events_[4], s));
   HIP_CHECK(hipStreamWaitEvent(aux_stream_, events_[4], 0));
   int nslab = 0;
-  launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s);
+  launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s, split_bwd() ? 1 : 0);
   post_launch(s);
+  if (split_bwd()) {
+    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), nullptr, aux_stream_, 2);
+    post_launch(aux_stream_);
+  }
   const int splits =
       launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, aux_stream_, hrows);
   post_launch(aux_stream_);
   launch_reduce(ptr<const float>(p_.slab_fc), nparam_, splits, cp, nparam_, scale, ptr<float>(p_.grad), aux_stream_);
   post_launch(aux_stream_);
   HIP_CHECK(hipEventRecord(events_[5], aux_stream_));
+  if (split_bwd()) HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));  // conv2 columns come from the aux half
   launch_reduce(ptr<const float>(p_.slab_conv), cp, nslab, 0, cp, scale, ptr<float>(p_.grad), s);
   post_launch(s);
   float* g = ptr<float>(p_.grad);

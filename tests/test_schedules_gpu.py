@@ -24,9 +24,10 @@ def _digest(env_extra, args):
     return re.search(r"digest (\w+)", r.stdout).group(1)
 
 
-@pytest.mark.timeout(900)  # four fresh interpreters (torch import + GPU init each)
+@pytest.mark.timeout(900)  # five fresh interpreters (torch import + GPU init each)
 def test_schedules_bitwise_equal(native):
     ref = _digest({"MNIST_AMD_CONCURRENT": "0"}, [])
     assert _digest({"MNIST_AMD_CONCURRENT": "1"}, []) == ref
+    assert _digest({"MNIST_AMD_CONCURRENT": "1", "MNIST_AMD_SPLIT_BWD": "1"}, []) == ref  # conv_bwd halves
     assert _digest({"MNIST_AMD_CONCURRENT": "1"}, ["--comm"]) == ref
     assert _digest({"MNIST_AMD_CONCURRENT": "1", "MNIST_AMD_MG_SCHED": "split"}, ["--comm"]) == ref
