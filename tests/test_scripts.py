@@ -63,3 +63,16 @@ def test_byo_model_example_two_ranks(tmp_path):
                 "--limit", "3000"], tmp_path)
     m = re.findall(r"^Epoch=0, top1=(\d\.\d+)$", out, re.M)
     assert len(m) == 1 and float(m[0]) > 0.5, out  # rank 0 prints
+
+
+def test_converter_notebook_runs(tmp_path, monkeypatch):
+    """mnist_to_netcdf.ipynb (reference entry point, survey CS4): its code cells convert and read back."""
+    import json
+    nb = json.load(open(os.path.join(ROOT, "mnist_to_netcdf.ipynb")))
+    monkeypatch.chdir(tmp_path)
+    g = {}
+    for cell in nb["cells"]:
+        if cell["cell_type"] == "code":
+            exec("".join(cell["source"]).replace("os.path.abspath('.')", repr(ROOT)), g)
+    assert g["x"].shape == (60000, 28, 28) and g["y"].shape == (60000,)
+    assert (tmp_path / "mnist_test_images.nc").exists()
