@@ -115,7 +115,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
 
   // optional per-phase wall-clock stamps (MNIST_AMD_STAMPS; thread 0, one vector store each)
   auto stamp = [&](int k) {
-    if (hb.stamps && tid == 0) hb.stamps[blockIdx.x * 16 + k] = wall_clock64();
+    if (hb.stamps && tid == 0 && blockIdx.x < 1024) hb.stamps[blockIdx.x * 16 + k] = wall_clock64();
   };
   stamp(0);
 

@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   const float* prm = cb.params;
   // optional wall-clock stamps (profiling): [0] start, [1] setup, 3 per image for images 0..3, [14] loop end
   auto stamp = [&](int k) {
-    if (cb.stamps && tid == 0) cb.stamps[(1024 + blockIdx.x) * 16 + k] = wall_clock64();
+    if (cb.stamps && tid == 0 && blockIdx.x < 1024) cb.stamps[(1024 + blockIdx.x) * 16 + k] = wall_clock64();
   };
   stamp(0);
 
@@ -383,7 +383,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   // optional wall-clock stamps (profiling): [0] start, [1] setup, 3 per image for images 0..3,
   // [14] loop end, [15] slab written
   auto stamp = [&](int k) {
-    if (cb.stamps && tid == 0) cb.stamps[(blockIdx.x + (MODE == 2 ? 512 : 0)) * 16 + k] = wall_clock64();
+    if (cb.stamps && tid == 0 && blockIdx.x < 512) cb.stamps[(blockIdx.x + (MODE == 2 ? 512 : 0)) * 16 + k] = wall_clock64();
   };
   stamp(0);
 

@@ -107,7 +107,8 @@ class NativeTrainer:
         P.dy1T, P.dy2T, P.dy3T = ptr(self.dy1T), ptr(self.dy2T), ptr(self.dy3T)
         P.p1, P.m1, P.p2, P.m2, P.dp2 = ptr(self.p1), ptr(self.m1), ptr(self.p2), ptr(self.m2), ptr(self.dp2)
         P.z1p = ptr(self.z1p)
-        # MNIST_AMD_STAMPS=1: per-block phase timestamps (wall clock, 100 MHz) of the head kernel
+        # MNIST_AMD_STAMPS=1: per-workgroup phase timestamps (wall clock, 100 MHz), 16 slots per workgroup:
+        # head blocks [0, 1024), conv_bwd [1024, 2048), conv_fwd [2048, 3072) (later workgroups skip)
         self.stamps = z(4096 * 16, dt=torch.int64) if os.environ.get("MNIST_AMD_STAMPS") else None
         P.stamps = ptr(self.stamps)
         self._ptrs = P
