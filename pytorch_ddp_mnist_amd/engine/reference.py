@@ -34,6 +34,7 @@ class EpochResult:
     last_b: int = 0
     seconds: float = 0.0
     steps: int = 0
+    next_indices: object = None  # the prefetch callback's result (next epoch's sampler order), if any
 
     @property
     def mean_loss(self) -> float:
@@ -68,7 +69,7 @@ class TorchCPUEngine:
         self.crit = F.nll_loss if model == "lenet5" else F.cross_entropy
         self.fault = FaultInjector(int(os.environ.get("RANK", "0")))
 
-    def train_epoch(self, indices: torch.Tensor, progress=None) -> EpochResult:
+    def train_epoch(self, indices: torch.Tensor, progress=None, prefetch=None) -> EpochResult:
         r = EpochResult()
         self.module.train()
         t0 = time.perf_counter()
@@ -96,6 +97,8 @@ class TorchCPUEngine:
             if progress:
                 progress(float(loss.item()))
         r.seconds = time.perf_counter() - t0
+        if prefetch is not None:
+            r.next_indices = prefetch()
         return r
 
     @torch.no_grad()

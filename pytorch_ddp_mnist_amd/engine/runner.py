@@ -76,7 +76,9 @@ class NativeEngine:
         else:
             self.tr.step(b, use_graph=self.use_graph)
 
-    def train_epoch(self, indices: torch.Tensor, progress=None) -> EpochResult:
+    def train_epoch(self, indices: torch.Tensor, progress=None, prefetch=None) -> EpochResult:
+        """``prefetch`` (optional) runs on the host while the epoch's steps execute on the GPU: the
+        next epoch's sampler order is ready when this one ends (no host gap between epochs)."""
         tr, B = self.tr, self.batch
         r = EpochResult()
         t0 = time.perf_counter()
@@ -87,6 +89,8 @@ class NativeEngine:
         with range_("train_full_batches"):
             for _ in range(nfull):
                 self._step(B)
+        if prefetch is not None:
+            r.next_indices = prefetch()
         m = tr.read_metrics()
         r.full_sum, r.n_full = m.loss_sum, nfull
         if last:
@@ -188,10 +192,16 @@ def run(cfg: TrainConfig, entry: str = "ddp_tutorial_cpu", show_banner: bool = F
         start = int(st["epoch"]) + 1
         if ctx.rank == 0:
             print(f"=> resumed from {cfg.resume} after epoch {st['epoch']}", flush=True)
+    idx = None
     for i in range(start, cfg.n_epochs):
-        idx = epoch_indices(len(ytr), ctx.world, ctx.rank, i, cfg.seed)
+        if idx is None:
+            idx = epoch_indices(len(ytr), ctx.world, ctx.rank, i, cfg.seed)
+        nxt = None
+        if i + 1 < cfg.n_epochs:
+            nxt = lambda e=i + 1: epoch_indices(len(ytr), ctx.world, ctx.rank, e, cfg.seed)  # noqa: E731
         with range_(f"epoch{i}.train"):
-            tr = engine.train_epoch(idx)
+            tr = engine.train_epoch(idx, prefetch=nxt)
+        idx = tr.next_indices
         if cfg.shard_eval and ctx.world > 1:
             tidx = torch.arange(ctx.rank, ntest, ctx.world)
         else:
