@@ -8,19 +8,26 @@ top-1 acc", config "LeNet-5 MNIST DDP 8xMI355X large-batch 8192/GPU bf16".  Weak
 Each timed step is a COMPLETE data-parallel training step through the native path: gather +
 normalise of the step's samples from the HBM-resident uint8 dataset, LeNet-5 forward and
 backward (hand-written CDNA4 MFMA kernels, bf16 inputs / fp32 accumulate / fp32 master
-weights), the gradient all-reduce (native RCCL communicator, two buckets, the conv one overlapped
-with the FC weight gradient) and the SGD-momentum update, replayed as one hipGraph per step.
+weights), at N > 1 the gradient all-reduce over the native RCCL communicator (the step plan --
+one coalesced all-reduce after the backward join, or the FC bucket sent beside conv_bwd -- is
+chosen at start-up by timing both on the real communicator and is reported in the JSON), and
+the SGD-momentum update, replayed as one hipGraph per step.
 The DistributedSampler(seed=42) order of every epoch the run touches is computed
 before timing and kept in HBM (the step counter crosses epoch boundaries on the device).
 Data: synthetic 28x28 uint8 images of the MNIST shape (no network), random init.
 
-Launch: ``python bench.py`` (1 GPU) or
-``python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
---master-port P bench.py --gpus N --steps K --warmup W``.  Rank 0 prints ONE JSON line.
+Launch:
+  ``python bench.py`` (1 GPU);
+  ``python bench.py --gpus N`` spawns N rank processes itself (one per GPU, torchrun-style env,
+  before this parent touches a GPU) and relays rank 0's JSON line;
+  ``python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
+  --master-port P bench.py --gpus N --steps K --warmup W`` runs the ranks under torchrun.
+Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
 import argparse
+import importlib.util
 import json
 import os
 import sys
@@ -29,8 +36,10 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+METRIC = "images/sec (whole node) MNIST ConvNet DDP at 1/2/4/8 MI355X; top-1 acc"
 
-def parse():
+
+def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
@@ -41,19 +50,63 @@ def parse():
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--momentum", type=float, default=0.9)
     ap.add_argument("--comm", default="rccl", choices=["rccl", "torch"])
+    ap.add_argument("--plan", default="auto", choices=["auto", "join", "split"],
+                    help="multi-GPU step plan (auto = time the candidates at start-up and keep the fastest)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--comm-world1", action="store_true",
-                    help="attach the RCCL communicator at world size 1 (runs the multi-GPU step schedule on one GPU)")
+                    help="attach a world-1 RCCL communicator (runs the multi-GPU step schedule on one GPU)")
     ap.add_argument("--eval", action="store_true", default=True)
     ap.add_argument("--no-eval", dest="eval", action="store_false")
     ap.add_argument("--json-out", default=None)
-    return ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="check the launch wiring only: every rank validates its env, rank 0 prints a JSON line, no GPU")
+    return ap.parse_args(argv)
 
 
-def main() -> int:
-    a = parse()
-    import numpy as np
+def _launcher():
+    """parallel/launch.py loaded by path: the parent must not import torch / touch a GPU."""
+    spec = importlib.util.spec_from_file_location("_mnist_launch", os.path.join(ROOT, "pytorch_ddp_mnist_amd",
+                                                                                 "parallel", "launch.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def spawn_ranks(a) -> int:
+    """``--gpus N`` without a launcher: start N rank processes and relay rank 0's JSON line."""
+    L = _launcher()
+    cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    rc, lines = L.launch_relay(cmd, a.gpus, style="torch", relay_rank=0)
+    if rc == 0 and not any(l.lstrip().startswith("{") for l in lines):
+        print("[bench] rank 0 printed no result line", file=sys.stderr)
+        return 1
+    if rc != 0:
+        print(f"[bench] a rank failed with exit code {rc}", file=sys.stderr)
+    return rc
+
+
+def dry_run(a) -> int:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    lrank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus or not (0 <= rank < world) or lrank != rank or (world > 1 and not os.environ.get("MASTER_PORT")):
+        print(f"[bench] bad rank env: RANK={rank} WORLD_SIZE={world} LOCAL_RANK={lrank}", file=sys.stderr)
+        return 3
+    if os.environ.get("MNIST_AMD_DRYRUN_FAIL_RANK") == str(rank):
+        return 7
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "n_gpus": world, "dry_run": True,
+                          "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}), flush=True)
+    return 0
+
+
+def main(argv=None) -> int:
+    a = parse(argv)
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(a)
+    if a.dry_run:
+        return dry_run(a)
+
     import torch
 
     from pytorch_ddp_mnist_amd.data.sampler import epoch_indices, num_samples
@@ -61,6 +114,7 @@ def main() -> int:
     from pytorch_ddp_mnist_amd.engine.native import NativeTrainer
     from pytorch_ddp_mnist_amd.models import build_model
     from pytorch_ddp_mnist_amd.parallel.comm import init_distributed
+    from pytorch_ddp_mnist_amd.parallel.ddp import model_phases, plan_buckets
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     ctx = init_distributed(None, parallel=world_env > 1, device="cuda", comm=a.comm)
@@ -89,22 +143,29 @@ def main() -> int:
     torch.manual_seed(0)
     tr = NativeTrainer(a.model, a.dtype, a.batch, images, labels, device=dev, lr=a.lr, momentum=a.momentum,
                        dropout=0.0, init=build_model(a.model), max_indices=idx_all.numel())
+    tr.set_buckets(plan_buckets(model_phases(a.model)))
+    tr.set_epoch_indices(idx_all)
+    comm, rccl_version, tune = None, None, None
     if W > 1 or a.comm_world1:
         if a.comm == "rccl":
+            from pytorch_ddp_mnist_amd.ops.native import load_c
+            C = load_c()
             comm = ctx.rccl
             if comm is None:  # --comm-world1: a world-1 RCCL communicator, no rendezvous needed
-                from pytorch_ddp_mnist_amd.ops.native import load_c
-                C = load_c()
                 comm = C.RcclComm(bytes(C.RcclComm.make_unique_id()), 0, 1, ctx.local_rank)
-            tr.attach_comm(comm, W, overlap=not a.no_overlap)
+            rccl_version = C.rccl_version()
+            tr.attach_comm(comm, W)
             tr.broadcast_params(0)
+            if a.plan == "auto":
+                tune = tr.autotune_plan(reduce_max=ctx.all_reduce_max)
+            else:
+                tr.set_plan(a.plan)
         else:
             import torch.distributed as dist
             dist.broadcast(tr.params, 0)
             tr.load_flat(tr.params.clone())
 
     use_graph = not a.no_graph and a.comm == "rccl"
-    tr.set_epoch_indices(idx_all)
 
     def one_step():
         if a.comm == "rccl" or W == 1:
@@ -131,6 +192,7 @@ def main() -> int:
     t1 = time.perf_counter()
     elapsed = ctx.all_reduce_max(t1 - t0)
     train = tr.read_metrics()
+    tr.check_comm()
 
     top1 = None
     if a.eval:
@@ -138,13 +200,22 @@ def main() -> int:
                          torch.arange(10000, dtype=torch.int32))
         top1 = ev.accuracy
 
+    n_gpus = comm.world if comm is not None else W
+    info = tr.plan_info()
+    if comm is not None:
+        colls = " + ".join(f"{c['bytes'] // 1024} KiB" for c in info["collectives"])
+        comm_desc = f"native RCCL {rccl_version}, plan={info['plan']}: all-reduce {colls} per step"
+    elif a.comm == "torch" and W > 1:
+        comm_desc = "c10d nccl (RCCL) all_reduce of the whole grad slab"
+    else:
+        comm_desc = "none (single process, no gradient exchange)"
     ms = elapsed / a.steps * 1e3
-    value = W * a.batch * a.steps / elapsed
+    value = n_gpus * a.batch * a.steps / elapsed
     out = {
-        "metric": "images/sec (whole node) MNIST ConvNet DDP at 1/2/4/8 MI355X; top-1 acc",
+        "metric": METRIC,
         "value": round(value, 1),
         "unit": "images/s",
-        "n_gpus": W,
+        "n_gpus": n_gpus,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(ms, 4),
@@ -155,13 +226,15 @@ def main() -> int:
         "data": "synthetic (MNIST-shaped 28x28 uint8, class-template + noise; random-init weights)",
         "config": {
             "model": "LeNet-5" if a.model == "lenet5" else "MLP-784-128-128-10",
-            "global_batch": W * a.batch,
+            "global_batch": n_gpus * a.batch,
             "per_gpu_batch": a.batch,
             "seq_len": None,
             "image_shape": [1, 28, 28],
-            "parallelism": f"dp{W}",
+            "parallelism": f"dp{n_gpus}",
             "optimizer": f"SGD(lr={a.lr}, momentum={a.momentum})",
-            "comm": "native RCCL, 2 buckets (conv bucket overlapped with FC wgrad)" if a.comm == "rccl" else "c10d nccl",
+            "comm": comm_desc,
+            "plan": info,
+            "plan_autotune": tune,
             "hipgraph": use_graph,
         },
         "top1": None if top1 is None else round(top1, 4),

@@ -1,7 +1,12 @@
 // pybind11 surface of the native HIP extension ``pytorch_ddp_mnist_amd._C``.
 // Device buffers are owned by torch (HBM via its caching allocator) and passed as raw
 // addresses; streams are passed as the integer handles of torch.cuda.Stream.cuda_stream.
+#include <execinfo.h>
 #include <pybind11/pybind11.h>
+#include <signal.h>
+#include <unistd.h>
+
+#include <cstdlib>
 #include <stdexcept>
 #include <pybind11/stl.h>
 
@@ -12,13 +17,29 @@
 
 namespace py = pybind11;
 
+namespace {
+// MNIST_AMD_SEGV_TRACE=1: print the native backtrace of a host segfault (faulthandler shows only
+// Python frames), then re-raise with the default action.
+void segv_trace(int sig) {
+  void* frames[64];
+  const int n = backtrace(frames, 64);
+  const char msg[] = "\n[mnist_amd] native backtrace:\n";
+  (void)!write(2, msg, sizeof(msg) - 1);
+  backtrace_symbols_fd(frames, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+}  // namespace
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X (gfx950) native kernels, step runtime and RCCL communicator";
+  if (const char* e = std::getenv("MNIST_AMD_SEGV_TRACE"); e && *e == '1') signal(SIGSEGV, segv_trace);
 
   m.def("model_nparam", [](int model) { return model_nparam(static_cast<ModelKind>(model)); });
   m.def("model_conv_params", [](int model) { return model_conv_params(static_cast<ModelKind>(model)); });
   m.def("model_pack_size", [](int model) { return model_pack_size(static_cast<ModelKind>(model)); });
-  m.def("conv_bwd_blocks", &lenet_conv_bwd_blocks);
+  m.def("conv_bwd_blocks", &lenet_conv_bwd_blocks, py::arg("B"), py::arg("target_blocks") = 0);
+  m.def("conv_bwd_max_blocks", &lenet_conv_bwd_max_blocks, py::arg("B"), py::arg("target_blocks") = 0);
   m.attr("L1_KSPLIT") = L1_KSPLIT;
   m.attr("L1_SPLIT_MAX_B") = L1_SPLIT_MAX_B;
   m.def("device_count", [] {
@@ -82,9 +103,10 @@ PYBIND11_MODULE(_C, m) {
            })
       .def("async_error", &RcclComm::async_error)
       .def("wait_stream",
-           [](RcclComm& c, uintptr_t s, double timeout) { c.wait_stream(reinterpret_cast<hipStream_t>(s), timeout); },
+           [](RcclComm& c, uintptr_t s, double timeout) { return c.wait_stream(reinterpret_cast<hipStream_t>(s), timeout); },
            py::call_guard<py::gil_scoped_release>())
       .def("abort", &RcclComm::abort)
+      .def_property_readonly("aborted", &RcclComm::aborted)
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("world", &RcclComm::world);
 
@@ -97,7 +119,15 @@ PYBIND11_MODULE(_C, m) {
       .def("set_dropout", &Trainer::set_dropout)
       .def("set_buckets", &Trainer::set_buckets)
       .def("buckets", &Trainer::buckets)
-      .def("set_overlap", &Trainer::set_overlap)
+      .def("set_plan", &Trainer::set_plan)
+      .def_property_readonly("plan", &Trainer::plan)
+      .def("set_bwd_blocks", &Trainer::set_bwd_blocks)
+      .def_property_readonly("bwd_blocks", &Trainer::bwd_blocks)
+      .def_property_readonly("bwd_grid", &Trainer::bwd_grid)
+      .def("issued_collectives", &Trainer::issued_collectives)
+      .def_property_readonly("has_comm", &Trainer::has_comm)
+      .def_property_readonly("world", &Trainer::world)
+      .def("spin", &Trainer::spin)
       .def("pack", &Trainer::pack)
       .def("train_step", &Trainer::train_step)
       .def("forward_backward", &Trainer::forward_backward)

@@ -31,15 +31,13 @@
 #include <thread>
 #include <vector>
 
+#include "formats.h"
+
 namespace py = pybind11;
 
 namespace mnist_io {
 
-// ------------------------------------------------------------------ big-endian helpers
-static inline uint32_t be32(const uint8_t* p) {
-  return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | uint32_t(p[3]);
-}
-static inline uint64_t be64(const uint8_t* p) { return (uint64_t(be32(p)) << 32) | be32(p + 4); }
+// ------------------------------------------------------------------ big-endian writers
 static inline void put32(std::vector<uint8_t>& o, uint32_t v) {
   for (int s = 24; s >= 0; s -= 8) o.push_back(uint8_t(v >> s));
 }
@@ -110,26 +108,25 @@ py::array_t<uint8_t> idx_read(const std::string& path, int64_t limit) {
   int fd = ::open(path.c_str(), O_RDONLY);
   if (fd < 0) throw std::runtime_error("cannot open " + path + ": " + std::strerror(errno));
   Fd guard(fd);
-  uint8_t hdr[4];
-  pread_all(fd, hdr, 4, 0);
-  if (hdr[0] != 0 || hdr[1] != 0) throw std::runtime_error(path + ": bad idx magic");
-  if (hdr[2] != 0x08) throw std::runtime_error(path + ": only unsigned-byte idx files are supported");
-  int ndim = hdr[3];
-  if (ndim < 1 || ndim > 4) throw std::runtime_error(path + ": bad idx rank");
-  std::vector<uint8_t> dimb(4 * size_t(ndim));
-  pread_all(fd, dimb.data(), dimb.size(), 4);
-  std::vector<ssize_t> shape(ndim);
-  size_t per = 1;
-  for (int i = 0; i < ndim; ++i) {
-    shape[i] = ssize_t(be32(&dimb[4 * i]));
-    if (i) per *= size_t(shape[i]);
+  struct stat st;
+  if (::fstat(fd, &st) != 0) throw std::runtime_error("cannot stat " + path);
+  const uint64_t fsize = uint64_t(st.st_size);
+  uint8_t hdr[20] = {0};
+  const size_t hn = size_t(std::min<uint64_t>(fsize, sizeof(hdr)));
+  pread_all(fd, hdr, hn, 0);
+  IdxHeader h;
+  try {
+    h = parse_idx_header(hdr, hn, fsize);
+  } catch (const std::exception& e) {
+    throw std::runtime_error(path + ": " + e.what());
   }
+  std::vector<ssize_t> shape(h.shape.begin(), h.shape.end());
   if (limit >= 0 && limit < shape[0]) shape[0] = limit;
   py::array_t<uint8_t> out(shape);
-  size_t bytes = per * size_t(shape[0]);
+  size_t bytes = size_t(h.row_bytes * uint64_t(shape[0]));  // <= file size (checked by the parser)
   {
     py::gil_scoped_release nogil;
-    pread_parallel(fd, out.mutable_data(), bytes, 4 + 4 * uint64_t(ndim), 4);
+    pread_parallel(fd, out.mutable_data(), bytes, h.data_offset, 4);
   }
   return out;
 }
@@ -145,119 +142,55 @@ void idx_write(const std::string& path, py::array_t<uint8_t, py::array::c_style 
   write_all(fd, a.data(), size_t(a.nbytes()));
 }
 
-// ------------------------------------------------------------------ netCDF classic
-enum NcType : int32_t { NC_BYTE = 1, NC_CHAR = 2, NC_SHORT = 3, NC_INT = 4, NC_FLOAT = 5, NC_DOUBLE = 6,
-                        NC_UBYTE = 7, NC_USHORT = 8, NC_UINT = 9, NC_INT64 = 10, NC_UINT64 = 11 };
-static const uint32_t TAG_DIM = 0x0A, TAG_VAR = 0x0B, TAG_ATT = 0x0C;
-
-static size_t type_size(int32_t t) {
-  switch (t) {
-    case NC_BYTE: case NC_CHAR: case NC_UBYTE: return 1;
-    case NC_SHORT: case NC_USHORT: return 2;
-    case NC_INT: case NC_FLOAT: case NC_UINT: return 4;
-    case NC_DOUBLE: case NC_INT64: case NC_UINT64: return 8;
-  }
-  throw std::runtime_error("unknown netCDF type " + std::to_string(t));
-}
-
-struct NcDim { std::string name; uint64_t len; };
-struct NcAtt { std::string name; int32_t type; uint64_t nelems; std::vector<uint8_t> raw; };
-struct NcVar {
-  std::string name; std::vector<uint64_t> dimids; std::vector<NcAtt> atts;
-  int32_t type; uint64_t vsize; uint64_t begin;
-};
-
-class Cursor {
- public:
-  Cursor(const std::vector<uint8_t>& b, int ver) : b_(b), ver_(ver) {}
-  uint32_t u32() { need(4); uint32_t v = be32(&b_[p_]); p_ += 4; return v; }
-  uint64_t u64() { need(8); uint64_t v = be64(&b_[p_]); p_ += 8; return v; }
-  uint64_t nonneg() { return ver_ == 5 ? u64() : u32(); }
-  uint64_t offset() { return ver_ == 1 ? u32() : u64(); }
-  std::string name() {
-    uint64_t n = nonneg();
-    need(n);
-    std::string s(reinterpret_cast<const char*>(&b_[p_]), size_t(n));
-    p_ += (n + 3) & ~uint64_t(3);
-    return s;
-  }
-  std::vector<uint8_t> bytes(uint64_t n) {
-    need(n);
-    std::vector<uint8_t> v(b_.begin() + p_, b_.begin() + p_ + n);
-    p_ += (n + 3) & ~uint64_t(3);
-    return v;
-  }
-  size_t pos() const { return p_; }
-  bool has(size_t n) const { return p_ + n <= b_.size(); }
-
- private:
-  void need(uint64_t n) const {
-    if (p_ + n > b_.size()) throw std::out_of_range("header truncated");
-  }
-  const std::vector<uint8_t>& b_;
-  int ver_;
-  size_t p_ = 4;
-};
-
-static std::vector<NcAtt> read_atts(Cursor& c) {
-  std::vector<NcAtt> out;
-  uint32_t tag = c.u32();
-  uint64_t n = c.nonneg();
-  if (tag == 0 && n == 0) return out;
-  if (tag != TAG_ATT) throw std::runtime_error("bad attribute list tag");
-  for (uint64_t i = 0; i < n; ++i) {
-    NcAtt a;
-    a.name = c.name();
-    a.type = int32_t(c.u32());
-    a.nelems = c.nonneg();
-    a.raw = c.bytes(a.nelems * type_size(a.type));
-    out.push_back(std::move(a));
-  }
-  return out;
-}
-
+// ------------------------------------------------------------------ netCDF classic (parser: formats.h)
 class NcFile {
  public:
   explicit NcFile(const std::string& path) : path_(path) {
     fd_ = ::open(path.c_str(), O_RDONLY);
     if (fd_ < 0) throw std::runtime_error("cannot open " + path + ": " + std::strerror(errno));
     struct stat st;
-    ::fstat(fd_, &st);
+    if (::fstat(fd_, &st) != 0) { ::close(fd_); throw std::runtime_error("cannot stat " + path); }
     file_size_ = uint64_t(st.st_size);
     // Headers of MNIST-sized files are a few hundred bytes; grow the window if needed.
-    for (size_t win = 4096;; win *= 4) {
-      size_t n = size_t(std::min<uint64_t>(win, file_size_));
-      std::vector<uint8_t> buf(n);
-      pread_all(fd_, buf.data(), n, 0);
-      try {
-        parse(buf);
-        break;
-      } catch (const std::out_of_range&) {
-        if (n == file_size_) throw std::runtime_error(path + ": truncated netCDF header");
+    try {
+      for (uint64_t win = 4096;; win *= 4) {
+        const size_t n = size_t(std::min<uint64_t>(win, file_size_));
+        std::vector<uint8_t> buf(n);
+        pread_all(fd_, buf.data(), n, 0);
+        try {
+          h_.parse(buf.data(), n, file_size_);
+          break;
+        } catch (const NcTruncated&) {
+          if (n == file_size_) throw std::runtime_error("truncated netCDF header");
+        }
       }
+    } catch (const std::exception& e) {
+      ::close(fd_);
+      fd_ = -1;
+      throw std::runtime_error(path + ": " + e.what());
     }
   }
   ~NcFile() { if (fd_ >= 0) ::close(fd_); }
 
-  int version() const { return ver_; }
+  int version() const { return h_.ver; }
   const std::string& path() const { return path_; }
   std::vector<std::pair<std::string, uint64_t>> dims() const {
     std::vector<std::pair<std::string, uint64_t>> o;
-    for (auto& d : dims_) o.emplace_back(d.name, d.len);
+    for (auto& d : h_.dims) o.emplace_back(d.name, d.len);
     return o;
   }
   std::vector<std::string> variables() const {
     std::vector<std::string> o;
-    for (auto& v : vars_) o.push_back(v.name);
+    for (auto& v : h_.vars) o.push_back(v.name);
     return o;
   }
   const NcVar& var(const std::string& n) const {
-    for (auto& v : vars_) if (v.name == n) return v;
+    for (auto& v : h_.vars) if (v.name == n) return v;
     throw std::runtime_error(path_ + ": no variable " + n);
   }
   std::vector<uint64_t> shape(const std::string& n) const {
     std::vector<uint64_t> s;
-    for (auto id : var(n).dimids) s.push_back(dims_.at(size_t(id)).len);
+    for (auto id : var(n).dimids) s.push_back(h_.dims.at(size_t(id)).len);
     return s;
   }
   int32_t vtype(const std::string& n) const { return var(n).type; }
@@ -268,13 +201,13 @@ class NcFile {
     d["type"] = v.type; d["vsize"] = v.vsize; d["begin"] = v.begin;
     d["shape"] = shape(n);
     std::vector<std::string> dn;
-    for (auto id : v.dimids) dn.push_back(dims_.at(size_t(id)).name);
+    for (auto id : v.dimids) dn.push_back(h_.dims.at(size_t(id)).name);
     d["dims"] = dn;
     return d;
   }
   py::dict global_attributes() const {
     py::dict d;
-    for (auto& a : gatts_) d[py::str(a.name)] = py::bytes(reinterpret_cast<const char*>(a.raw.data()), a.raw.size());
+    for (auto& a : h_.gatts) d[py::str(a.name)] = py::bytes(reinterpret_cast<const char*>(a.raw.data()), a.raw.size());
     return d;
   }
 
@@ -285,9 +218,8 @@ class NcFile {
     if (shp.empty()) throw std::runtime_error("scalar variable");
     uint64_t nrows = shp[0];
     uint64_t cnt = count < 0 ? nrows - std::min(start, nrows) : uint64_t(count);
-    if (start + cnt > nrows) throw std::out_of_range("read_rows: rows out of range");
-    uint64_t row_bytes = type_size(v.type);
-    for (size_t i = 1; i < shp.size(); ++i) row_bytes *= shp[i];
+    if (start > nrows || cnt > nrows - start) throw std::out_of_range("read_rows: rows out of range");
+    const uint64_t row_bytes = row_size(v, shp);
     std::vector<ssize_t> oshape = {ssize_t(cnt)};
     for (size_t i = 1; i < shp.size(); ++i) oshape.push_back(ssize_t(shp[i]));
     py::array out(dtype_of(v.type), oshape);
@@ -306,9 +238,9 @@ class NcFile {
                           uint64_t dst_bytes, int threads) const {
     const NcVar& v = var(n);
     auto shp = shape(n);
-    uint64_t row_bytes = type_size(v.type);
-    for (size_t i = 1; i < shp.size(); ++i) row_bytes *= shp[i];
-    if (start + count > shp[0]) throw std::out_of_range("read_rows_into: rows out of range");
+    if (shp.empty()) throw std::runtime_error("scalar variable");
+    const uint64_t row_bytes = row_size(v, shp);
+    if (start > shp[0] || count > shp[0] - start) throw std::out_of_range("read_rows_into: rows out of range");
     uint64_t bytes = count * row_bytes;
     if (bytes > dst_bytes) throw std::runtime_error("read_rows_into: destination too small");
     py::gil_scoped_release nogil;
@@ -337,54 +269,20 @@ class NcFile {
     }
     throw std::runtime_error("unknown type");
   }
+  // bytes of one row (slice along dim 0); the whole variable was checked to fit the file at parse time
+  static uint64_t row_size(const NcVar& v, const std::vector<uint64_t>& shp) {
+    uint64_t r = type_size(v.type);
+    for (size_t i = 1; i < shp.size(); ++i) r = mul_checked(r, shp[i], "netCDF row");
+    return r;
+  }
   static void fix_endian(uint8_t* p, size_t bytes, size_t w) {
     if (w == 1) return;
     for (size_t i = 0; i + w <= bytes; i += w) std::reverse(p + i, p + i + w);
   }
-  void parse(const std::vector<uint8_t>& b) {
-    if (b.size() < 4 || b[0] != 'C' || b[1] != 'D' || b[2] != 'F')
-      throw std::runtime_error(path_ + ": not a classic netCDF file");
-    ver_ = b[3];
-    if (ver_ != 1 && ver_ != 2 && ver_ != 5) throw std::runtime_error(path_ + ": unsupported CDF version");
-    Cursor c(b, ver_);
-    dims_.clear(); gatts_.clear(); vars_.clear();
-    numrecs_ = c.nonneg();
-    uint32_t tag = c.u32();
-    uint64_t n = c.nonneg();
-    if (!(tag == 0 && n == 0)) {
-      if (tag != TAG_DIM) throw std::runtime_error("bad dim list tag");
-      for (uint64_t i = 0; i < n; ++i) {
-        NcDim d; d.name = c.name(); d.len = c.nonneg();
-        dims_.push_back(d);
-      }
-    }
-    gatts_ = read_atts(c);
-    tag = c.u32();
-    n = c.nonneg();
-    if (!(tag == 0 && n == 0)) {
-      if (tag != TAG_VAR) throw std::runtime_error("bad var list tag");
-      for (uint64_t i = 0; i < n; ++i) {
-        NcVar v;
-        v.name = c.name();
-        uint64_t nd = c.nonneg();
-        for (uint64_t k = 0; k < nd; ++k) v.dimids.push_back(c.nonneg());
-        v.atts = read_atts(c);
-        v.type = int32_t(c.u32());
-        v.vsize = c.nonneg();
-        v.begin = c.offset();
-        for (auto id : v.dimids)
-          if (id >= dims_.size()) throw std::runtime_error("dimid out of range");
-        vars_.push_back(std::move(v));
-      }
-    }
-  }
   std::string path_;
   int fd_ = -1;
-  int ver_ = 0;
-  uint64_t file_size_ = 0, numrecs_ = 0;
-  std::vector<NcDim> dims_;
-  std::vector<NcAtt> gatts_;
-  std::vector<NcVar> vars_;
+  uint64_t file_size_ = 0;
+  NcHeader h_;
 };
 
 // CDF-5 writer for non-record variables.  Semantics of the notebook's to_nc()

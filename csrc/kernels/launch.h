@@ -68,9 +68,12 @@ int launch_head_wgrad(ModelKind m, DType t, const HeadBuffers& hb, int B, int sp
 void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetConvBuffers& cb,
                            hipStream_t s);
 // mode 0: full backward; 1: conv2 dgrad + conv1 wgrad half; 2: conv2 wgrad half (lenet.hip MODE)
+// target_blocks: workgroup count to aim for (0 = default, one full round of 2 blocks per CU); each
+// block walks ceil(B / target) images, so a smaller target leaves whole CUs free (for RCCL kernels).
 void launch_lenet_conv_bwd(DType t, const BatchRef& br, const LenetConvBuffers& cb, int* nslab_out,
-                           hipStream_t s, int mode = 0);
-int lenet_conv_bwd_blocks(int B);
+                           hipStream_t s, int mode = 0, int target_blocks = 0);
+int lenet_conv_bwd_blocks(int B, int target_blocks = 0);
+int lenet_conv_bwd_max_blocks(int B, int target_blocks = 0);  // slab rows needed for any batch <= B
 
 // grad[p] = scale * sum_s slab[s][p]  for p in [p0, p1)
 void launch_reduce(const float* slab, int slab_ld, int nslab, int p0, int p1, float scale, float* grad,
@@ -80,7 +83,12 @@ void launch_reduce(const float* slab, int slab_ld, int nslab, int p0, int p1, fl
 void launch_sgd_pack(ModelKind m, DType t, float* params, const float* grad, float* mom, void* pack,
                      int nparam, float lr, float momentum, float gscale, int32_t* step_ptr,
                      hipStream_t s);
+// Same, over the parameter range [p0, p1) only (per-bucket updates of the split multi-GPU plan).
+void launch_sgd_pack_range(ModelKind m, DType t, float* params, const float* grad, float* mom, void* pack, int p0,
+                           int p1, float lr, float momentum, float gscale, int32_t* step_ptr, hipStream_t s);
 void launch_pack(ModelKind m, DType t, const float* params, void* pack, int nparam, hipStream_t s);
+// Bounded device busy-wait (watchdog tests).
+void launch_spin(double seconds, hipStream_t s);
 // Fused gradient reduce + SGD + pack + step bump (no all-reduce between them: single-GPU runs).
 void launch_reduce_sgd(ModelKind m, DType t, const float* slab_a, int lda, int na, const float* slab_b, int ldb,
                        int nb, int split, int p0, int n, float scale, float* params, float* grad, float* mom,

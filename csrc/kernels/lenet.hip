@@ -685,17 +685,28 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
 }  // namespace
 
 static int fwd_ipb(int B) { return std::max(1, (B + 1023) / 1024); }
-static int bwd_ipb(int B) {
-  static const int div = [] {
-    const char* e = std::getenv("MNIST_AMD_BWD_BLOCKS");  // tuning knob: target block count
+static int default_bwd_target() {
+  static const int def = [] {
+    const char* e = std::getenv("MNIST_AMD_BWD_BLOCKS");  // tuning knob: default target block count
     return e ? std::max(1, std::atoi(e)) : 512;  // 512 = one full round of 2 blocks/CU; 1024/768 measured slower
   }();
+  return def;
+}
+
+static int bwd_ipb(int B, int target) {
+  const int div = target > 0 ? target : default_bwd_target();
   return std::max(1, (B + div - 1) / div);
 }
 
-int lenet_conv_bwd_blocks(int B) {
-  const int ipb = bwd_ipb(B);
+int lenet_conv_bwd_blocks(int B, int target) {
+  const int ipb = bwd_ipb(B, target);
   return (B + ipb - 1) / ipb;
+}
+
+// Upper bound of lenet_conv_bwd_blocks(b, target) over every b <= B (partial last batches included):
+// ceil(b / ceil(b / t)) <= min(b, t).  Size the conv slab with this, not with the full-batch grid.
+int lenet_conv_bwd_max_blocks(int B, int target) {
+  return std::max(1, std::min(B, target > 0 ? target : default_bwd_target()));
 }
 
 void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetConvBuffers& cb, hipStream_t s) {
@@ -711,8 +722,8 @@ void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetC
 }
 
 void launch_lenet_conv_bwd(DType t, const BatchRef& br, const LenetConvBuffers& cb, int* nslab_out, hipStream_t s,
-                           int mode) {
-  const int ipb = bwd_ipb(br.B), grid = (br.B + ipb - 1) / ipb;
+                           int mode, int target_blocks) {
+  const int ipb = bwd_ipb(br.B, target_blocks), grid = (br.B + ipb - 1) / ipb;
   if (nslab_out) *nslab_out = grid;
   if (br.B <= 0) return;
   if (t == DType::F32) {

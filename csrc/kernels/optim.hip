@@ -72,10 +72,10 @@ __global__ __launch_bounds__(NW * 64) void reduce_slabs_kernel(const float* __re
 
 template <class Model, typename T>
 __global__ __launch_bounds__(256) void sgd_pack_kernel(float* __restrict__ params, const float* __restrict__ grad,
-                                                       float* __restrict__ mom, T* __restrict__ pack, int n,
+                                                       float* __restrict__ mom, T* __restrict__ pack, int p0, int n,
                                                        float lr, float mu, float gscale, int32_t* step_ptr,
                                                        int update) {
-  for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
+  for (int p = p0 + blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
     float v = params[p];
     if (update) {
       float g = grad[p] * gscale;
@@ -149,11 +149,18 @@ void reduce_sgd_t(const float* sa, int lda, int na, const float* sb, int ldb, in
 }
 
 template <class Model, typename T>
-void sgd_launch(float* params, const float* grad, float* mom, void* pack, int n, float lr, float mu, float gscale,
-                int32_t* step_ptr, int update, hipStream_t s) {
-  const int grid = std::min(1024, (n + 255) / 256);
+void sgd_launch(float* params, const float* grad, float* mom, void* pack, int p0, int n, float lr, float mu,
+                float gscale, int32_t* step_ptr, int update, hipStream_t s) {
+  const int grid = std::max(1, std::min(1024, (n - p0 + 255) / 256));
   hipLaunchKernelGGL((sgd_pack_kernel<Model, T>), dim3(grid), dim3(256), 0, s, params, grad, mom,
-                     reinterpret_cast<T*>(pack), n, lr, mu, gscale, step_ptr, update);
+                     reinterpret_cast<T*>(pack), p0, n, lr, mu, gscale, step_ptr, update);
+}
+
+// Bounded busy wait of `ticks` periods of the 100 MHz wall clock (one lane; tests of the collective
+// watchdog use it to hold a stream busy for a known time).  Every wave exits once the deadline passes.
+__global__ void spin_kernel(unsigned long long ticks) {
+  const unsigned long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
 }
 
 template <typename T>
@@ -175,26 +182,37 @@ void launch_reduce(const float* slab, int slab_ld, int nslab, int p0, int p1, fl
                      grad);
 }
 
-void launch_sgd_pack(ModelKind m, DType t, float* params, const float* grad, float* mom, void* pack, int nparam,
-                     float lr, float momentum, float gscale, int32_t* step_ptr, hipStream_t s) {
+void launch_sgd_pack_range(ModelKind m, DType t, float* params, const float* grad, float* mom, void* pack, int p0,
+                           int p1, float lr, float momentum, float gscale, int32_t* step_ptr, hipStream_t s) {
+  if (p1 <= p0) return;
   float* mb = momentum != 0.f ? mom : nullptr;
   if (m == ModelKind::MLP) {
-    if (t == DType::F32) sgd_launch<MlpModel, float>(params, grad, mb, pack, nparam, lr, momentum, gscale, step_ptr, 1, s);
-    else sgd_launch<MlpModel, bf16>(params, grad, mb, pack, nparam, lr, momentum, gscale, step_ptr, 1, s);
+    if (t == DType::F32) sgd_launch<MlpModel, float>(params, grad, mb, pack, p0, p1, lr, momentum, gscale, step_ptr, 1, s);
+    else sgd_launch<MlpModel, bf16>(params, grad, mb, pack, p0, p1, lr, momentum, gscale, step_ptr, 1, s);
   } else {
-    if (t == DType::F32) sgd_launch<LenetModel, float>(params, grad, mb, pack, nparam, lr, momentum, gscale, step_ptr, 1, s);
-    else sgd_launch<LenetModel, bf16>(params, grad, mb, pack, nparam, lr, momentum, gscale, step_ptr, 1, s);
+    if (t == DType::F32) sgd_launch<LenetModel, float>(params, grad, mb, pack, p0, p1, lr, momentum, gscale, step_ptr, 1, s);
+    else sgd_launch<LenetModel, bf16>(params, grad, mb, pack, p0, p1, lr, momentum, gscale, step_ptr, 1, s);
   }
+}
+
+void launch_sgd_pack(ModelKind m, DType t, float* params, const float* grad, float* mom, void* pack, int nparam,
+                     float lr, float momentum, float gscale, int32_t* step_ptr, hipStream_t s) {
+  launch_sgd_pack_range(m, t, params, grad, mom, pack, 0, nparam, lr, momentum, gscale, step_ptr, s);
+}
+
+void launch_spin(double seconds, hipStream_t s) {
+  const unsigned long long ticks = (unsigned long long)(seconds * 1e8);  // wall_clock64 runs at 100 MHz
+  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, s, ticks);
 }
 
 void launch_pack(ModelKind m, DType t, const float* params, void* pack, int nparam, hipStream_t s) {
   float* p = const_cast<float*>(params);
   if (m == ModelKind::MLP) {
-    if (t == DType::F32) sgd_launch<MlpModel, float>(p, nullptr, nullptr, pack, nparam, 0.f, 0.f, 0.f, nullptr, 0, s);
-    else sgd_launch<MlpModel, bf16>(p, nullptr, nullptr, pack, nparam, 0.f, 0.f, 0.f, nullptr, 0, s);
+    if (t == DType::F32) sgd_launch<MlpModel, float>(p, nullptr, nullptr, pack, 0, nparam, 0.f, 0.f, 0.f, nullptr, 0, s);
+    else sgd_launch<MlpModel, bf16>(p, nullptr, nullptr, pack, 0, nparam, 0.f, 0.f, 0.f, nullptr, 0, s);
   } else {
-    if (t == DType::F32) sgd_launch<LenetModel, float>(p, nullptr, nullptr, pack, nparam, 0.f, 0.f, 0.f, nullptr, 0, s);
-    else sgd_launch<LenetModel, bf16>(p, nullptr, nullptr, pack, nparam, 0.f, 0.f, 0.f, nullptr, 0, s);
+    if (t == DType::F32) sgd_launch<LenetModel, float>(p, nullptr, nullptr, pack, 0, nparam, 0.f, 0.f, 0.f, nullptr, 0, s);
+    else sgd_launch<LenetModel, bf16>(p, nullptr, nullptr, pack, 0, nparam, 0.f, 0.f, 0.f, nullptr, 0, s);
   }
 }
 

@@ -25,11 +25,13 @@ class RcclComm {
   void all_reduce_max_f64(double* buf, size_t count, hipStream_t s);
   // Returns "" if healthy, else the error string.  Non-blocking.
   std::string async_error();
-  // Wait for `s` with async-error polling; aborts the communicator and throws on error/timeout.
-  void wait_stream(hipStream_t s, double timeout_s);
+  // Wait for `s` with async-error polling: "" once it drains, else the RCCL error or "timeout after …".
+  // Does not abort: the caller decides (NativeTrainer.synchronize aborts, then raises).
+  std::string wait_stream(hipStream_t s, double timeout_s);
   void abort();
   int rank() const { return rank_; }
   int world() const { return world_; }
+  bool aborted() const { return aborted_; }
   static int version();
 
  private:

@@ -1,21 +1,24 @@
 // Static-schedule step orchestration (see trainer.h).
 //
 // Kernel sequence of one data-parallel step (reference CS5, survey §3; kernel IDs of §2.6):
-//   LeNet, 1 GPU : conv_fwd -> head(fwd+loss+dgrad) -> { conv_bwd  ||  wgrad(FC) on the aux stream }
-//                  -> reduce+sgd+pack (fused)
-//   LeNet, W > 1 : conv_fwd -> head -> { conv_bwd -> reduce(conv)  ||  wgrad(FC) -> reduce(FC) }
-//                  -> ONE all-reduce of the whole grad slab (RCCL) -> sgd_pack
-//   MLP          : head -> wgrad -> reduce -> [RCCL bucket] -> join -> sgd_pack
+//   LeNet, no comm : conv_fwd -> head(fwd+loss+dgrad) -> { conv_bwd  ||  wgrad(FC) -> reduce+sgd(FC) on aux }
+//                    -> reduce+sgd(conv) + step bump (fused reduce/SGD/pack kernels)
+//   LeNet, comm    : conv_fwd -> head -> { conv_bwd -> reduce(conv)  ||  wgrad(FC) -> reduce(FC) on aux }
+//                    then Plan::JOIN  : ONE all-reduce of the coalesced slab -> sgd_pack
+//                      or Plan::SPLIT : comm stream: AR(FC buckets) as soon as reduce(FC) is done (beside
+//                                       conv_bwd), then AR(conv buckets) after reduce(conv) -> sgd_pack
+//   MLP            : head -> wgrad -> reduce -> [RCCL buckets] -> sgd_pack
 // conv_bwd's one-round grid (2 blocks/CU) is LDS-bound and leaves VGPR room on every SIMD, which the
 // FC wgrad (no LDS) fills: running the two concurrently hides most of the wgrad (-6% step time on
-// one MI355X).  MNIST_AMD_CONCURRENT=0 restores the serial schedule (W > 1: conv bucket overlapped
-// with the FC wgrad, FC bucket exposed); MNIST_AMD_MG_SCHED=split sends the FC bucket as soon as it
-// is reduced (see launch_step_concurrent_comm).
-// All launches are allocation- and sync-free; capture() records the sequence (both streams,
-// RCCL included) into one hipGraph, so a training step costs one hipGraphLaunch on the host.
+// one MI355X).  MNIST_AMD_CONCURRENT=0 restores the serial single-GPU schedule.  Which multi-GPU plan
+// runs is chosen at start-up by timing the candidates (NativeTrainer.autotune_plan, parallel/ddp.py
+// choose_plan); MNIST_AMD_MG_SCHED=join|split overrides it.
+// All launches are allocation- and sync-free; capture() records the sequence (all streams, RCCL
+// included) into one hipGraph, so a training step costs one hipGraphLaunch on the host.
 #include "trainer.h"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
@@ -57,6 +60,14 @@ bool split_bwd() {
   }();
   return on;
 }
+// MNIST_AMD_TRACE=1: log every orchestration call of a step to stderr (host-side debugging)
+void trace(const char* what) {
+  static const bool on = [] {
+    const char* e = std::getenv("MNIST_AMD_TRACE");
+    return e && *e == '1';
+  }();
+  if (on) { std::fputs(what, stderr); std::fputc('\n', stderr); std::fflush(stderr); }
+}
 inline hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 template <typename P> P* ptr(uintptr_t v) { return reinterpret_cast<P*>(v); }
 }  // namespace
@@ -69,6 +80,7 @@ Trainer::Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const
   if (batch <= 0) throw std::invalid_argument("batch must be positive");
   if (ld_b < ((batch + 63) / 64) * 64) throw std::invalid_argument("ld_b must be >= batch rounded up to 64");
   nparam_ = model_nparam(model_);
+  max_conv_slabs_ = model_ == ModelKind::LENET ? lenet_conv_bwd_max_blocks(batch_, 0) : 0;
   const int cp = model_conv_params(model_);
   if (cp > 0) {
     buckets_.push_back({cp, nparam_, 0});
@@ -95,7 +107,7 @@ Trainer::~Trainer() {
 
 int Trainer::pack_size() const { return model_pack_size(model_); }
 int Trainer::conv_params() const { return model_conv_params(model_); }
-int Trainer::conv_slabs() const { return model_ == ModelKind::LENET ? lenet_conv_bwd_blocks(batch_) : 0; }
+int Trainer::conv_slabs() const { return model_ == ModelKind::LENET ? lenet_conv_bwd_blocks(batch_, bwd_blocks_) : 0; }
 
 void Trainer::invalidate() {
   if (exec_) { hipGraphExecDestroy(exec_); exec_ = nullptr; }
@@ -173,7 +185,7 @@ void Trainer::forward_backward(int B, uintptr_t stream) {
   launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s, hrows);
   post_launch(s);
   if (model_ == ModelKind::LENET) {
-    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), nullptr, s);
+    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), nullptr, s, 0, bwd_blocks_);
     post_launch(s);
   }
 }
@@ -193,7 +205,7 @@ void Trainer::reduce_grads(int B, uintptr_t stream) {
   launch_reduce(ptr<const float>(p_.slab_fc), nparam_, splits, cp, nparam_, scale, ptr<float>(p_.grad), s);
   post_launch(s);
   if (cp > 0) {
-    launch_reduce(ptr<const float>(p_.slab_conv), cp, lenet_conv_bwd_blocks(B), 0, cp, scale, ptr<float>(p_.grad), s);
+    launch_reduce(ptr<const float>(p_.slab_conv), cp, lenet_conv_bwd_blocks(B, bwd_blocks_), 0, cp, scale, ptr<float>(p_.grad), s);
     post_launch(s);
   }
 }
@@ -204,16 +216,29 @@ void Trainer::optimizer_step(float gscale, uintptr_t stream) {
   post_launch(S(stream));
 }
 
-void Trainer::comm_phase(int phase, hipStream_t s) {
-  if (!comm_) return;  // an attached communicator is always used (world 1 included: tests RCCL-in-graph)
-  hipStream_t cs = s;
-  if (overlap_) {
-    HIP_CHECK(hipEventRecord(events_[phase], s));
-    HIP_CHECK(hipStreamWaitEvent(comm_stream_, events_[phase], 0));
-    cs = comm_stream_;
+int Trainer::bwd_grid() const {
+  return model_ == ModelKind::LENET ? lenet_conv_bwd_blocks(batch_, bwd_blocks_) : 0;
+}
+
+void Trainer::spin(double seconds, uintptr_t stream) {
+  launch_spin(seconds, S(stream));
+  post_launch(S(stream));
+}
+
+void Trainer::all_reduce(const std::vector<Bucket>& bs, int phase, hipStream_t s) {
+  for (const Bucket& b : bs)
+    if (phase < 0 || b.phase == phase) comm_->all_reduce_sum_f32(ptr<float>(p_.grad) + b.p0, size_t(b.p1 - b.p0), s);
+}
+
+std::vector<Bucket> Trainer::issued_collectives() const {
+  std::vector<Bucket> out;
+  if (!comm_) return out;
+  if (model_ == ModelKind::LENET && plan_ == Plan::SPLIT) {
+    for (const Bucket& b : buckets_) if (b.phase == 0) out.push_back(b);
+    for (const Bucket& b : buckets_) if (b.phase != 0) out.push_back(b);
+    return out;
   }
-  for (const Bucket& b : buckets_)
-    if (b.phase == phase) comm_->all_reduce_sum_f32(ptr<float>(p_.grad) + b.p0, size_t(b.p1 - b.p0), cs);
+  return coalesced_buckets();
 }
 
 void Trainer::launch_step(int B, hipStream_t s) {
@@ -228,42 +253,29 @@ void Trainer::launch_step(int B, hipStream_t s) {
   }
   const int hrows = launch_head(model_, dtype_, true, br, hb, head_rows_per_block(model_, dtype_, batch_), s);
   post_launch(s);
-  if (comm_ && model_ == ModelKind::LENET && concurrent_mode() != 0) {
-    launch_step_concurrent_comm(B, hrows, s);
-    return;
-  }
-  if (comm_ && model_ == ModelKind::LENET) {
-    // Serial multi-GPU order (MNIST_AMD_CONCURRENT=0): conv backward FIRST, its (small) bucket
-    // all-reduce on the side stream then overlaps the FC wgrad + reduce below.  conv_bwd's 2 blocks/CU
-    // fill every CU's LDS for the kernel's whole life, so a collective queued "behind" it could not
-    // start until it ended.
-    int nslab = 0;
-    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s);
-    post_launch(s);
-    launch_reduce(ptr<const float>(p_.slab_conv), cp, nslab, 0, cp, scale, ptr<float>(p_.grad), s);
-    post_launch(s);
-    comm_phase(1, s);
-  }
-  if (!comm_ && model_ == ModelKind::LENET && concurrent_mode() != 0) {
-    // single GPU, concurrent branches: the FC wgrad (no LDS, 320 small blocks) runs on the aux stream
-    // beside conv_bwd (LDS-bound, 2 blocks/CU, 2 waves/SIMD: VGPR room is left for wgrad waves), then
-    // both join before the fused reduce + SGD + pack.  conv_bwd is enqueued first so its one-round
-    // grid is dispatched whole (measured: wgrad enqueued first 0.1692 ms/step, conv_bwd first 0.1565,
-    // serial 0.1671).
+
+  if (model_ == ModelKind::LENET && (comm_ || concurrent_mode() != 0)) {
+    // fork: conv_bwd on the main stream (enqueued first, so its one-round grid is dispatched whole:
+    // measured wgrad-first 0.1692 ms/step, conv_bwd-first 0.1565, serial 0.1671), the FC wgrad (no LDS,
+    // 320 small blocks) on the aux stream beside it
     HIP_CHECK(hipEventRecord(events_[4], s));
     HIP_CHECK(hipStreamWaitEvent(aux_stream_, events_[4], 0));
     int nslab = 0;
-    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s, split_bwd() ? 1 : 0);
+    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s, split_bwd() ? 1 : 0, bwd_blocks_);
     post_launch(s);
     if (split_bwd()) {
-      launch_lenet_conv_bwd(dtype_, br, conv_buffers(), nullptr, aux_stream_, 2);
+      launch_lenet_conv_bwd(dtype_, br, conv_buffers(), nullptr, aux_stream_, 2, bwd_blocks_);
       post_launch(aux_stream_);
     }
     const int splits =
         launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, aux_stream_, hrows);
     post_launch(aux_stream_);
-    // the FC update follows the FC wgrad on the aux stream (it touches only FC parameters and FC
-    // operand images); the conv update + step bump follows the join
+    if (comm_) {
+      launch_lenet_comm_tail(B, nslab, splits, s);
+      return;
+    }
+    // single GPU: the FC update follows the FC wgrad on the aux stream (it touches only FC parameters
+    // and FC operand images); the conv update + step bump follows the join
     launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
                       nparam_, splits, cp, cp, nparam_, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
                       ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, nullptr, aux_stream_);
@@ -276,87 +288,74 @@ void Trainer::launch_step(int B, hipStream_t s) {
     post_launch(s);
     return;
   }
+
   const int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s, hrows);
   post_launch(s);
+  int nslab = 0;
+  if (model_ == ModelKind::LENET) {  // serial single-GPU schedule (MNIST_AMD_CONCURRENT=0)
+    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s, 0, bwd_blocks_);
+    post_launch(s);
+  }
   if (!comm_) {
-    // single GPU: conv backward, then ONE fused reduce + SGD + pack kernel (2 boundaries fewer)
-    int nslab = 0;
-    if (model_ == ModelKind::LENET) {
-      launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s);
-      post_launch(s);
-    }
+    // ONE fused reduce + SGD + pack kernel (2 boundaries fewer than reduce -> sgd)
     launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
                       nparam_, splits, cp, 0, nparam_, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
                       ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, ptr<int32_t>(p_.step), s);
     post_launch(s);
     return;
   }
+  // MLP with a communicator: the whole backward is done here, nothing is left to overlap with
   launch_reduce(ptr<const float>(p_.slab_fc), nparam_, splits, cp, nparam_, scale, ptr<float>(p_.grad), s);
   post_launch(s);
-  comm_phase(0, s);
-  if (comm_ && overlap_) {
-    HIP_CHECK(hipEventRecord(events_[2], comm_stream_));
-    HIP_CHECK(hipStreamWaitEvent(s, events_[2], 0));
-  }
+  all_reduce(coalesced_buckets(), -1, s);
   launch_sgd_pack(model_, dtype_, ptr<float>(p_.params), ptr<const float>(p_.grad), ptr<float>(p_.mom),
                   ptr<void>(p_.pack), nparam_, lr_, momentum_, 1.0f / float(world_), ptr<int32_t>(p_.step), s);
   post_launch(s);
 }
 
-// LeNet with a communicator, concurrent branches:
-//   main : conv_bwd -> reduce(conv)                      \
-//   aux  : wgrad(FC) -> reduce(FC)   (beside conv_bwd)    > join -> all-reduce -> sgd_pack
-// MNIST_AMD_MG_SCHED=join (default): after the join, adjacent buckets of different backward phases are
-//   coalesced, so the default plan is ONE all-reduce of the whole 246,824-byte slab -- the exchange is
-//   latency-bound on xGMI, and one call pays the ring latency once instead of twice.
-// MNIST_AMD_MG_SCHED=split: the FC buckets go out on the comm stream as soon as reduce(FC) is done
-//   (they can only overlap conv_bwd where a CU has room beside its 2 LDS-heavy blocks), the conv
-//   buckets after reduce(conv).
-void Trainer::launch_step_concurrent_comm(int B, int hrows, hipStream_t s) {
-  static const bool split = [] {
-    const char* e = std::getenv("MNIST_AMD_MG_SCHED");
-    return e && std::string(e) == "split";
-  }();
-  const BatchRef br = batch_ref(B);
-  const HeadBuffers hb = head_buffers(ptr<float>(p_.metrics));
-  const float scale = 1.0f / float(B);
+// LeNet with a communicator, after the fork (conv_bwd on `s`, FC wgrad on the aux stream).
+// Every collective is issued on ONE stream per plan (JOIN: main, SPLIT: comm), in a fixed order, so all
+// ranks enqueue the same RCCL sequence.
+void Trainer::launch_lenet_comm_tail(int B, int nslab, int splits, hipStream_t s) {
+  const float scale = 1.0f / float(B), gs = 1.0f / float(world_);
   const int cp = model_conv_params(model_);
-  HIP_CHECK(hipEventRecord(events_[4], s));
-  HIP_CHECK(hipStreamWaitEvent(aux_stream_, events_[4], 0));
-  int nslab = 0;
-  launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s, split_bwd() ? 1 : 0);
-  post_launch(s);
-  if (split_bwd()) {
-    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), nullptr, aux_stream_, 2);
-    post_launch(aux_stream_);
-  }
-  const int splits =
-      launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, aux_stream_, hrows);
-  post_launch(aux_stream_);
-  launch_reduce(ptr<const float>(p_.slab_fc), nparam_, splits, cp, nparam_, scale, ptr<float>(p_.grad), aux_stream_);
+  float* g = ptr<float>(p_.grad);
+  launch_reduce(ptr<const float>(p_.slab_fc), nparam_, splits, cp, nparam_, scale, g, aux_stream_);
   post_launch(aux_stream_);
   HIP_CHECK(hipEventRecord(events_[5], aux_stream_));
   if (split_bwd()) HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));  // conv2 columns come from the aux half
-  launch_reduce(ptr<const float>(p_.slab_conv), cp, nslab, 0, cp, scale, ptr<float>(p_.grad), s);
-  post_launch(s);
-  float* g = ptr<float>(p_.grad);
-  if (split) {
-    HIP_CHECK(hipStreamWaitEvent(comm_stream_, events_[5], 0));
-    for (const Bucket& b : buckets_)
-      if (b.phase == 0) comm_->all_reduce_sum_f32(g + b.p0, size_t(b.p1 - b.p0), comm_stream_);
-    HIP_CHECK(hipEventRecord(events_[1], s));
-    HIP_CHECK(hipStreamWaitEvent(comm_stream_, events_[1], 0));
-    for (const Bucket& b : buckets_)
-      if (b.phase != 0) comm_->all_reduce_sum_f32(g + b.p0, size_t(b.p1 - b.p0), comm_stream_);
-    HIP_CHECK(hipEventRecord(events_[2], comm_stream_));
-    HIP_CHECK(hipStreamWaitEvent(s, events_[2], 0));
-  } else {
+  if (plan_ == Plan::JOIN) {
+    launch_reduce(ptr<const float>(p_.slab_conv), cp, nslab, 0, cp, scale, g, s);
+    post_launch(s);
     HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));
-    for (const Bucket& b : coalesced_buckets()) comm_->all_reduce_sum_f32(g + b.p0, size_t(b.p1 - b.p0), s);
+    all_reduce(coalesced_buckets(), -1, s);
+    launch_sgd_pack(model_, dtype_, ptr<float>(p_.params), g, ptr<float>(p_.mom), ptr<void>(p_.pack), nparam_, lr_,
+                    momentum_, gs, ptr<int32_t>(p_.step), s);
+    post_launch(s);
+    return;
   }
-  launch_sgd_pack(model_, dtype_, ptr<float>(p_.params), ptr<const float>(p_.grad), ptr<float>(p_.mom),
-                  ptr<void>(p_.pack), nparam_, lr_, momentum_, 1.0f / float(world_), ptr<int32_t>(p_.step), s);
+  // SPLIT: the comm stream sends the FC buckets as soon as reduce(FC) is done (beside conv_bwd), then
+  // the conv buckets after reduce(conv); one update after both.  (A graph where another stream waits
+  // on an event recorded behind a captured RCCL call made hipStreamEndCapture segfault on ROCm 7.0's
+  // runtime, so only the main stream consumes the comm stream's completion.)
+  trace("split: comm waits reduce(FC)");
+  HIP_CHECK(hipStreamWaitEvent(comm_stream_, events_[5], 0));
+  trace("split: AR(FC)");
+  all_reduce(buckets_, 0, comm_stream_);
+  trace("split: reduce(conv)");
+  launch_reduce(ptr<const float>(p_.slab_conv), cp, nslab, 0, cp, scale, g, s);
   post_launch(s);
+  HIP_CHECK(hipEventRecord(events_[1], s));
+  HIP_CHECK(hipStreamWaitEvent(comm_stream_, events_[1], 0));
+  trace("split: AR(conv)");
+  all_reduce(buckets_, 1, comm_stream_);
+  HIP_CHECK(hipEventRecord(events_[0], comm_stream_));
+  HIP_CHECK(hipStreamWaitEvent(s, events_[0], 0));
+  trace("split: update");
+  launch_sgd_pack(model_, dtype_, ptr<float>(p_.params), g, ptr<float>(p_.mom), ptr<void>(p_.pack), nparam_, lr_,
+                  momentum_, gs, ptr<int32_t>(p_.step), s);
+  post_launch(s);
+  trace("split: done");
 }
 
 std::vector<Bucket> Trainer::coalesced_buckets() const {
@@ -401,6 +400,7 @@ void Trainer::eval_batch(uintptr_t images, uintptr_t labels, uintptr_t idx, int 
 void Trainer::capture(uintptr_t stream) {
   invalidate();
   hipStream_t s = S(stream);
+  trace("capture: begin");
   HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
   try {
     launch_step(batch_, s);
@@ -410,8 +410,11 @@ void Trainer::capture(uintptr_t stream) {
     if (g) hipGraphDestroy(g);
     throw;
   }
+  trace("capture: end");
   HIP_CHECK(hipStreamEndCapture(s, &graph_));
+  trace("capture: instantiate");
   HIP_CHECK(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
+  trace("capture: done");
 }
 
 void Trainer::replay(uintptr_t stream) {

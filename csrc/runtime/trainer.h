@@ -6,6 +6,7 @@
 
 #include <cstdint>
 #include <map>
+#include <stdexcept>
 #include <memory>
 #include <string>
 #include <vector>
@@ -29,6 +30,14 @@ struct Bucket {
   int p0, p1, phase;
 };
 
+// Multi-GPU step plans (LeNet; the MLP's backward is one fused head kernel + one wgrad, so it always
+// joins).  Both keep every collective on ONE comm stream, in the same order on every rank.
+//   JOIN  : FC branch and conv_bwd join, then ONE all-reduce of the coalesced slab, then one SGD.
+//   SPLIT : the FC buckets go out on the comm stream as soon as the FC grads are reduced (beside
+//           conv_bwd, which may be given fewer workgroups so whole CUs stay free for RCCL's kernels);
+//           the conv buckets follow reduce(conv) on the same stream, then one update.
+enum class Plan : int { JOIN = 0, SPLIT = 1 };
+
 class Trainer {
  public:
   Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const TrainerPtrs& p);
@@ -40,7 +49,28 @@ class Trainer {
   void set_dropout(float p, uint32_t seed) { drop_p_ = p; seed_ = seed; invalidate(); }
   void set_buckets(const std::vector<Bucket>& b) { buckets_ = b; invalidate(); }
   std::vector<Bucket> buckets() const { return buckets_; }
-  void set_overlap(bool on) { overlap_ = on; invalidate(); }
+  void set_plan(int p) {
+    if (p != 0 && p != 1) throw std::invalid_argument("plan must be 0 (join) or 1 (split)");
+    plan_ = static_cast<Plan>(p);
+    invalidate();
+  }
+  int plan() const { return static_cast<int>(plan_); }
+  // conv_bwd workgroup target (0 = default); the grid actually used for the full batch is bwd_grid()
+  void set_bwd_blocks(int n) {
+    n = n < 0 ? 0 : n;
+    if (lenet_conv_bwd_max_blocks(batch_, n) > max_conv_slabs_)
+      throw std::invalid_argument("set_bwd_blocks: more conv_bwd workgroups than conv slab rows");
+    bwd_blocks_ = n;
+    invalidate();
+  }
+  int bwd_blocks() const { return bwd_blocks_; }
+  int bwd_grid() const;
+  // The collectives one full-batch step issues under the current plan, in issue order.
+  std::vector<Bucket> issued_collectives() const;
+  bool has_comm() const { return comm_ != nullptr; }
+  int world() const { return world_; }
+  // Hold `stream` busy for `seconds` (bounded device spin; watchdog tests).
+  void spin(double seconds, uintptr_t stream);
 
   void pack(uintptr_t stream);
   // Full eager step for a batch of B rows (B <= batch).
@@ -70,9 +100,9 @@ class Trainer {
   HeadBuffers head_buffers(float* metrics) const;
   LenetConvBuffers conv_buffers() const;
   void launch_step(int B, hipStream_t s);
-  void launch_step_concurrent_comm(int B, int hrows, hipStream_t s);
+  void launch_lenet_comm_tail(int B, int nslab, int splits, hipStream_t s);
   std::vector<Bucket> coalesced_buckets() const;
-  void comm_phase(int phase, hipStream_t s);
+  void all_reduce(const std::vector<Bucket>& bs, int phase, hipStream_t s);
 
   ModelKind model_;
   DType dtype_;
@@ -81,7 +111,9 @@ class Trainer {
   float lr_ = 0.01f, momentum_ = 0.f, drop_p_ = 0.2f;
   uint32_t seed_ = 1234;
   int world_ = 1;
-  bool overlap_ = true;
+  Plan plan_ = Plan::JOIN;
+  int bwd_blocks_ = 0;
+  int max_conv_slabs_ = 0;  // rows of the conv slab (lenet_conv_bwd_max_blocks(batch) at the default target)
   std::shared_ptr<RcclComm> comm_;
   std::vector<Bucket> buckets_;
   hipStream_t comm_stream_ = nullptr;

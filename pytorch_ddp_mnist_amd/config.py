@@ -11,7 +11,8 @@ Reference behaviour reproduced here:
     ``LOCAL_RANK`` env var).
 
 Additive flags (survey §5.6): --model, --dtype, --momentum, --lr, --synthetic,
---bucket_cap_kb, --profile, --seed, --no_save, --comm, --graph.
+--bucket_cap_kb, --profile, --seed, --no_save, --comm, --no_graph, --plan, --tqdm, --progress_every,
+--resume, --io_mode.
 """
 from __future__ import annotations
 
@@ -56,7 +57,8 @@ class TrainConfig:
     metrics_jsonl: Optional[str] = None
     local_rank: Optional[int] = None
     shard_eval: bool = False
-    sampler: str = "torch"      # "torch" (bit-equal DistributedSampler) | "device"
+    progress_every: int = 0     # --tqdm update period in batches (0 = ~20 updates per epoch)
+    plan: str = "auto"          # multi-GPU step plan: "auto" (timed at start-up) | "join" | "split"
     resume: Optional[str] = None  # params + momentum + epoch file: loaded if present, rewritten each epoch
 
     def to_nested(self) -> dict:
@@ -101,16 +103,18 @@ def _add_extra_flags(p: argparse.ArgumentParser, defaults: TrainConfig) -> None:
     add("--no_save", action="store_true", help="do not write model.pt")
     add("--save_path", type=str, default=None)
     add("--metrics_jsonl", type=str, default=None, help="append per-epoch metrics as JSON lines")
-    add("--tqdm", action="store_true", help="show progress bars (reference DISABLE_TQDM=True is ignored there)")
+    add("--tqdm", action="store_true", help="rank-0 progress bars with the batch loss (reference: tqdm per batch)")
+    add("--progress_every", type=int, default=None, help="--tqdm update period in batches (one device sync each)")
     add("--shard_eval", action="store_true", help="shard the test set across ranks (reference: every rank evaluates all)")
-    add("--sampler", type=str, default=None, choices=["torch", "device"])
+    add("--plan", type=str, default=None, choices=["auto", "join", "split"],
+        help="multi-GPU step plan (auto: time the candidates on the communicator at start-up)")
     add("--resume", type=str, default=None,
         help="resume file (params + momentum + epoch): loaded when it exists, rewritten after every epoch")
 
 
 def _apply_extra(cfg: TrainConfig, a: argparse.Namespace) -> None:
     for name in ("model", "dtype", "lr", "momentum", "dropout", "seed", "init_seed", "data_format",
-                 "device", "bucket_cap_kb", "comm", "save_path", "metrics_jsonl", "sampler", "resume"):
+                 "device", "bucket_cap_kb", "comm", "save_path", "metrics_jsonl", "plan", "resume", "progress_every"):
         v = getattr(a, name, None)
         if v is not None:
             setattr(cfg, name, v)

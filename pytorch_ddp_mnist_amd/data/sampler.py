@@ -8,15 +8,13 @@ padded by repeating its head to ``ceil(N/W)*W``, then ``[rank::W]``.
 The native engine does not iterate a Python sampler per batch: it uploads one
 int32 index vector per epoch into HBM and every training kernel reads its
 batch slice from there (``device_loader``).  ``epoch_indices`` builds that
-vector; for the device-only shuffle (no host randperm at all) see
-``feistel_permutation`` which the HIP gather kernels can evaluate in-register.
+vector (the next epoch's is computed on the host while the current one trains).
 """
 from __future__ import annotations
 
 import math
-from typing import Iterator, List, Optional
+from typing import Iterator, List
 
-import numpy as np
 import torch
 
 
@@ -83,40 +81,3 @@ def batch_slices(count: int, batch_size: int, drop_last: bool = False) -> List[t
             break
         out.append((s, b))
     return out
-
-
-# ---------------------------------------------------------------------------------------------
-# Device-side shuffle: a keyed bijection on [0, n) (4-round Feistel on the next power of two with
-# cycle walking).  Mirrors csrc/kernels/common.h::feistel_index bit for bit.
-# ---------------------------------------------------------------------------------------------
-def _mix32(x: np.ndarray, k: int) -> np.ndarray:
-    x = (x ^ np.uint32(k)) * np.uint32(0x9E3779B1)
-    x ^= x >> np.uint32(15)
-    x = x * np.uint32(0x85EBCA77)
-    x ^= x >> np.uint32(13)
-    return x
-
-
-def feistel_permutation(n: int, key: int, out: Optional[np.ndarray] = None) -> np.ndarray:
-    bits = max(2, int(math.ceil(math.log2(max(n, 2)))))
-    if bits % 2:
-        bits += 1
-    half = bits // 2
-    mask = np.uint32((1 << half) - 1)
-    keys = [(key * 0x27D4EB2F + r * 0x165667B1) & 0xFFFFFFFF for r in range(4)]
-
-    def perm(v: np.ndarray) -> np.ndarray:
-        with np.errstate(over="ignore"):
-            left = (v >> np.uint32(half)) & mask
-            right = v & mask
-            for r in range(4):
-                left, right = right, left ^ (_mix32(right.copy(), keys[r]) & mask)
-            return (left << np.uint32(half)) | right
-
-    idx = np.arange(n, dtype=np.uint32)
-    res = perm(idx)
-    bad = res >= n
-    while bad.any():            # cycle walking keeps the map a bijection on [0, n)
-        res[bad] = perm(res[bad])
-        bad = res >= n
-    return res.astype(np.int64) if out is None else out

@@ -9,12 +9,19 @@ allocator, never re-allocated per step) and exposes epoch-level operations:
     async copy; kernels address their batch through a device step counter, so the captured
     hipGraph of a step is replayed unchanged for every full batch;
   * loss / accuracy are accumulated on the device and read back once per epoch (the reference
-    syncs with ``.item()`` every batch, survey K16).
+    syncs with ``.item()`` every batch, survey K16);
+  * with a communicator attached, every host wait goes through the RCCL watchdog
+    (``RcclComm.wait_stream``: async-error polling + deadline -> ``ncclCommAbort`` ->
+    :class:`CollectiveError`), the behaviour the reference inherits from ProcessGroupNCCL's
+    timeout (ddp_tutorial_multi_gpu.py:133-134, survey N10/§5.3);
+  * the multi-GPU step plan (JOIN / SPLIT, ``csrc/runtime/trainer.h``) is chosen at start-up by
+    timing the candidates on the real communicator (:meth:`NativeTrainer.autotune_plan`).
 """
 from __future__ import annotations
 
 import math
 import os
+import time
 from dataclasses import dataclass
 from typing import Dict, Optional, Tuple
 
@@ -22,6 +29,24 @@ import torch
 
 from ..models import MODEL_IDS, build_model, flatten_state, unflatten_state
 from ..ops.native import require_gpu
+
+PLANS = {"join": 0, "split": 1}
+PLAN_NAMES = {v: k for k, v in PLANS.items()}
+
+
+class CollectiveError(RuntimeError):
+    """A gradient collective failed or exceeded the watchdog deadline; the communicator is aborted.
+    ``detected_after`` = seconds from the start of the wait to the detection (before the abort)."""
+
+    def __init__(self, msg: str, detected_after: float = 0.0):
+        super().__init__(msg)
+        self.detected_after = detected_after
+
+
+def comm_timeout() -> float:
+    """Watchdog deadline in seconds (``MNIST_AMD_COMM_TIMEOUT``, default 600 = c10d's NCCL default)."""
+    return float(os.environ.get("MNIST_AMD_COMM_TIMEOUT", "600"))
+
 
 HEAD_DIMS = {  # K0P, N1P, N2P  (csrc/kernels/models.h)
     "mlp": (800, 128, 128),
@@ -84,7 +109,8 @@ class NativeTrainer:
         self.xT, self.h1T, self.h2T = z(K0P, self.ld_b), z(N1P, self.ld_b), z(N2P, self.ld_b)
         self.dy1T, self.dy2T, self.dy3T = z(N1P, self.ld_b), z(N2P, self.ld_b), z(16, self.ld_b)
         self.slab_fc = z(fc_splits, self.nparam, dt=torch.float32)
-        conv_slabs = C.conv_bwd_blocks(self.batch) if model == "lenet5" else 0
+        # rows for any batch <= self.batch (a partial last batch can need more workgroups than a full one)
+        conv_slabs = C.conv_bwd_max_blocks(self.batch) if model == "lenet5" else 0
         ncp = C.model_conv_params(mid)
         self.slab_conv = z(max(conv_slabs, 1), max(ncp, 1), dt=torch.float32)
         if model == "lenet5":
@@ -142,7 +168,7 @@ class NativeTrainer:
         self.load_flat(flatten_state(module))
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
-        self.stream.synchronize()
+        self.synchronize()
         return unflatten_state(self.module_template, self.params)
 
     def to_module(self) -> torch.nn.Module:
@@ -151,13 +177,29 @@ class NativeTrainer:
         return m
 
     # ------------------------------------------------------------------ distributed
-    def attach_comm(self, comm, world: int, overlap: bool = True) -> None:
+    def attach_comm(self, comm, world: int, plan: str = "join", bwd_blocks: int = 0) -> None:
         """Use a native RcclComm for the gradient all-reduce (None = local only)."""
         self.comm, self.world = comm, world
         if comm is not None:
             self.rt.set_comm(comm)
         self.rt.set_world(world)
-        self.rt.set_overlap(overlap)
+        self.set_plan(plan, bwd_blocks)
+
+    def set_plan(self, plan: str, bwd_blocks: int = 0) -> None:
+        self.rt.set_plan(PLANS[plan])
+        if self.model_name == "lenet5":
+            self.rt.set_bwd_blocks(int(bwd_blocks))
+
+    @property
+    def plan(self) -> str:
+        return PLAN_NAMES[self.rt.plan]
+
+    def plan_info(self) -> dict:
+        """What a full-batch step runs: plan, conv_bwd grid, and the collectives in issue order."""
+        coll = [(b.p0, b.p1) for b in self.rt.issued_collectives()]
+        return {"plan": self.plan if self.comm is not None else "local",
+                "conv_bwd_grid": self.rt.bwd_grid if self.model_name == "lenet5" else None,
+                "collectives": [{"params": [a, b], "bytes": 4 * (b - a)} for a, b in coll]}
 
     def set_buckets(self, ranges) -> None:
         self.rt.set_buckets([self.C.Bucket(int(a), int(b), int(ph)) for a, b, ph in ranges])
@@ -169,7 +211,77 @@ class NativeTrainer:
         self._sync_in()
         self.comm.broadcast_f32(self.params.data_ptr(), self.nparam, root, self.stream.cuda_stream)
         self.rt.pack(self.stream.cuda_stream)
-        self.comm.wait_stream(self.stream.cuda_stream, 300.0)
+        self.synchronize()
+
+    def check_comm(self) -> None:
+        """Non-blocking health poll (once per epoch): abort + raise on an asynchronous RCCL error."""
+        if self.comm is None:
+            return
+        err = self.comm.async_error()
+        if err:
+            self.comm.abort()
+            raise CollectiveError(f"RCCL communicator error on rank {self.comm.rank}: {err}")
+
+    def autotune_plan(self, candidates=None, iters: int = 12, warmup: int = 3, reduce_max=None,
+                      margin: float = 0.015, log=None) -> dict:
+        """Time each candidate plan on the attached communicator and keep the fastest.
+
+        Every candidate replays the captured step ``warmup + iters`` times on batch 0 of the loaded
+        epoch order (the device step counter is rewound after each replay), so all ranks issue the
+        same collectives in the same order; per-replay GPU times come from events on the step
+        stream and ``reduce_max`` (e.g. a gloo MAX all-reduce) makes the decision identical on every
+        rank.  Parameters, momentum, counters and metrics are restored afterwards.
+        ``MNIST_AMD_MG_SCHED=join|split`` skips the search.
+        """
+        from ..parallel.ddp import choose_plan, default_plan_candidates
+        forced = os.environ.get("MNIST_AMD_MG_SCHED")
+        if self.comm is None:
+            return {"chosen": "local", "timings_ms": {}}
+        if forced:
+            self.set_plan(forced, 0)
+            return {"chosen": forced, "timings_ms": {}, "forced": True}
+        if self.model_name != "lenet5":
+            self.set_plan("join", 0)
+            return {"chosen": "join", "timings_ms": {}}
+        if candidates is None:
+            ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+            candidates = default_plan_candidates(self.C.conv_bwd_blocks(self.batch), ncu)
+        if getattr(self, "n_epoch", 0) < max(2, self.host_step + 1) * self.batch:
+            raise RuntimeError("autotune_plan: the loaded epoch order needs >= 2 full batches beyond the current step")
+        self.synchronize()
+        saved = [t.clone() for t in (self.params, self.mom, self.grad, self.step_ctr, self.metrics)]
+        self._sync_in()
+        timings = {}
+        st = self.stream
+        for name, (plan, blocks) in candidates.items():
+            self.set_plan(plan, blocks)
+            self.capture()
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(warmup + iters)]
+            with torch.cuda.stream(st):
+                self.step_ctr[0].zero_()  # every replay trains on batch 0 of the loaded order
+            for a, b in ev:
+                a.record(st)
+                self.rt.replay(st.cuda_stream)
+                b.record(st)
+                with torch.cuda.stream(st):
+                    self.step_ctr[0].zero_()
+            self.synchronize()
+            ts = sorted(a.elapsed_time(b) for a, b in ev[warmup:])
+            med = ts[len(ts) // 2]
+            timings[name] = reduce_max(med) if reduce_max is not None else med
+        with torch.cuda.stream(st):
+            for dst, src in zip((self.params, self.mom, self.grad, self.step_ctr, self.metrics), saved):
+                dst.copy_(src)
+        self.rt.pack(st.cuda_stream)
+        chosen = choose_plan(timings, margin=margin)
+        self.set_plan(*candidates[chosen])
+        self.synchronize()
+        out = {"chosen": chosen, "timings_ms": {k: round(v, 4) for k, v in timings.items()},
+               "candidates": {k: {"plan": p, "bwd_blocks": b} for k, (p, b) in candidates.items()}}
+        if log is not None:
+            log(out)
+        return out
 
     # ------------------------------------------------------------------ training
     def set_epoch_indices(self, indices: torch.Tensor) -> None:
@@ -183,13 +295,23 @@ class NativeTrainer:
             self.idx[:n].copy_(src, non_blocking=True)
             self.step_ctr[0].zero_()
         self.n_epoch = n
+        self.host_step = 0  # mirror of the device step counter: every launch is bounds-checked on the host
+
+    def _check_rows(self, B: int) -> None:
+        """The kernels read idx[step * batch + r], r < B, through the DEVICE step counter: refuse on the
+        host any step that would index past the loaded order (an out-of-bounds gather faults the GPU)."""
+        if B <= 0 or B > self.batch:
+            raise ValueError(f"batch of {B} rows outside (0, {self.batch}]")
+        if getattr(self, "n_epoch", 0) < self.host_step * self.batch + B:
+            raise RuntimeError(f"step {self.host_step} of {B} rows would read past the {getattr(self, 'n_epoch', 0)} "
+                               f"loaded indices; call set_epoch_indices first")
 
     def reset_metrics(self) -> None:
         with torch.cuda.stream(self.stream):
             self.metrics.zero_()
 
     def read_metrics(self, which: str = "train") -> EpochStats:
-        self.stream.synchronize()
+        self.synchronize()
         m = (self.metrics if which == "train" else self.eval_metrics).tolist()
         return EpochStats(*m)
 
@@ -198,6 +320,8 @@ class NativeTrainer:
 
     def step(self, B: Optional[int] = None, use_graph: bool = True) -> None:
         B = self.batch if B is None else B
+        self._check_rows(B)
+        self.host_step += 1
         if use_graph and B == self.batch:
             if not self.rt.captured:
                 self.capture()
@@ -236,15 +360,29 @@ class NativeTrainer:
     # ------------------------------------------------------------------ phases (tests / torch comm)
     def forward_backward(self, B: Optional[int] = None) -> None:
         B = self.batch if B is None else B
+        self._check_rows(B)
         self.rt.forward_backward(B, self.stream.cuda_stream)
         self.rt.reduce_grads(B, self.stream.cuda_stream)
 
     def optimizer_step(self, gscale: float = 1.0) -> None:
         self.rt.optimizer_step(float(gscale), self.stream.cuda_stream)
+        self.host_step += 1  # the SGD kernel bumps the device counter
 
     def grads(self) -> torch.Tensor:
-        self.stream.synchronize()
+        self.synchronize()
         return self.grad.detach().cpu().clone()
 
-    def synchronize(self) -> None:
-        self.stream.synchronize()
+    def synchronize(self, timeout: Optional[float] = None) -> None:
+        """Wait for the step stream.  With a communicator this is the collective watchdog: RCCL async
+        errors are polled while waiting and a deadline (``MNIST_AMD_COMM_TIMEOUT``) aborts the
+        communicator and raises :class:`CollectiveError` instead of hanging in hipStreamSynchronize."""
+        if self.comm is None:
+            self.stream.synchronize()
+            return
+        t0 = time.perf_counter()
+        err = self.comm.wait_stream(self.stream.cuda_stream, comm_timeout() if timeout is None else timeout)
+        if err:
+            detected = time.perf_counter() - t0
+            self.comm.abort()  # ncclCommAbort: RCCL kernels still waiting on peers exit
+            raise CollectiveError(f"rank {self.comm.rank}: RCCL collective failed: {err} (communicator aborted)",
+                                  detected)

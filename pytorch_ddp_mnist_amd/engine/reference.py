@@ -68,6 +68,7 @@ class TorchCPUEngine:
         self.reducer = GlooReducer(self.module, world, plan_buckets(model_phases(model), cap))
         self.crit = F.nll_loss if model == "lenet5" else F.cross_entropy
         self.fault = FaultInjector(int(os.environ.get("RANK", "0")))
+        self.global_step = 0
 
     def train_epoch(self, indices: torch.Tensor, progress=None, prefetch=None) -> EpochResult:
         r = EpochResult()
@@ -77,13 +78,14 @@ class TorchCPUEngine:
         for s, b in slices:
             idx = indices[s:s + b]
             x, y = self.x[idx], self.y[idx]
+            self.fault.tick()  # before the step, as NativeEngine._step: FAIL_AT_STEP=k -> k completed steps
             self.opt.zero_grad()
             out = self.module(x)
             loss = self.crit(out, y)
             loss.backward()
             self.reducer.sync_grads()
             self.opt.step()
-            self.fault.tick()
+            self.global_step += 1
             lv = float(loss.item()) * b
             r.loss_sum += lv
             r.correct += float((out.argmax(1) == y).sum())
@@ -94,15 +96,15 @@ class TorchCPUEngine:
             else:
                 r.last_sum, r.last_b = lv, b
             r.steps += 1
-            if progress:
-                progress(float(loss.item()))
+            if progress is not None:
+                progress(lv / b, 1)
         r.seconds = time.perf_counter() - t0
         if prefetch is not None:
             r.next_indices = prefetch()
         return r
 
     @torch.no_grad()
-    def evaluate(self, indices: torch.Tensor) -> EpochResult:
+    def evaluate(self, indices: torch.Tensor, progress=None) -> EpochResult:
         r = EpochResult()
         self.module.eval()
         for s, b in batch_slices(indices.numel(), self.batch):
@@ -110,6 +112,8 @@ class TorchCPUEngine:
             out = self.module(self.xt[idx])
             y = self.yt[idx]
             lv = float(self.crit(out, y, reduction="sum"))
+            if progress is not None:
+                progress(lv / b, 1)
             r.loss_sum += lv
             r.correct += float((out.argmax(1) == y).sum())
             r.count += b
@@ -129,9 +133,10 @@ class TorchCPUEngine:
         bufs = [self.opt.state.get(p, {}).get("momentum_buffer") for p in self.module.parameters()]
         mom = torch.cat([(b if b is not None else torch.zeros_like(p)).reshape(-1)
                          for b, p in zip(bufs, self.module.parameters())])
-        return params, mom
+        return params, mom, self.global_step
 
-    def set_state(self, params: torch.Tensor, mom) -> None:
+    def set_state(self, params: torch.Tensor, mom, global_step: int = 0) -> None:
+        self.global_step = int(global_step)
         off = 0
         with torch.no_grad():
             for p in self.module.parameters():

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import os
 import time
-from typing import Optional
+from typing import Optional, Tuple
 
 import numpy as np
 import torch
@@ -22,8 +22,8 @@ from ..parallel.comm import DistContext, init_distributed
 from ..parallel.ddp import model_phases, plan_buckets
 from ..utils.checkpoint import load_resume, save_model, save_resume
 from ..utils.fault import FaultInjector, check_finite
-from ..utils.logging import MetricsWriter, banner, epoch_line, reference_epoch_loss
-from ..utils.profiling import enable as enable_roctx, range_
+from ..utils.logging import MetricsWriter, ProgressBar, banner, epoch_line, reference_epoch_loss
+from ..utils.profiling import PhaseTimer, enable as enable_roctx, range_
 from .reference import EpochResult, TorchCPUEngine
 
 
@@ -54,15 +54,21 @@ class NativeEngine:
             self.tr.load_flat(self.tr.params.clone())
         self.use_graph = cfg.graph and not self.torch_comm
         self.fault = FaultInjector(ctx.rank)
+        self.plan_forced = None if cfg.plan == "auto" else cfg.plan
+        self.tuned = self.tr.comm is None
+        self.tune = None
 
     def get_state(self):
         self.tr.synchronize()
-        return self.tr.params.detach().cpu().clone(), self.tr.mom.detach().cpu().clone()
+        return (self.tr.params.detach().cpu().clone(), self.tr.mom.detach().cpu().clone(),
+                int(self.tr.step_ctr[1].item()))
 
-    def set_state(self, params: torch.Tensor, mom) -> None:
+    def set_state(self, params: torch.Tensor, mom, global_step: int = 0) -> None:
         self.tr.load_flat(params)
-        if mom is not None:
-            self.tr.mom.copy_(mom.to(self.tr.mom.device))
+        with torch.cuda.stream(self.tr.stream):  # ordered before the next step on the trainer stream
+            if mom is not None:
+                self.tr.mom.copy_(mom.to(self.tr.mom.device), non_blocking=True)
+            self.tr.step_ctr[1].fill_(int(global_step))  # dropout stream continues, not replayed
         self.tr.synchronize()
 
     def _step(self, b: int) -> None:
@@ -70,25 +76,52 @@ class NativeEngine:
         if self.torch_comm:
             import torch.distributed as dist
             self.tr.forward_backward(b)
-            self.tr.synchronize()
-            dist.all_reduce(self.tr.grad)
+            # the collective is enqueued behind the backward on the trainer stream, and the SGD kernel
+            # that follows on the same stream waits for it (c10d makes the current stream wait)
+            with torch.cuda.stream(self.tr.stream):
+                dist.all_reduce(self.tr.grad)
             self.tr.optimizer_step(1.0 / self.ctx.world)
         else:
             self.tr.step(b, use_graph=self.use_graph)
 
+    def _maybe_tune(self, nfull: int) -> None:
+        """First epoch with a communicator: pick the multi-GPU step plan by timing the candidates."""
+        if self.tuned or nfull < 1:
+            return
+        self.tuned = True
+        if self.plan_forced:
+            self.tr.set_plan(self.plan_forced)
+            return
+        self.tune = self.tr.autotune_plan(reduce_max=self.ctx.all_reduce_max)
+        if self.ctx.rank == 0:
+            print(f"[rank0] step plan: {self.tune['chosen']} (ms/step {self.tune['timings_ms']})", flush=True)
+
+    def _window_loss(self, prev: float, steps: int, B: int) -> Tuple[float, float]:
+        cur = self.tr.read_metrics().loss_sum
+        return cur, (cur - prev) / max(1, steps * B)
+
     def train_epoch(self, indices: torch.Tensor, progress=None, prefetch=None) -> EpochResult:
         """``prefetch`` (optional) runs on the host while the epoch's steps execute on the GPU: the
-        next epoch's sampler order is ready when this one ends (no host gap between epochs)."""
+        next epoch's sampler order is ready when this one ends (no host gap between epochs).
+        ``progress`` (optional, --tqdm) gets the mean batch loss of the last ``progress.every``
+        batches; reading it is a device sync, so it happens only every ``every`` steps."""
         tr, B = self.tr, self.batch
         r = EpochResult()
         t0 = time.perf_counter()
         tr.set_epoch_indices(indices)
-        tr.reset_metrics()
         n = indices.numel()
         nfull, last = divmod(n, B)
+        self._maybe_tune(nfull)
+        tr.reset_metrics()
+        every = getattr(progress, "every", 0) if progress is not None else 0
+        prev = 0.0
         with range_("train_full_batches"):
-            for _ in range(nfull):
+            for i in range(nfull):
                 self._step(B)
+                if every and ((i + 1) % every == 0 or i + 1 == nfull):
+                    k = (i % every) + 1
+                    prev, bl = self._window_loss(prev, k, B)
+                    progress(bl, k)
         if prefetch is not None:
             r.next_indices = prefetch()
         m = tr.read_metrics()
@@ -98,12 +131,15 @@ class NativeEngine:
             m2 = tr.read_metrics()
             r.last_sum, r.last_b = m2.loss_sum - m.loss_sum, last
             m = m2
+            if every:
+                progress(r.last_sum / last, 1)
         tr.synchronize()
+        tr.check_comm()
         r.loss_sum, r.correct, r.count = m.loss_sum, m.correct, m.count
         r.seconds, r.steps = time.perf_counter() - t0, nfull + (1 if last else 0)
         return r
 
-    def evaluate(self, indices: torch.Tensor) -> EpochResult:
+    def evaluate(self, indices: torch.Tensor, progress=None) -> EpochResult:
         tr, B = self.tr, self.batch
         r = EpochResult()
         idx = indices.to(self.ctx.device, torch.int32).contiguous()
@@ -115,8 +151,15 @@ class NativeEngine:
         def run(s, b):
             tr.rt.eval_batch(self.test_images.data_ptr(), self.test_labels.data_ptr(), idx.data_ptr() + 4 * s, b,
                              tr.eval_metrics.data_ptr(), tr.stream.cuda_stream)
+        every = getattr(progress, "every", 0) if progress is not None else 0
+        prev = 0.0
         for i in range(nfull):
             run(i * B, B)
+            if every and ((i + 1) % every == 0 or i + 1 == nfull):
+                k = (i % every) + 1
+                cur = tr.read_metrics("eval").loss_sum
+                progress((cur - prev) / (k * B), k)
+                prev = cur
         m = tr.read_metrics("eval")
         r.full_sum, r.n_full = m.loss_sum, nfull
         if last:
@@ -124,6 +167,8 @@ class NativeEngine:
             m2 = tr.read_metrics("eval")
             r.last_sum, r.last_b = m2.loss_sum - m.loss_sum, last
             m = m2
+            if every:
+                progress(r.last_sum / last, 1)
         r.loss_sum, r.correct, r.count = m.loss_sum, m.correct, m.count
         return r
 
@@ -188,10 +233,11 @@ def run(cfg: TrainConfig, entry: str = "ddp_tutorial_cpu", show_banner: bool = F
         st = load_resume(cfg.resume)
         if st.get("model") != cfg.model:
             raise ValueError(f"resume file {cfg.resume} holds a {st.get('model')} model, not {cfg.model}")
-        engine.set_state(st["params"], st.get("momentum"))
+        engine.set_state(st["params"], st.get("momentum"), int(st.get("global_step", 0)))
         start = int(st["epoch"]) + 1
         if ctx.rank == 0:
             print(f"=> resumed from {cfg.resume} after epoch {st['epoch']}", flush=True)
+    timer = PhaseTimer(sync=engine.finish)
     idx = None
     for i in range(start, cfg.n_epochs):
         if idx is None:
@@ -199,15 +245,21 @@ def run(cfg: TrainConfig, entry: str = "ddp_tutorial_cpu", show_banner: bool = F
         nxt = None
         if i + 1 < cfg.n_epochs:
             nxt = lambda e=i + 1: epoch_indices(len(ytr), ctx.world, ctx.rank, e, cfg.seed)  # noqa: E731
-        with range_(f"epoch{i}.train"):
-            tr = engine.train_epoch(idx, prefetch=nxt)
+        bar = ProgressBar.make(cfg, ctx.rank, len(idx), "training")
+        with range_(f"epoch{i}.train"), timer("train"):
+            tr = engine.train_epoch(idx, progress=bar, prefetch=nxt)
+        if bar is not None:
+            bar.close()
         idx = tr.next_indices
         if cfg.shard_eval and ctx.world > 1:
             tidx = torch.arange(ctx.rank, ntest, ctx.world)
         else:
             tidx = torch.arange(ntest)
-        with range_(f"epoch{i}.eval"):
-            ev = engine.evaluate(tidx)
+        bar = ProgressBar.make(cfg, ctx.rank, len(tidx), "validation")
+        with range_(f"epoch{i}.eval"), timer("eval"):
+            ev = engine.evaluate(tidx, progress=bar)
+        if bar is not None:
+            bar.close()
         check_finite(f"epoch {i} training loss", tr.loss_sum)
         train_loss = reference_epoch_loss(tr.full_sum, tr.n_full, cfg.batch_size, tr.last_sum, tr.last_b)
         val_loss = reference_epoch_loss(ev.full_sum, ev.n_full, cfg.batch_size, ev.last_sum, ev.last_b)
@@ -224,10 +276,12 @@ def run(cfg: TrainConfig, entry: str = "ddp_tutorial_cpu", show_banner: bool = F
                   f"val_loss={rec['val_loss_mean']:.4f} val_acc={rec['val_acc']:.4f} "
                   f"images/s={ips:,.0f} ({engine.name}, world={ctx.world})", flush=True)
         metrics.write(**rec)
+        if cfg.profile and ctx.rank == 0:
+            print("[rank0] phase seconds: " + ", ".join(f"{k}={v:.4f}" for k, v in timer.summary().items()), flush=True)
         if cfg.resume:
-            params, mom = engine.get_state()  # every rank holds the same replica
+            params, mom, gstep = engine.get_state()  # every rank holds the same replica
             if ctx.rank == 0:
-                save_resume(cfg.resume, params, mom, i, cfg.model, cfg.dtype)
+                save_resume(cfg.resume, params, mom, i, cfg.model, cfg.dtype, global_step=gstep)
     engine.finish()
     sd = engine.state_dict()
     if ctx.rank == 0 and cfg.save_path:

@@ -90,7 +90,7 @@ def build_c(force: bool = False, jobs: int = 8) -> Path:
 def build_io(force: bool = False) -> Path:
     src = CSRC / "io" / "mnist_io.cpp"
     cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-fvisibility=hidden"] + _pybind_includes()
-    obj = _compile(src, [], cmd, force)
+    obj = _compile(src, [CSRC / "io" / "formats.h"], cmd, force)
     out = PKG / f"_io{EXT}"
     tmp = out.with_name(out.name + ".tmp")
     _run(["g++", "-shared", "-fPIC", "-o", str(tmp), str(obj), "-lpthread"])

@@ -6,8 +6,10 @@ class keeps that surface on top of :func:`~pytorch_ddp_mnist_amd.parallel.comm.i
   ``get_size()`` / ``get_rank()``   world size / rank, 1 / 0 before initialisation (ref :15-27)
   ``get_local_rank()``              ``LOCAL_RANK`` env, else ``rank % device_count`` on GPUs, else
                                     -1 on CPU (ref :29-39; survey Q21 prefers the env variable)
-  ``reduceMAX(src)``                element-wise MAX over ranks of a numpy vector (ref :193-199,
-                                    MPI Reduce to rank 0); here an all-reduce so every rank gets it
+  ``reduceMAX(src, root=0)``        element-wise MAX over ranks of a vector as float64 (ref :193-199:
+                                    ``MPI.COMM_WORLD.Reduce(src, dst, op=MAX, root=root)``).  The
+                                    value on ``root`` is the reference's; the other ranks get the same
+                                    result instead of the reference's uninitialised ``numpy.empty``
   ``barrier()`` / ``finalize()``    ref :201-206 (never called upstream; here they work, Q16)
 
 No mpi4py: rank/size come from the launcher environment and the control plane is c10d gloo.
@@ -45,9 +47,12 @@ class distributed:  # noqa: N801  (reference class name)
         return distributed.get_rank() % n if n > 0 else -1
 
     @staticmethod
-    def reduceMAX(src) -> np.ndarray:  # noqa: N802  (reference method name)
-        a = np.asarray(src, dtype=np.float64)
-        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    def reduceMAX(src, root: int = 0) -> np.ndarray:  # noqa: N802  (reference method name and signature)
+        a = np.array(src, dtype=np.float64).reshape(-1)
+        world = distributed.get_size()
+        if not 0 <= int(root) < world:
+            raise ValueError(f"reduceMAX: root {root} outside [0, {world})")
+        if not (dist.is_available() and dist.is_initialized()) or world == 1:
             return a.copy()
         t = torch.from_numpy(a.copy())
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

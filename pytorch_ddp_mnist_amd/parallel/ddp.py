@@ -8,21 +8,30 @@ first bucket, so the reference does ONE 473,088-byte (MLP) all-reduce per step w
 (survey §2.7, CS5).
 
 MI355X design (GPU path, csrc/runtime/trainer.cpp): gradients are written by the kernels into
-ONE flat fp32 slab; a bucket is a contiguous range of it, launched on the comm stream as soon as
-the backward phase that produces it has been reduced.  :func:`plan_buckets` decides the ranges:
-for the small messages of these models the all-reduce is latency-bound on xGMI (7 point-to-point
-links, ~153 GB/s each — a 473 KB ring step is a few microseconds), so the plan is "as few buckets
-as possible, split only at phase boundaries where the remaining backward work can hide one":
-LeNet-5 gets two buckets (conv 10 KB, all-reduced while the FC weight gradient runs; FC head
-236.5 KB, exposed: see csrc/runtime/trainer.cpp for why the convolution backward goes first),
-the MLP one.  ``bucket_cap_kb`` forces further splits (A/B experiments).
+ONE flat fp32 slab; a bucket is a contiguous range of it.  :func:`plan_buckets` decides the ranges
+(one per backward phase by default: LeNet-5 FC head 236.5 KB | conv 10 KB, the MLP one 473 KB;
+``bucket_cap_kb`` forces further splits).  For messages this small the all-reduce is latency-bound
+on xGMI (7 point-to-point links, ~153 GB/s each: a 247 KB ring step is ~2 us of wire time), so
+WHEN the buckets go out matters more than how many there are.  Two step plans exist (trainer.h):
+
+  * ``join``  -- the FC and conv backward branches join, then ONE all-reduce of the coalesced
+    slab (one ring latency per step, fully exposed);
+  * ``split`` -- the FC buckets go out on the comm stream as soon as the FC grads are reduced,
+    beside conv_bwd (whose grid can be capped to leave whole CUs free for RCCL's kernels), and the
+    FC update runs on the aux stream; only the 10 KB conv bucket is exposed.
+
+Which one is faster depends on the xGMI latency at the actual world size and on whether RCCL's
+kernels find CU room beside conv_bwd, so it is not hard-coded: at start-up every candidate of
+:func:`default_plan_candidates` is timed on the real communicator (NativeTrainer.autotune_plan)
+and :func:`choose_plan` keeps the fastest, preferring ``join`` unless another plan wins by a
+margin (rank-max timings, so every rank decides the same).
 
 :class:`GlooReducer` is the same contract for the CPU path (plumbing / oracle): it broadcasts
 parameters at construction and all-reduces the flattened gradients in the same bucket plan.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -50,6 +59,31 @@ def plan_buckets(phases: Sequence[Tuple[int, int]], cap_bytes: Optional[int] = N
             out.append((s, e, ph))
             e = s
     return out
+
+
+def default_plan_candidates(default_grid: int, n_cu: int, reserve_cus=(16,)) -> Dict[str, Tuple[str, int]]:
+    """Candidate plans: name -> (plan, conv_bwd target workgroups; 0 = default one full round).
+
+    ``split_rN`` caps conv_bwd to the workgroups that fit on ``n_cu - N`` CUs at the default
+    workgroups-per-CU, so N CUs stay free for RCCL's kernels while conv_bwd runs.
+    """
+    out: Dict[str, Tuple[str, int]] = {"join": ("join", 0), "split": ("split", 0)}
+    per_cu = max(1, round(default_grid / max(1, n_cu)))
+    for r in reserve_cus:
+        if 0 < r < n_cu and default_grid >= n_cu:
+            out[f"split_r{r}"] = ("split", per_cu * (n_cu - r))
+    return out
+
+
+def choose_plan(timings_ms: Dict[str, float], prefer: str = "join", margin: float = 0.015) -> str:
+    """Fastest candidate, but keep ``prefer`` unless the winner beats it by more than ``margin``
+    (relative): the simpler schedule wins ties and timing noise."""
+    if not timings_ms:
+        raise ValueError("choose_plan: no timings")
+    best = min(timings_ms, key=lambda k: (timings_ms[k], k != prefer))
+    if prefer in timings_ms and timings_ms[best] > timings_ms[prefer] * (1.0 - margin):
+        return prefer
+    return best
 
 
 def model_phases(model: str) -> List[Tuple[int, int]]:

@@ -17,8 +17,9 @@ import signal
 import socket
 import subprocess
 import sys
+import threading
 import time
-from typing import List
+from typing import List, Optional, Tuple
 
 
 def free_port() -> int:
@@ -83,6 +84,72 @@ def launch(cmd: List[str], n: int, style: str = "pmi", timeout: float = 0.0) -> 
             except subprocess.TimeoutExpired:
                 os.killpg(p.pid, signal.SIGKILL)
     return rc
+
+
+def _pump(stream, sink, keep: Optional[list]) -> None:
+    for line in iter(stream.readline, ""):
+        if keep is not None:
+            keep.append(line)
+        sink.write(line)
+        sink.flush()
+    stream.close()
+
+
+def launch_relay(cmd: List[str], n: int, style: str = "torch", timeout: float = 0.0,
+                 relay_rank: int = 0, extra_env: Optional[dict] = None) -> Tuple[int, List[str]]:
+    """``launch`` for one-process-per-GPU jobs whose rank-``relay_rank`` stdout is the result.
+
+    That rank's stdout is forwarded to ours (and returned as a list of lines); every other
+    rank's stdout goes to our stderr, so exactly one rank can print to stdout.  The children
+    start before this process touches a GPU (it never does).  Exit code: the first non-zero
+    child code, 124 on timeout, else 0; the surviving children are killed on failure.
+    """
+    port = free_port()
+    procs, pumps, kept = [], [], []
+    for r in range(n):
+        env = child_env(style, r, n, port)
+        env["LOCAL_WORLD_SIZE"] = str(n)
+        env.update(extra_env or {})
+        p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, start_new_session=True)
+        procs.append(p)
+        th = threading.Thread(target=_pump, args=(p.stdout, sys.stdout if r == relay_rank else sys.stderr,
+                                                  kept if r == relay_rank else None), daemon=True)
+        th.start()
+        pumps.append(th)
+    t0 = time.time()
+    rc = 0
+    try:
+        while True:
+            alive = 0
+            for p in procs:
+                code = p.poll()
+                if code is None:
+                    alive += 1
+                elif code != 0 and rc == 0:
+                    rc = code
+            if rc != 0 or alive == 0:
+                break
+            if timeout and time.time() - t0 > timeout:
+                rc = 124
+                break
+            time.sleep(0.05)
+    finally:
+        if rc != 0:
+            for p in procs:
+                if p.poll() is None:
+                    try:
+                        os.killpg(p.pid, signal.SIGTERM)
+                    except ProcessLookupError:
+                        pass
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+        for th in pumps:
+            th.join(timeout=5)
+    return (rc if rc >= 0 else 128 - rc), kept
 
 
 def main(argv=None) -> int:

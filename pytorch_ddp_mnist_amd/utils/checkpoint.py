@@ -28,8 +28,11 @@ def load_model(path: str = "model.pt") -> Dict[str, torch.Tensor]:
 
 
 def save_resume(path: str, params: torch.Tensor, momentum: Optional[torch.Tensor], epoch: int,
-                model: str, dtype: str) -> str:
-    blob = {"params": params.detach().cpu(), "epoch": int(epoch), "model": model, "dtype": dtype}
+                model: str, dtype: str, global_step: int = 0) -> str:
+    """``global_step`` seeds the native dropout stream: restoring it keeps the masks of a resumed run
+    from replaying those of the first epochs."""
+    blob = {"params": params.detach().cpu(), "epoch": int(epoch), "model": model, "dtype": dtype,
+            "global_step": int(global_step)}
     if momentum is not None:
         blob["momentum"] = momentum.detach().cpu()
     tmp = path + ".tmp"

@@ -65,21 +65,46 @@ class MetricsWriter:
             self.f.close()
 
 
-class Progress:
-    """Minimal tqdm stand-in honouring DISABLE_TQDM (ddp_tutorial_cpu.py:9, unused upstream)."""
+class ProgressBar:
+    """Rank-0 per-batch progress (``--tqdm``): the reference's ``tqdm(loader)`` with
+    ``set_description(f'training batch_loss={:.4f}')`` / ``validation …`` (ddp_tutorial_multi_gpu.py:85,98,
+    104,114; ddp_tutorial_cpu.py:69,79,85,93).  The native engine accumulates the loss on the device,
+    so the bar is fed every ``every`` batches with the mean loss of that window (one device sync
+    per update instead of the reference's ``.item()`` per batch).  Uses tqdm when importable."""
 
-    def __init__(self, total: int, desc: str = "", disable: bool = True):
-        self.total, self.desc, self.disable = total, desc, disable
+    def __init__(self, total_batches: int, kind: str, every: int, out=sys.stderr):
+        self.kind, self.every, self.total = kind, max(1, every), total_batches
         self.n = 0
         self.t0 = time.perf_counter()
+        self.out = out
+        try:
+            from tqdm import tqdm
+            self.bar = tqdm(total=total_batches, file=out, leave=False, dynamic_ncols=True)
+        except ImportError:  # pragma: no cover - tqdm ships with the image
+            self.bar = None
+        self.last = None
 
-    def set_description(self, d: str) -> None:
-        self.desc = d
+    @classmethod
+    def make(cls, cfg, rank: int, n_samples: int, kind: str) -> Optional["ProgressBar"]:
+        if cfg.disable_tqdm or rank != 0:
+            return None
+        nb = -(-int(n_samples) // int(cfg.batch_size))
+        every = cfg.progress_every or max(1, nb // 20)
+        return cls(nb, kind, every)
 
-    def update(self, k: int = 1) -> None:
-        self.n += k
-        if not self.disable and (self.n == self.total or self.n % max(1, self.total // 20) == 0):
+    def __call__(self, batch_loss: float, n: int = 1) -> None:
+        self.n += n
+        self.last = float(batch_loss)
+        desc = f"{self.kind} batch_loss={self.last:.4f}"
+        if self.bar is not None:
+            self.bar.set_description(desc)
+            self.bar.update(n)
+        else:
             rate = self.n / max(1e-9, time.perf_counter() - self.t0)
-            print(f"\r{self.desc} {self.n}/{self.total} [{rate:.1f}it/s]", end="", file=sys.stderr, flush=True)
-            if self.n == self.total:
-                print(file=sys.stderr)
+            print(f"\r{desc} {self.n}/{self.total} [{rate:.1f}it/s]", end="", file=self.out, flush=True)
+
+    def close(self) -> None:
+        if self.bar is not None:
+            self.bar.close()
+        else:
+            print(file=self.out)

@@ -50,16 +50,20 @@ def range_(name: str):
 
 
 class PhaseTimer:
-    """Wall-clock per phase (host view; device phases need a synchronize to be meaningful)."""
+    """Wall-clock seconds per named phase (``--profile`` prints them per epoch).  ``sync`` (e.g. the
+    trainer's stream synchronize) runs before a phase's clock stops, so device work is included."""
 
-    def __init__(self):
+    def __init__(self, sync=None):
         self.t: Dict[str, List[float]] = defaultdict(list)
+        self.sync = sync
 
     @contextlib.contextmanager
     def __call__(self, name: str):
         t0 = time.perf_counter()
         with range_(name):
             yield
+            if self.sync is not None:
+                self.sync()
         self.t[name].append(time.perf_counter() - t0)
 
     def summary(self) -> Dict[str, float]:

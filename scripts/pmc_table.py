@@ -1,0 +1,97 @@
+"""Per-kernel hardware-counter table from the four passes of scripts/pmc_final.sh.
+
+    python scripts/pmc_table.py gpurun_out/pmcf [--batch 8192] > profiles/<tag>/pmc_table.md
+
+Columns: mean duration (counter runs, kernel-trace timestamps), VGPR/AGPR/LDS per workgroup,
+waves per SIMD the resources allow, MFMA-busy share of the kernel's SIMD-cycles, LDS bank-conflict
+share of LDS-active cycles, LDS-active share of the kernel's CU-cycles, wave cycles spent parked
+(s_waitcnt / barrier), achieved TFLOP/s (analytic FLOP per image, survey §2.6), and HBM-side
+GB/s from FETCH_SIZE (x2: gfx950 tallies 128-B requests at 64 B, MI355X_MICROARCH.md §HBM) and
+WRITE_SIZE.  Counter values are summed over the dispatch's instances and averaged over dispatches.
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import csv
+import os
+
+N_CU, SIMD, N_XCD = 256, 4, 8
+# GRBM_GUI_ACTIVE comes back summed over the 8 XCDs (x8 the kernel's cycles: 1.544e6 for a 78 us
+# conv_bwd at ~2.4 GHz); SQ_VALU_MFMA_BUSY_CYCLES is summed over all 1024 SIMDs (it equals the
+# kernel's MFMA count x 16 cycles of v_mfma_f32_16x16x32_bf16) and SQ_LDS_* over the 256 CUs.
+# analytic FLOP per image of each LeNet-5 kernel (2 x MACs), batch 8192 in the bench
+FLOP_PER_IMG = {
+    "conv_fwd": 2 * (6 * 784 * 25 + 16 * 100 * 150),
+    "head": 2 * 2 * (400 * 120 + 120 * 84 + 84 * 10),
+    "wgrad": 2 * (400 * 120 + 120 * 84 + 84 * 10),
+    "conv_bwd": 2 * (16 * 100 * 150 * 2 + 6 * 784 * 25),
+}
+
+
+def short(name: str) -> str:
+    for k in ("conv_fwd", "conv_bwd", "head_kernel", "wgrad", "reduce_sgd", "reduce_slabs", "sgd_pack"):
+        if k in name:
+            return k.replace("_kernel", "")
+    return name[:24]
+
+
+def load(path):
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    disp = collections.defaultdict(set)
+    meta, dur = {}, collections.defaultdict(dict)
+    for r in csv.DictReader(open(path)):
+        k = short(r["Kernel_Name"])
+        if k.startswith("void at::") or "rocclr" in k:
+            continue
+        did = r["Dispatch_Id"]
+        agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        disp[k].add(did)
+        meta[k] = (int(r["VGPR_Count"]), int(r["Accum_VGPR_Count"]), int(r["LDS_Block_Size"]),
+                   int(r["Workgroup_Size"]), int(r["Grid_Size"]))
+        dur[k][did] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    out = {}
+    for k in agg:
+        n = len(disp[k])
+        out[k] = ({c: v / n for c, v in agg[k].items()}, meta[k], sum(dur[k].values()) / len(dur[k]), n)
+    return out
+
+
+def waves_per_simd(vgpr, agpr, lds, wg):
+    regs = -(-(vgpr + agpr) // 8) * 8
+    by_reg = min(8, 512 // max(regs, 1))
+    waves_per_wg = max(1, wg // 64)
+    by_lds = (160 * 1024 // lds) * waves_per_wg / SIMD if lds else 8
+    return min(by_reg, by_lds)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("prefix", help="e.g. gpurun_out/pmcf (expects _a.._d run dirs)")
+    ap.add_argument("--batch", type=int, default=8192)
+    a = ap.parse_args()
+    P = {s: load(os.path.join(f"{a.prefix}_{s}", "run_counter_collection.csv")) for s in "abcd"}
+    print("| kernel | calls | us | VGPR/AGPR | LDS B/WG | waves/SIMD (res.) | MFMA busy % | LDS bank-conflict % "
+          "| LDS active % | WAIT_ANY % | TFLOP/s | HBM read GB/s | HBM write GB/s |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|---|")
+    for k in sorted(P["b"], key=lambda x: -P["b"][x][2]):
+        cb, (vg, ag, lds, wg, grid), t, n = P["b"][k]
+        ca = P["a"].get(k, ({}, None, t, 0))[0]
+        cc, _, tc, _ = P["c"].get(k, ({}, None, t, 0))
+        cd, _, td, _ = P["d"].get(k, ({}, None, t, 0))
+        cyc = cb.get("GRBM_GUI_ACTIVE", 0.0) / N_XCD
+        mfma = 100.0 * cb.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / max(1.0, cyc * N_CU * SIMD) if cyc else float("nan")
+        lds_act = 100.0 * cb.get("SQ_LDS_IDX_ACTIVE", 0.0) / max(1.0, cyc * N_CU) if cyc else float("nan")
+        lds_c = 100.0 * cb.get("SQ_LDS_BANK_CONFLICT", 0.0) / max(1.0, cb.get("SQ_LDS_IDX_ACTIVE", 0.0))
+        wait = 100.0 * ca.get("SQ_WAIT_ANY", 0.0) / max(1.0, ca.get("SQ_WAVE_CYCLES", 0.0))
+        fl = FLOP_PER_IMG.get(k)
+        tf = fl * a.batch / t / 1e12 if fl else float("nan")
+        rd = 2 * cc.get("FETCH_SIZE", 0.0) * 1024 / tc / 1e9 if tc else float("nan")
+        wr = cd.get("WRITE_SIZE", 0.0) * 1024 / td / 1e9 if td else float("nan")
+        occ = waves_per_simd(vg, ag, lds, wg)
+        print(f"| {k} | {n} | {t * 1e6:.1f} | {vg}/{ag} | {lds} | {occ:g} | {mfma:.1f} | {lds_c:.1f} | {lds_act:.0f} | {wait:.0f} | "
+              f"{tf:.1f} | {rd:.0f} | {wr:.0f} |")
+
+
+if __name__ == "__main__":
+    main()

@@ -19,7 +19,7 @@ def _worker(rank, world, port, q):
     from pytorch_ddp_mnist_amd.parallel import distributed
     assert distributed.get_size() == 1 and distributed.get_rank() == 0  # before init: fallbacks
     d = distributed("gloo", device="cpu")
-    out = (d.get_size(), d.get_rank(), d.reduceMAX(np.array([rank, -rank, 3.5])).tolist(), str(d.device))
+    out = (d.get_size(), d.get_rank(), d.reduceMAX(np.array([rank, -rank, 3.5]), 0).tolist(), str(d.device))
     d.barrier()
     d.finalize()
     q.put((rank, out))

@@ -23,16 +23,16 @@ def test_rccl_world1_collectives(native):
     s = torch.cuda.current_stream()
     comm.all_reduce_sum_f32(x.data_ptr(), x.numel(), s.cuda_stream)
     comm.broadcast_f32(x.data_ptr(), x.numel(), 0, s.cuda_stream)
-    comm.wait_stream(s.cuda_stream, 60.0)
+    assert comm.wait_stream(s.cuda_stream, 60.0) == ""
     assert torch.equal(x.cpu(), torch.arange(1000, dtype=torch.float32))
     assert comm.async_error() == ""
     assert (comm.rank, comm.world) == (0, 1)
 
 
-@pytest.mark.parametrize("overlap", [True, False])
+@pytest.mark.parametrize("plan", ["join", "split"])
 @pytest.mark.parametrize("model_name", ["mlp", "lenet5"])
-def test_rccl_inside_captured_step(native, small_mnist, model_name, overlap):
-    """The step graph with the RCCL bucket all-reduces captured on the side stream == eager without comm."""
+def test_rccl_inside_captured_step(native, small_mnist, model_name, plan):
+    """The step graph with the RCCL bucket all-reduces captured (main or comm stream) == eager without comm."""
     from pytorch_ddp_mnist_amd.engine.native import NativeTrainer
     from pytorch_ddp_mnist_amd.models import build_model
     x, y, _, _ = small_mnist
@@ -44,7 +44,7 @@ def test_rccl_inside_captured_step(native, small_mnist, model_name, overlap):
         tr = NativeTrainer(model_name, "bf16", 128, torch.from_numpy(x.reshape(-1, 784)), torch.from_numpy(y),
                            dropout=0.0, init=m)
         if with_comm:
-            tr.attach_comm(native.RcclComm(native.RcclComm.make_unique_id(), 0, 1, 0), 1, overlap=overlap)
+            tr.attach_comm(native.RcclComm(native.RcclComm.make_unique_id(), 0, 1, 0), 1, plan=plan)
             tr.broadcast_params(0)
         tr.set_epoch_indices(idx)
         for _ in range(3):

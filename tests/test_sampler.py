@@ -3,7 +3,7 @@ import pytest
 import torch
 from torch.utils.data import DistributedSampler
 
-from pytorch_ddp_mnist_amd.data.sampler import ShardedSampler, batch_slices, epoch_indices, feistel_permutation, num_samples
+from pytorch_ddp_mnist_amd.data.sampler import ShardedSampler, batch_slices, epoch_indices, num_samples
 
 
 class _DS:
@@ -43,9 +43,3 @@ def test_batches_match_dataloader():
 def test_steps_per_epoch_table():  # survey §6
     for w, steps in ((1, 469), (2, 235), (4, 118), (8, 59)):
         assert len(batch_slices(num_samples(60000, w), 128)) == steps
-
-
-@pytest.mark.parametrize("n", [1, 2, 100, 60000, 65537])
-def test_feistel_is_a_bijection(n):
-    p = feistel_permutation(n, key=123)
-    assert sorted(p.tolist()) == list(range(n))

@@ -1,9 +1,12 @@
 """Step-schedule equivalence on one MI355X (csrc/runtime/trainer.cpp launch_step).
 
 The FC weight gradient runs on an aux stream beside conv_bwd (default) or after it
-(MNIST_AMD_CONCURRENT=0); with a communicator the two gradient reductions join into one whole-slab
-all-reduce (default) or the FC bucket goes out first (MNIST_AMD_MG_SCHED=split).  All of them
-reduce in the same fixed order, so the trained parameters must be bitwise identical.
+(MNIST_AMD_CONCURRENT=0); conv_bwd can run as two concurrent halves (MNIST_AMD_SPLIT_BWD=1); with a
+communicator the gradient exchange follows the JOIN plan (one coalesced all-reduce after the backward
+join) or the SPLIT plan (FC buckets on the comm stream beside conv_bwd, per-range updates).  All of
+them reduce in the same fixed order, so the trained parameters must be bitwise identical; a capped
+conv_bwd grid changes the summation order, so capped variants are compared among themselves.  The
+``_w2`` variants check the 1/W averaging of both plans against a local run at half the learning rate.
 """
 import os
 import re
@@ -16,18 +19,23 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _digest(env_extra, args):
+def _digests(env_extra, variants):
     env = dict(os.environ, PYTHONPATH=ROOT, **env_extra)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "sched_equiv.py")] + args, env=env,
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "sched_equiv.py")] + variants, env=env,
                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:]
-    return re.search(r"digest (\w+)", r.stdout).group(1)
+    return dict(re.findall(r"digest (\S+) (\w+)", r.stdout))
 
 
-@pytest.mark.timeout(900)  # five fresh interpreters (torch import + GPU init each)
+@pytest.mark.timeout(900)  # three fresh interpreters (torch import + GPU init each)
 def test_schedules_bitwise_equal(native):
-    ref = _digest({"MNIST_AMD_CONCURRENT": "0"}, [])
-    assert _digest({"MNIST_AMD_CONCURRENT": "1"}, []) == ref
-    assert _digest({"MNIST_AMD_CONCURRENT": "1", "MNIST_AMD_SPLIT_BWD": "1"}, []) == ref  # conv_bwd halves
-    assert _digest({"MNIST_AMD_CONCURRENT": "1"}, ["--comm"]) == ref
-    assert _digest({"MNIST_AMD_CONCURRENT": "1", "MNIST_AMD_MG_SCHED": "split"}, ["--comm"]) == ref
+    serial = _digests({"MNIST_AMD_CONCURRENT": "0"}, ["local", "local_halflr"])
+    d = _digests({"MNIST_AMD_CONCURRENT": "1"},
+                 ["local", "join", "split", "join_w2", "split_w2", "local_b480", "join_b480", "split_b480"])
+    halves = _digests({"MNIST_AMD_CONCURRENT": "1", "MNIST_AMD_SPLIT_BWD": "1"}, ["local", "split"])
+    ref = serial["local"]
+    for k in ("local", "join", "split"):
+        assert d[k] == ref, k
+    assert halves["local"] == ref and halves["split"] == ref
+    assert d["join_w2"] == serial["local_halflr"] and d["split_w2"] == serial["local_halflr"]
+    assert d["join_b480"] == d["local_b480"] and d["split_b480"] == d["local_b480"]
