@@ -29,6 +29,13 @@ namespace {
 
 using L = LenetModel;
 constexpr int K0P = L::Head::K0P;  // 416
+// pool1 activations / codes handed from conv_fwd to conv_bwd through HBM, channel-major with rows
+// padded 14 -> 16 (CHW16), the layout conv_bwd stages into LDS with 16-byte stores; channel pitches
+// padded so conv_fwd's per-lane epilogue stores hit distinct LDS banks (lane = channel fastest)
+constexpr int P1CP = 232;            // pool1 value channel pitch (elements), >= 14 * 16
+constexpr int P1IMG = 6 * P1CP;      // elements per image in cb.p1
+constexpr int M1CP = 240;            // pool1 code channel pitch (bytes), multiple of 16
+constexpr int M1IMG = 6 * M1CP;      // bytes per image in cb.m1
 
 template <typename T>
 DEV void zero_lds(T* p, int n) {  // p 16-byte aligned; 16-byte stores, scalar tail
@@ -59,9 +66,10 @@ struct FwdSmem {
   static constexpr int XP = 1048;  // plane pitch (32x32 + pad): 2-way worst-case conflicts (was 8-way at 1024)
   static constexpr int OFF_XS = 0;                                        // [8][XP] T
   static constexpr int XTAIL = 64;  // zeroed tail: conv1's all-zero kernel row kh' = 7 reads 1 row past plane 7
-  static constexpr int OFF_P1 = rup((8 * XP + XTAIL) * (int)sizeof(T), 16);  // [196][8] T   pool1 output
-  static constexpr int OFF_M1 = rup(OFF_P1 + 196 * 8 * (int)sizeof(T), 16);  // [196][8] u8 pool1 codes
-  static constexpr int OFF_P2 = rup(OFF_M1 + 196 * 8, 16);                // [400] T      pool2 output (NCHW)
+  static constexpr int OFF_P1 = rup((8 * XP + XTAIL) * (int)sizeof(T), 16);  // [196][8] T   pool1 output (conv2 im2col)
+  static constexpr int OFF_P1C = rup(OFF_P1 + 196 * 8 * (int)sizeof(T), 16);  // [6][P1CP] T pool1, CHW16 (-> HBM)
+  static constexpr int OFF_M1 = rup(OFF_P1C + P1IMG * (int)sizeof(T), 16);    // [6][M1CP] u8 pool1 codes, CHW16
+  static constexpr int OFF_P2 = rup(OFF_M1 + M1IMG, 16);                  // [400] T      pool2 output (NCHW)
   static constexpr int OFF_M2 = rup(OFF_P2 + 400 * (int)sizeof(T), 16);   // [400] u8     pool2 codes
   static constexpr int W2P = 232;                                          // C2F row pitch (224 + 8)
   static constexpr int OFF_W2 = rup(OFF_M2 + 400, 16);                     // [16][W2P] T  conv2 B operand
@@ -83,6 +91,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   __shared__ __attribute__((aligned(16))) char smem[S::TOTAL];
   T* xs = reinterpret_cast<T*>(smem + S::OFF_XS);
   T* p1s = reinterpret_cast<T*>(smem + S::OFF_P1);
+  T* p1c = reinterpret_cast<T*>(smem + S::OFF_P1C);
   uint8_t* m1s = reinterpret_cast<uint8_t*>(smem + S::OFF_M1);
   T* p2s = reinterpret_cast<T*>(smem + S::OFF_P2);
   uint8_t* m2s = reinterpret_cast<uint8_t*>(smem + S::OFF_M2);
@@ -107,7 +116,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
     Raw r{{0u, 0u, 0u, 0u, 0u}};
     const int bb = blockIdx.x * ipb + t;
     if (tid >= 224 || t >= ipb || bb >= br.B) return r;
-    const uint8_t* rowp = br.images + (size_t)idx[bb] * 784 + (sy - 2) * 28;
+    const int im = idx[bb];
+    const uint8_t* rowp = br.images + (size_t)im * 784 + (sy - 2) * 28;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
       const int c = 8 * sg - 4 + 4 * k;
@@ -169,8 +179,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
       if (acc[i] > mx) { mx = acc[i]; am = i; }
     const float pre = mx + bias1;
     if (c1valid) {
-      p1s[pp * 8 + n] = to_t<T>(n < 6 ? fmaxf(pre, 0.f) : 0.f);
-      m1s[pp * 8 + n] = (n < 6) ? (uint8_t)(am | (pre > 0.f ? 4 : 0)) : 0;
+      const T v = to_t<T>(n < 6 ? fmaxf(pre, 0.f) : 0.f);
+      p1s[pp * 8 + n] = v;
+      if (TRAIN && n < 6) {
+        const int yx = (2 * t + (row >> 3)) * 16 + 4 * w + grp;  // CHW16 position
+        p1c[n * P1CP + yx] = v;
+        m1s[n * M1CP + yx] = (uint8_t)(am | (pre > 0.f ? 4 : 0));
+      }
     }
   };
   auto c2_acc = [&](int mt, f32x4& acc) {
@@ -208,6 +223,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   };
 
   zero_lds<T>(xs, 8 * S::XP + S::XTAIL);
+  if (TRAIN) {
+    zero_lds<T>(p1c, P1IMG);
+    zero_lds<uint8_t>(m1s, M1IMG);
+  }
   __syncthreads();
   stamp(1);
   for (int t = 0; t < ipb; ++t) {
@@ -295,8 +314,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
 
     // ---- pool1 -> HBM for the backward pass (16-byte stores), overlapped with conv2
     if (TRAIN && valid && !(cb.ablate & 1024)) {
-      copy_out16(reinterpret_cast<T*>(cb.p1) + (size_t)b * 196 * 8, p1s, 196 * 8 * (int)sizeof(T));
-      copy_out16(cb.m1 + (size_t)b * 196 * 8, m1s, 196 * 8);
+      copy_out16(reinterpret_cast<T*>(cb.p1) + (size_t)b * P1IMG, p1c, P1IMG * (int)sizeof(T));
+      copy_out16(cb.m1 + (size_t)b * M1IMG, m1s, M1IMG);
     }
     // ---- conv2 + bias + ReLU + maxpool: 100 rows (25 pooled x 4) = 7 M-tiles, N = 16
     if (!(cb.ablate & 4)) {
@@ -343,7 +362,9 @@ struct BwdSmem {
   // pitches padded so the fragment reads and the un-pooling scatters are <= 2-way bank
   // conflicted (measured 60% conflict cycles with the unpadded 1024/224/160/896 pitches)
   // W2R: conv2 dgrad B operand for TWO output rows per tile, [16 = (r, c)][30 taps x 16 ch + pad]
-  static constexpr int W2P = 488, XP = 1048, P1P = 240, D2P = 176, D1P = 912;
+  // (pitches from scripts/lds_model.py, a bank model of every LDS access of this kernel that matches
+  //  the measured SQ_LDS_BANK_CONFLICT share: 38.5 % modelled vs 38.9 % measured at 488/1048/240/176/912)
+  static constexpr int W2P = 496, XP = 1040, P1P = 240, D2P = 168, D1P = 920;
   // XS has 7 planes (5 shifted copies + an all-zero + an all-ones plane) and P1T 32 (30 + zero +
   // ones): padding / bias-gradient columns read a constant plane instead of branching per lane
   static constexpr int XPL = 7, PPL = 32;
@@ -353,8 +374,8 @@ struct BwdSmem {
   static constexpr int OFF_DYS = rup(OFF_DY2T + (HW ? 16 * D2P * (int)sizeof(T) : 0), 16);  // [18][18][16] zero-padded
   static constexpr int OFF_W2 = rup(OFF_DYS + (HD ? 18 * 18 * 16 * (int)sizeof(T) : 0), 16);
   static constexpr int OFF_DY1T = rup(OFF_W2 + (HD ? 16 * W2P * (int)sizeof(T) : 0), 16);
-  static constexpr int OFF_M1 = rup(OFF_DY1T + (HD ? 8 * D1P * (int)sizeof(T) : 0), 16);  // [6][14][16] u8 pool1 codes
-  static constexpr int TOTAL = rup(OFF_M1 + (HD ? 6 * 14 * 16 : 0), 16);
+  static constexpr int OFF_M1 = rup(OFF_DY1T + (HD ? 8 * D1P * (int)sizeof(T) : 0), 16);  // [6][M1CP] u8 pool1 codes
+  static constexpr int TOTAL = rup(OFF_M1 + (HD ? M1IMG : 0), 16);
   static constexpr int OFF_RED = OFF_XS;  // [4][2][256] f32 scratch after the image loop (dgrad side)
   static_assert(!HD || 4 * 2 * 256 * 4 <= XPL * XP * (int)sizeof(T), "reduction scratch must fit in the aliased XS region");
 };
@@ -389,28 +410,47 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
 
   // ---- software pipeline: every global input of image t+1 is loaded into registers while
   //      image t computes (phases B and C), so phase A only moves registers into LDS
+  // Phase-A thread roles (every LDS image is written with 16-byte stores, source rows prefetched):
+  //   tid [0, 112)   : input row y = tid/4, column chunk g = tid%4 -> its chunk of the 5 shifted XS planes
+  //   tid [112, 202) : 16-byte chunk tid-112 of the CHW16 pool1 codes -> M1
+  //   tid [128, 212) : pool1 channel c, row y ((tid-128) = c*14 + y) -> its row of the 5 shifted P1T planes
+  constexpr int PV = 16 * (int)sizeof(T) / 16;  // uint4 per CHW16 pool1 row (2 bf16 / 4 f32)
   struct Pre {
-    uint32_t u;       // 4 pixels
-    uint4 p[2];       // pool1 position (8 channels of T)
-    uint2 m;          // pool1 codes
+    uint32_t u[4];    // input pixels, image columns [8g-4, 8g+12) of row y-2
+    uint4 p[PV];      // pool1 row (16 positions of one channel)
+    uint4 m;          // 16 pool1 codes
     uint32_t c[2];    // pool2 codes for scatter items tid, tid + 256
     float g[2];       // pool2 grads
   };
   auto fetch = [&](int t) -> Pre {
     Pre f;
-    f.u = 0; f.p[0] = f.p[1] = make_uint4(0, 0, 0, 0); f.m = make_uint2(0, 0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) f.u[k] = 0;
+#pragma unroll
+    for (int k = 0; k < PV; ++k) f.p[k] = make_uint4(0, 0, 0, 0);
+    f.m = make_uint4(0, 0, 0, 0);
     f.c[0] = f.c[1] = 0; f.g[0] = f.g[1] = 0.f;
     const int bb = blockIdx.x * ipb + t;
     if (t >= ipb || bb >= br.B) return f;
-    if (tid < 196) {
-      if constexpr (HD) {
-        f.u = *reinterpret_cast<const uint32_t*>(br.images + (size_t)idx[bb] * 784 + tid * 4);
-        f.m = *reinterpret_cast<const uint2*>(cb.m1 + ((size_t)bb * 196 + tid) * 8);
+    if constexpr (HD) {
+      const int im = idx[bb];
+      if (tid < 112) {
+        const uint8_t* rowp = br.images + (size_t)im * 784 + (tid >> 2) * 28;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int col = 8 * (tid & 3) - 4 + 4 * k;
+          if (col >= 0 && col < 28) f.u[k] = *reinterpret_cast<const uint32_t*>(rowp + col);
+        }
       }
-      if constexpr (HW) {
-        const uint4* ps = reinterpret_cast<const uint4*>(p1g + ((size_t)bb * 196 + tid) * 8);
-        f.p[0] = ps[0];
-        if constexpr (sizeof(T) == 4) f.p[1] = ps[1];
+      if (tid >= 112 && tid < 112 + M1IMG / 16)
+        f.m = reinterpret_cast<const uint4*>(cb.m1 + (size_t)bb * M1IMG)[tid - 112];
+    }
+    if constexpr (HW) {
+      if (tid >= 128 && tid < 128 + 84) {
+        const int i = tid - 128, c = i / 14, y = i - 14 * c;
+        const uint4* ps = reinterpret_cast<const uint4*>(p1g + (size_t)bb * P1IMG + c * P1CP + y * 16);
+#pragma unroll
+        for (int k = 0; k < PV; ++k) f.p[k] = ps[k];
       }
     }
 #pragma unroll
@@ -461,19 +501,18 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     }
   }
   // ---- static work split of phase B (dgrad row-pair tile = 15 K-chunks, wgrad tile = 5):
-  //      dgrad pairs {2,2,2,1}, wgrad tiles {3,3,3,4}  ->  45/45/45/35 chunks per wave
+  //      dgrad pairs {2,2,2,1}, wgrad tiles {2,2,3,3}  ->  40/40/45/30 MFMAs per wave
   const int np = w < 3 ? 2 : 1, q0 = 2 * w;              // dgrad row pairs [q0, q0 + np)
-  const int nw = w < 3 ? 3 : 4, n0w = 3 * w;
-  constexpr int NWT = 4;  // wgrad accumulators per wave
+  const int nw = w < 2 ? 2 : 3, n0w = w < 2 ? 2 * w : 4 + 3 * (w - 2);
+  constexpr int NWT = 3;  // wgrad accumulators per wave
   // ---- per-lane operand offsets (loop invariant)
-  int w2off[NWT];   // conv2 wgrad B: this wave's output tiles (kcol = tap*8 + c; 200 = bias)
-  int w2sel[NWT];   // 0 data, 1 ones (bias), 2 zero
+  // conv2 wgrad B: DENSE columns kcol = tap*6 + c (150 weights) + 1 bias column = 10 tiles of 16
+  // (was tap*8 + c: 13 tiles, a quarter of them zero channels 6, 7)
+  int w2off[NWT];
 #pragma unroll
   for (int i = 0; i < NWT; ++i) {
-    const int kcol = (n0w + i) * 16 + row, tap = kcol >> 3, c = kcol & 7;
-    w2sel[i] = (kcol < 200 && c < 6) ? 0 : (kcol == 200 ? 1 : 2);
-    w2off[i] = w2sel[i] == 0 ? ((tap % 5) * 6 + c) * S::P1P + (tap / 5) * 16 : (w2sel[i] == 1 ? 31 : 30) * S::P1P;
-    if (i >= nw) w2off[i] = 30 * S::P1P;  // unused tile of this wave: zero plane
+    const int kcol = (n0w + i) * 16 + row, tap = kcol / 6, c = kcol - 6 * tap;
+    w2off[i] = kcol < 150 ? ((tap % 5) * 6 + c) * S::P1P + (tap / 5) * 16 : (kcol == 150 ? 31 : 30) * S::P1P;
   }
   int w1off[2], w1sel[2];  // conv1 wgrad B: tiles over kcol = tap (25 = bias)
 #pragma unroll
@@ -509,35 +548,84 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     nxt = fetch(t + 1);
     // ---- phase A: stage input (5 shifted copies), pool1 (5 shifted channel-major copies),
     //      pool1 codes, and the pool2 un-pooling scatter into DYS / DY2T
-    if (HD && tid < 196 && !(cb.ablate & 8)) {
-      const uint32_t u = cur.u;
-      const int k = tid * 4, y = k / 28 + 2, x = k % 28 + 2;
+    if (HD && tid < 112 && !(cb.ablate & 8)) {
+      // XS: planes kw = 0..4 of row y, columns [8g, 8g+8): xs[kw][y][x] = xpad[y][x + kw] = w[kw + 2 + j]
+      // with w[i] = normalised pixel at image column 8g - 4 + i (0 outside the image)
+      const int y = 2 + (tid >> 2), g = tid & 3;
+      float wv[16];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const T v = to_t<T>(valid ? mnist_norm((u >> (8 * j)) & 255u) : 0.f);
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t byte = (cur.u[i >> 2] >> (8 * (i & 3))) & 255u;
+        const bool in = valid && (unsigned)(8 * g - 4 + i) < 28u;
+        wv[i] = in ? mnist_norm(byte) : 0.f;
+      }
+      T* dst = xs + y * 32 + 8 * g;
+      if constexpr (sizeof(T) == 2) {
+        uint32_t D[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          bf16x2 pr;
+          pr[0] = (bf16)wv[2 * k];
+          pr[1] = (bf16)wv[2 * k + 1];
+          D[k] = __builtin_bit_cast(uint32_t, pr);
+        }
 #pragma unroll
         for (int kw = 0; kw < 5; ++kw) {
-          const int xx = x + j - kw;
-          if (xx >= 0) xs[kw * S::XP + y * 32 + xx] = v;
+          const int m = (kw + 2) >> 1;
+          uint4 o;
+          uint32_t* ov = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            ov[j] = (kw & 1) ? __builtin_amdgcn_alignbyte(D[m + j + 1], D[m + j], 2) : D[m + j];
+          *reinterpret_cast<uint4*>(dst + kw * S::XP) = o;
+        }
+      } else {
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) {
+          float* d = reinterpret_cast<float*>(dst + kw * S::XP);
+          *reinterpret_cast<f32x4*>(d) = f32x4{wv[kw + 2], wv[kw + 3], wv[kw + 4], wv[kw + 5]};
+          *reinterpret_cast<f32x4*>(d + 4) = f32x4{wv[kw + 6], wv[kw + 7], wv[kw + 8], wv[kw + 9]};
         }
       }
-      const int cy = tid / 14, cx = tid % 14;
-      const uint32_t mm[2] = {cur.m.x, cur.m.y};
-#pragma unroll
-      for (int c = 0; c < 6; ++c) m1s[(c * 14 + cy) * 16 + cx] = (uint8_t)(mm[c >> 2] >> (8 * (c & 3)));
     }
-    if (HW && tid < 196 && !(cb.ablate & 8)) {
-      // pool1 position tid: 8 channels
-      T pv[8];
-      *reinterpret_cast<uint4*>(pv) = cur.p[0];
-      if constexpr (sizeof(T) == 4) *reinterpret_cast<uint4*>(pv + 4) = cur.p[1];
-      const int py = tid / 14, px = tid % 14;
+    if (HD && tid >= 112 && tid < 112 + M1IMG / 16 && !(cb.ablate & 8))
+      reinterpret_cast<uint4*>(m1s)[tid - 112] = cur.m;
+    if (HW && tid >= 128 && tid < 128 + 84 && !(cb.ablate & 8)) {
+      // P1T: row y of planes (kw, c), kw = 0..4: p1t[kw*6+c][y][x] = pool1[y][x + kw][c], 0 for x + kw >= 14
+      const int i = tid - 128, c = i / 14, y = i - 14 * c;
+      T pv[16];
 #pragma unroll
-      for (int kw = 0; kw < 5; ++kw) {
-        const int xx = px - kw;
-        if (xx >= 0 && !(cb.ablate & 16)) {
+      for (int k = 0; k < PV; ++k) *reinterpret_cast<uint4*>(pv + k * (16 / (int)sizeof(T))) = cur.p[k];
+      T* dst = p1t + c * S::P1P + y * 16;
+      if constexpr (sizeof(T) == 2) {
+        uint32_t D[10];
 #pragma unroll
-          for (int c = 0; c < 6; ++c) p1t[(kw * 6 + c) * S::P1P + py * 16 + xx] = pv[c];
+        for (int k = 0; k < 7; ++k) D[k] = reinterpret_cast<const uint32_t*>(pv)[k];
+        D[7] = D[8] = D[9] = 0u;  // x = 14, 15 of the CHW16 row are padding
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) {
+          const int m = kw >> 1;
+          uint32_t o[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = (kw & 1) ? __builtin_amdgcn_alignbyte(D[m + j + 1], D[m + j], 2) : D[m + j];
+          T* d = dst + kw * 6 * S::P1P;
+          *reinterpret_cast<uint4*>(d) = make_uint4(o[0], o[1], o[2], o[3]);
+          *reinterpret_cast<uint4*>(d + 8) = make_uint4(o[4], o[5], o[6], o[7]);
+        }
+      } else {
+#pragma unroll
+        for (int kw = 0; kw < 5; ++kw) {
+          float* d = reinterpret_cast<float*>(dst + kw * 6 * S::P1P);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            f32x4 o;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int xx = 4 * q + j + kw;
+              o[j] = xx < 14 ? to_f(pv[xx]) : 0.f;
+            }
+            *reinterpret_cast<f32x4*>(d + 4 * q) = o;
+          }
         }
       }
     }
@@ -563,10 +651,10 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     for (int kc = 0; kc < ((!HW || (cb.ablate & 64)) ? 0 : W2CH); ++kc) {
       const int p0 = kc * KC + grp * KV, oh = p0 >> 4, ow0 = p0 & 15;
       const Frag a = M::load(dy2t + row * S::D2P + p0);
-      // unconditional loads + MFMAs (unused tiles read the zero plane): a lane-divergent branch
-      // around an MFMA on a loop-carried accumulator makes hipcc shuttle it VGPR<->AGPR every chunk
+      // the tile count is wave-uniform (w comes from readfirstlane), so the third tile is a scalar branch
 #pragma unroll
-      for (int i = 0; i < NWT; ++i) M::mma(accW2[i], a, M::load(p1t + w2off[i] + oh * 16 + ow0));
+      for (int i = 0; i < NWT; ++i)
+        if (i < nw) M::mma(accW2[i], a, M::load(p1t + w2off[i] + oh * 16 + ow0));
     }
 
     // ---- phase B2: conv2 dgrad, one tile = image rows (y, y+1) x 16 columns x (r, c):
@@ -578,7 +666,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
       auto dgrad_tile_epi = [&](int y, const f32x4& acc) {
         const int c = row & 7, Y = y + (row >> 3);
         if (c < 6) {
-          const uint32_t codes = *reinterpret_cast<const uint32_t*>(m1s + (c * 14 + Y) * 16 + grp * 4);
+          const uint32_t codes = *reinterpret_cast<const uint32_t*>(m1s + c * M1CP + Y * 16 + grp * 4);
           T r0[8], r1[8];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -651,16 +739,12 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
 #pragma unroll
   for (int i = 0; i < NWT; ++i) {
     if (!HW || i >= nw) break;
-    const int kcol = (n0w + i) * 16 + row;
+    const int kcol = (n0w + i) * 16 + row, tap = kcol / 6, c = kcol - 6 * tap;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = grp * 4 + r;
-      if (kcol < 200) {
-        const int tap = kcol >> 3, c = kcol & 7;
-        if (c < 6) out[L::CW2 + n * 150 + c * 25 + tap] = accW2[i][r];
-      } else if (kcol == 200) {
-        out[L::CB2 + n] = accW2[i][r];
-      }
+      if (kcol < 150) out[L::CW2 + n * 150 + c * 25 + tap] = accW2[i][r];
+      else if (kcol == 150) out[L::CB2 + n] = accW2[i][r];
     }
   }
   if constexpr (HD) {

@@ -59,6 +59,7 @@ class TrainConfig:
     shard_eval: bool = False
     progress_every: int = 0     # --tqdm update period in batches (0 = ~20 updates per epoch)
     plan: str = "auto"          # multi-GPU step plan: "auto" (timed at start-up) | "join" | "split"
+    io_mode: str = "bulk"       # netCDF: "bulk" (one pread per variable) | "per_sample" (reference __getitem__ reads)
     resume: Optional[str] = None  # params + momentum + epoch file: loaded if present, rewritten each epoch
 
     def to_nested(self) -> dict:
@@ -108,13 +109,16 @@ def _add_extra_flags(p: argparse.ArgumentParser, defaults: TrainConfig) -> None:
     add("--shard_eval", action="store_true", help="shard the test set across ranks (reference: every rank evaluates all)")
     add("--plan", type=str, default=None, choices=["auto", "join", "split"],
         help="multi-GPU step plan (auto: time the candidates on the communicator at start-up)")
+    add("--io_mode", type=str, default=None, choices=["bulk", "per_sample"],
+        help="netCDF input: bulk pread (default) or the reference's per-sample __getitem__ reads, timed (MB/s)")
     add("--resume", type=str, default=None,
         help="resume file (params + momentum + epoch): loaded when it exists, rewritten after every epoch")
 
 
 def _apply_extra(cfg: TrainConfig, a: argparse.Namespace) -> None:
     for name in ("model", "dtype", "lr", "momentum", "dropout", "seed", "init_seed", "data_format",
-                 "device", "bucket_cap_kb", "comm", "save_path", "metrics_jsonl", "plan", "resume", "progress_every"):
+                 "device", "bucket_cap_kb", "comm", "save_path", "metrics_jsonl", "plan", "resume", "progress_every",
+                 "io_mode"):
         v = getattr(a, name, None)
         if v is not None:
             setattr(cfg, name, v)

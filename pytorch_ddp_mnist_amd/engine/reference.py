@@ -58,7 +58,7 @@ class TorchCPUEngine:
         self.module = init if init is not None else build_model(model)
         if model == "mlp":
             self.module[2].p = dropout
-        shape = (-1, 784) if model == "mlp" else (-1, 1, 28, 28)
+        shape = self.shape = (-1, 784) if model == "mlp" else (-1, 1, 28, 28)
         self.x = normalize_batch(torch.from_numpy(np.ascontiguousarray(xtr))).reshape(shape)
         self.y = torch.from_numpy(ytr.astype(np.int64))
         self.xt = normalize_batch(torch.from_numpy(np.ascontiguousarray(xte))).reshape(shape)
@@ -69,6 +69,15 @@ class TorchCPUEngine:
         self.crit = F.nll_loss if model == "lenet5" else F.cross_entropy
         self.fault = FaultInjector(int(os.environ.get("RANK", "0")))
         self.global_step = 0
+
+    def load_train_arrays(self, x: np.ndarray, y: np.ndarray) -> None:
+        """Per-sample I/O mode: this epoch's rows (sampler order) become the resident training data."""
+        self.x = normalize_batch(torch.from_numpy(np.ascontiguousarray(x))).reshape(self.shape)
+        self.y = torch.from_numpy(y.astype(np.int64))
+
+    def load_test_arrays(self, x: np.ndarray, y: np.ndarray) -> None:
+        self.xt = normalize_batch(torch.from_numpy(np.ascontiguousarray(x))).reshape(self.shape)
+        self.yt = torch.from_numpy(y.astype(np.int64))
 
     def train_epoch(self, indices: torch.Tensor, progress=None, prefetch=None) -> EpochResult:
         r = EpochResult()

@@ -15,7 +15,9 @@ import numpy as np
 import torch
 
 from ..config import TrainConfig
-from ..data.datasets import load_arrays
+from ..data.datasets import find_netcdf, load_arrays, synthesize_netcdf
+from ..data.device_loader import upload_netcdf
+from ..data.per_sample import PerSampleReader
 from ..data.sampler import epoch_indices
 from ..models import build_model
 from ..parallel.comm import DistContext, init_distributed
@@ -35,8 +37,13 @@ class NativeEngine:
         from ..data.device_loader import upload_arrays
         from .native import NativeTrainer
         dev = ctx.device
-        images, labels = upload_arrays(xtr, ytr, dev)
-        self.test_images, self.test_labels = upload_arrays(xte, yte, dev)
+
+        def on_device(x, y):  # numpy arrays are staged (pinned -> async copy); device tensors used as is
+            if isinstance(x, torch.Tensor) and x.device.type == "cuda":
+                return x.view(-1, 784), y.view(-1)
+            return upload_arrays(x, y, dev)
+        images, labels = on_device(xtr, ytr)
+        self.test_images, self.test_labels = on_device(xte, yte)
         self.batch = cfg.batch_size
         self.cfg, self.ctx = cfg, ctx
         self.tr = NativeTrainer(cfg.model, cfg.dtype, cfg.batch_size, images, labels, device=dev, lr=cfg.lr,
@@ -57,6 +64,23 @@ class NativeEngine:
         self.plan_forced = None if cfg.plan == "auto" else cfg.plan
         self.tuned = self.tr.comm is None
         self.tune = None
+
+    def _load_rows(self, dst_x: torch.Tensor, dst_y: torch.Tensor, x: np.ndarray, y: np.ndarray) -> None:
+        """Per-sample I/O mode: this epoch's rows replace the resident data (stream-ordered after the
+        steps that read the previous contents)."""
+        n = len(y)
+        hx = torch.from_numpy(np.ascontiguousarray(x).reshape(n, 784)).pin_memory()
+        hy = torch.from_numpy(np.ascontiguousarray(y).reshape(n)).pin_memory()
+        with torch.cuda.stream(self.tr.stream):
+            dst_x[:n].copy_(hx, non_blocking=True)
+            dst_y[:n].copy_(hy, non_blocking=True)
+        self._staged = (hx, hy)  # alive until the copy has run (the epoch ends with a sync)
+
+    def load_train_arrays(self, x: np.ndarray, y: np.ndarray) -> None:
+        self._load_rows(self.tr.images, self.tr.labels, x, y)
+
+    def load_test_arrays(self, x: np.ndarray, y: np.ndarray) -> None:
+        self._load_rows(self.test_images, self.test_labels, x, y)
 
     def get_state(self):
         self.tr.synchronize()
@@ -210,14 +234,33 @@ def run(cfg: TrainConfig, entry: str = "ddp_tutorial_cpu", show_banner: bool = F
         ctx = init_distributed(method, parallel=parallel, device=cfg.device, comm=cfg.comm)
     fmt = _data_format(cfg, entry)
     root = cfg.data_path if cfg.data_path else ("." if fmt == "netcdf" else "./mnist_data")
+    if cfg.io_mode == "per_sample" and fmt != "netcdf":
+        raise ValueError("--io_mode per_sample is the netCDF read-cost experiment: use it with the netCDF format")
     if fmt == "netcdf" and ctx.rank == 0:
         print("=> Reading NetCDF File...")
     # rank 0 creates missing files first, the others wait, then every rank reads
-    if ctx.rank == 0:
-        xtr, ytr, xte, yte, src = load_arrays(fmt, root, cfg.data_limit, create=True, verbose=True)
-    ctx.barrier()
-    if ctx.rank != 0:
-        xtr, ytr, xte, yte, src = load_arrays(fmt, root, cfg.data_limit, create=False, verbose=False)
+    direct_nc = fmt == "netcdf" and ctx.device.type == "cuda" and cfg.io_mode == "bulk"
+    if fmt == "netcdf" and (direct_nc or cfg.io_mode == "per_sample"):
+        if ctx.rank == 0 and find_netcdf(root) is None:
+            synthesize_netcdf(root, verbose=True)
+        ctx.barrier()
+        paths = find_netcdf(root)
+        if cfg.io_mode == "per_sample":
+            readers = (PerSampleReader(root, True), PerSampleReader(root, False))
+            n_tr = len(readers[0]) if cfg.data_limit is None else min(len(readers[0]), int(cfg.data_limit))
+            xtr, ytr = np.zeros((n_tr, 28, 28), np.uint8), np.zeros(n_tr, np.uint8)
+            xte, yte = np.zeros((len(readers[1]), 28, 28), np.uint8), np.zeros(len(readers[1]), np.uint8)
+            src = f"netCDF CDF-5 ({paths['train']}), per-sample reads"
+        else:  # file -> pinned host memory (threaded pread) -> HBM, no intermediate numpy copy
+            xtr, ytr = upload_netcdf(paths["train"], ctx.device, cfg.data_limit)
+            xte, yte = upload_netcdf(paths["test"], ctx.device)
+            src = f"netCDF CDF-5 ({paths['train']}), pread -> pinned -> HBM"
+    else:
+        if ctx.rank == 0:
+            xtr, ytr, xte, yte, src = load_arrays(fmt, root, cfg.data_limit, create=True, verbose=True)
+        ctx.barrier()
+        if ctx.rank != 0:
+            xtr, ytr, xte, yte, src = load_arrays(fmt, root, cfg.data_limit, create=False, verbose=False)
     if fmt == "netcdf" and ctx.rank == 0:
         print("=> Dataset created, image nc file is : {}".format(os.path.join(root, "mnist_train_images.nc")))
     n_gpus = torch.cuda.device_count() if ctx.device.type == "cuda" else 0
@@ -245,9 +288,16 @@ def run(cfg: TrainConfig, entry: str = "ddp_tutorial_cpu", show_banner: bool = F
         nxt = None
         if i + 1 < cfg.n_epochs:
             nxt = lambda e=i + 1: epoch_indices(len(ytr), ctx.world, ctx.rank, e, cfg.seed)  # noqa: E731
-        bar = ProgressBar.make(cfg, ctx.rank, len(idx), "training")
+        io = {}
+        order = idx
+        if cfg.io_mode == "per_sample":  # read this epoch's samples one __getitem__ at a time
+            x_ep, y_ep, st = readers[0].read(idx)
+            engine.load_train_arrays(x_ep, y_ep)
+            order = torch.arange(len(y_ep))
+            io["train"] = st
+        bar = ProgressBar.make(cfg, ctx.rank, len(order), "training")
         with range_(f"epoch{i}.train"), timer("train"):
-            tr = engine.train_epoch(idx, progress=bar, prefetch=nxt)
+            tr = engine.train_epoch(order, progress=bar, prefetch=nxt)
         if bar is not None:
             bar.close()
         idx = tr.next_indices
@@ -255,6 +305,11 @@ def run(cfg: TrainConfig, entry: str = "ddp_tutorial_cpu", show_banner: bool = F
             tidx = torch.arange(ctx.rank, ntest, ctx.world)
         else:
             tidx = torch.arange(ntest)
+        if cfg.io_mode == "per_sample":
+            x_te, y_te, st = readers[1].read(tidx)
+            engine.load_test_arrays(x_te, y_te)
+            tidx = torch.arange(len(y_te))
+            io["test"] = st
         bar = ProgressBar.make(cfg, ctx.rank, len(tidx), "validation")
         with range_(f"epoch{i}.eval"), timer("eval"):
             ev = engine.evaluate(tidx, progress=bar)
@@ -270,6 +325,10 @@ def run(cfg: TrainConfig, entry: str = "ddp_tutorial_cpu", show_banner: bool = F
         rec = dict(epoch=i, train_loss_mean=g[0] / max(g[2], 1), train_acc=g[1] / max(g[2], 1),
                    val_loss_mean=g[3] / max(g[5], 1), val_acc=g[4] / max(g[5], 1), images_per_sec=ips,
                    epoch_seconds=secs, world=ctx.world, engine=engine.name)
+        for k, st in io.items():
+            rec[f"io_{k}_MBps"], rec[f"io_{k}_samples_per_s"] = st.mb_per_s, st.samples_per_s
+            if ctx.rank == 0:
+                print("[rank0] per-sample netCDF " + st.line(k), flush=True)
         history.append(rec)
         if ctx.rank == 0:
             print(f"[rank0] epoch={i} global_train_loss={rec['train_loss_mean']:.4f} train_acc={rec['train_acc']:.4f} "

@@ -76,3 +76,17 @@ def test_converter_notebook_runs(tmp_path, monkeypatch):
             exec("".join(cell["source"]).replace("os.path.abspath('.')", repr(ROOT)), g)
     assert g["x"].shape == (60000, 28, 28) and g["y"].shape == (60000,)
     assert (tmp_path / "mnist_test_images.nc").exists()
+
+
+def test_pnetcdf_per_sample_io_mode(tmp_path):
+    """--io_mode per_sample: every sample read through MNISTNetCDF.__getitem__ (2 reads each), timed;
+    same batches in the same order as the bulk read, so the epoch line is identical."""
+    _run([os.path.join(ROOT, "mnist_to_netcdf.py"), "--synthetic", "--output_dir", str(tmp_path)], tmp_path)
+    args = [os.path.join(ROOT, "mnist_pnetcdf_cpu.py"), "--data_limit", "1024", "--init_seed", "1", "--dropout", "0"]
+    bulk = _run(args, tmp_path)
+    per = _run(args + ["--io_mode", "per_sample"], tmp_path)
+    m = re.search(r"per-sample netCDF train: (\d+) samples, ([0-9.]+) MB in [0-9.]+ s = ([0-9.]+) MB/s", per)
+    assert m and int(m.group(1)) == 1024 and float(m.group(3)) > 0, per
+    assert "per-sample netCDF test: 10000 samples" in per
+    assert LINE.search(per).group(0) == LINE.search(bulk).group(0)
+    assert per.count("=> Dataset created, image nc file is") >= 2   # reference MNISTNetCDF prints, train + test
