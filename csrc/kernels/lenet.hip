@@ -44,20 +44,6 @@ DEV void zero_lds(T* p, int n) {  // p 16-byte aligned; 16-byte stores, scalar t
   for (int e = nv * 16 / (int)sizeof(T) + threadIdx.x; e < n; e += blockDim.x) p[e] = to_t<T>(0.f);
 }
 
-// The sample indices of a workgroup's images, loaded ONCE at kernel start: lane l of every wave holds
-// idx[first + l] and an image's index is read with v_readlane (no per-image global load; a per-image
-// scalar load put its latency -- and, through the shared lgkmcnt, every LDS wait behind it -- into
-// each image's staging phase).  Workgroups with more than 64 images fall back to plain loads.
-struct BlockIdx {
-  const int32_t* p;
-  int n, v;
-  DEV BlockIdx(const int32_t* idx, int first, int count, int B) : p(idx + first), n(count) {
-    const int l = threadIdx.x & 63;
-    v = (n <= 64 && l < n && first + l < B) ? p[l] : 0;
-  }
-  DEV int operator[](int t) const { return n <= 64 ? __builtin_amdgcn_readlane(v, t) : p[t]; }
-};
-
 // MFMA fragment of KV ones (bias-gradient column) / zeros
 template <typename T>
 DEV typename Mma<T>::Frag ones_frag() {
@@ -110,7 +96,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   T* p2s = reinterpret_cast<T*>(smem + S::OFF_P2);
   uint8_t* m2s = reinterpret_cast<uint8_t*>(smem + S::OFF_M2);
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
-  const BlockIdx bidx(br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride, blockIdx.x * ipb, ipb, br.B);
+  const int32_t* idx = br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride;
   const T* pack = reinterpret_cast<const T*>(cb.pack);
   const float* prm = cb.params;
   // optional wall-clock stamps (profiling): [0] start, [1] setup, 3 per image for images 0..3, [14] loop end
@@ -129,9 +115,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   auto fetch = [&](int t) -> Raw {  // software pipeline: image t+1's bytes are in flight during image t
     Raw r{{0u, 0u, 0u, 0u, 0u}};
     const int bb = blockIdx.x * ipb + t;
-    if (t >= ipb || bb >= br.B) return r;
-    const int im = bidx[t];  // wave-uniform readlane, before the lane-divergent exit below
-    if (tid >= 224) return r;
+    if (tid >= 224 || t >= ipb || bb >= br.B) return r;
+    const int im = idx[bb];
     const uint8_t* rowp = br.images + (size_t)im * 784 + (sy - 2) * 28;
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
@@ -412,7 +397,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   uint8_t* m1s = reinterpret_cast<uint8_t*>(smem + S::OFF_M1);
   float* red = reinterpret_cast<float*>(smem + S::OFF_RED);
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
-  const BlockIdx bidx(br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride, blockIdx.x * ipb, ipb, br.B);
+  const int32_t* idx = br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride;
   const T* pack = reinterpret_cast<const T*>(cb.pack);
   const T* dp2 = reinterpret_cast<const T*>(cb.dp2);
   const T* p1g = reinterpret_cast<const T*>(cb.p1);
@@ -448,7 +433,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     const int bb = blockIdx.x * ipb + t;
     if (t >= ipb || bb >= br.B) return f;
     if constexpr (HD) {
-      const int im = bidx[t];
+      const int im = idx[bb];
       if (tid < 112) {
         const uint8_t* rowp = br.images + (size_t)im * 784 + (tid >> 2) * 28;
 #pragma unroll
