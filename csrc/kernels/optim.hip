@@ -48,6 +48,27 @@ __device__ __forceinline__ float slab_partial(const float* __restrict__ slab, in
   return ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
 }
 
+// Slab counts up to DIRECT_MAX (the FC head's split-K slabs: 16 at B = 8192) are summed by ONE lane
+// per parameter: no LDS, no cross-wave step, so the kernel fits beside conv_bwd, whose two
+// workgroups per CU leave < 5 KB of LDS free (the LDS version of the FC update waited for CUs and
+// stretched from ~5 to ~48 us on the aux stream).  Every path (fused or not) uses the same tree for
+// a given slab count, so schedules stay bitwise equal.
+constexpr int DIRECT_MAX = 64;
+
+__device__ __forceinline__ float slab_sum_direct(const float* __restrict__ slab, int ld, int nslab, int p) {
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int k = 0;
+  for (; k + 8 <= nslab; k += 8) {
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = slab[(size_t)(k + i) * ld + p];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] += v[i];
+  }
+  for (; k < nslab; ++k) acc[0] += slab[(size_t)k * ld + p];
+  return 0.f + (((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7])));
+}
+
 // One block = 64 consecutive parameters (lane) x RNW waves splitting the slab rows; the per-wave
 // partial sums are combined in a fixed tree, so the result is bitwise reproducible.
 template <int NW>
@@ -68,6 +89,12 @@ __global__ __launch_bounds__(NW * 64) void reduce_slabs_kernel(const float* __re
     for (int i = 0; i < NW; ++i) t += part[i][lane];
     grad[p] = t * scale;
   }
+}
+
+__global__ __launch_bounds__(256) void reduce_direct_kernel(const float* __restrict__ slab, int ld, int nslab, int p0,
+                                                            int p1, float scale, float* __restrict__ grad) {
+  const int p = p0 + blockIdx.x * 256 + threadIdx.x;
+  if (p < p1) grad[p] = slab_sum_direct(slab, ld, nslab, p) * scale;
 }
 
 template <class Model, typename T>
@@ -113,7 +140,10 @@ __global__ __launch_bounds__(NW * 64) void reduce_sgd_kernel(const float* __rest
   float s = 0.f;
   if (p < n) {
     const bool a = p < split;
-    s = a ? slab_partial(slab_a, lda, na, p, w) : slab_partial(slab_b, ldb, nb, p, w);
+    const float* sl = a ? slab_a : slab_b;
+    const int ld = a ? lda : ldb, ns = a ? na : nb;
+    if (ns <= DIRECT_MAX) s = w == 0 ? slab_sum_direct(sl, ld, ns, p) : 0.f;  // same tree as the direct kernels
+    else s = slab_partial(sl, ld, ns, p, w);
   }
   part[w][lane] = s;
   __syncthreads();
@@ -138,12 +168,45 @@ __global__ __launch_bounds__(NW * 64) void reduce_sgd_kernel(const float* __rest
   }
 }
 
+// Fused reduce + SGD + pack of a parameter range whose slab count is <= DIRECT_MAX: no LDS.
+template <class Model, typename T>
+__global__ __launch_bounds__(256) void reduce_sgd_direct_kernel(const float* __restrict__ slab, int ld, int ns, int p0,
+                                                                int n, float scale, float* __restrict__ params,
+                                                                float* __restrict__ grad, float* __restrict__ mom,
+                                                                T* __restrict__ pack, float lr, float mu,
+                                                                int32_t* step_ptr) {
+  const int p = p0 + blockIdx.x * 256 + threadIdx.x;
+  if (p < n) {
+    float g = slab_sum_direct(slab, ld, ns, p) * scale;
+    grad[p] = g;
+    if (mom) {
+      const float b = mu * mom[p] + g;
+      mom[p] = b;
+      g = b;
+    }
+    const float v = params[p] - lr * g;
+    params[p] = v;
+    Packer<Model, T>::pack(p, v, pack);
+  }
+  if (step_ptr && blockIdx.x == 0 && threadIdx.x == 0) {
+    step_ptr[0] += 1;
+    step_ptr[1] += 1;
+  }
+}
+
 template <class Model, typename T>
 void reduce_sgd_t(const float* sa, int lda, int na, const float* sb, int ldb, int nb, int split, int p0, int n, float scale,
                   float* params, float* grad, float* mom, void* pack, float lr, float mu, int32_t* step_ptr,
                   hipStream_t s) {
+  if (n <= p0) return;
+  const bool only_b = p0 >= split, only_a = n <= split;
+  if ((only_b && nb <= DIRECT_MAX) || (only_a && na <= DIRECT_MAX)) {
+    hipLaunchKernelGGL((reduce_sgd_direct_kernel<Model, T>), dim3((n - p0 + 255) / 256), dim3(256), 0, s,
+                       only_b ? sb : sa, only_b ? ldb : lda, only_b ? nb : na, p0, n, scale, params, grad, mom,
+                       reinterpret_cast<T*>(pack), lr, mu, step_ptr);
+    return;
+  }
   const int grid = (n - p0 + 63) / 64;
-  if (grid <= 0) return;
   hipLaunchKernelGGL((reduce_sgd_kernel<Model, T, RNW>), dim3(grid), dim3(RNW * 64), 0, s, sa, lda, na, sb, ldb, nb, split,
                      p0, n, scale, params, grad, mom, reinterpret_cast<T*>(pack), lr, mu, step_ptr);
 }
@@ -177,6 +240,11 @@ __global__ __launch_bounds__(256) void gather_normalize_kernel(BatchRef br, T* o
 void launch_reduce(const float* slab, int slab_ld, int nslab, int p0, int p1, float scale, float* grad,
                    hipStream_t s) {
   if (p1 <= p0) return;
+  if (nslab <= DIRECT_MAX) {
+    hipLaunchKernelGGL(reduce_direct_kernel, dim3((p1 - p0 + 255) / 256), dim3(256), 0, s, slab, slab_ld, nslab, p0, p1,
+                       scale, grad);
+    return;
+  }
   const int grid = (p1 - p0 + 63) / 64;
   hipLaunchKernelGGL(reduce_slabs_kernel<RNW>, dim3(grid), dim3(RNW * 64), 0, s, slab, slab_ld, nslab, p0, p1, scale,
                      grad);
