@@ -44,6 +44,20 @@ DEV void zero_lds(T* p, int n) {  // p 16-byte aligned; 16-byte stores, scalar t
   for (int e = nv * 16 / (int)sizeof(T) + threadIdx.x; e < n; e += blockDim.x) p[e] = to_t<T>(0.f);
 }
 
+// The sample indices of a workgroup's images, loaded ONCE at kernel start: lane l of every wave holds
+// idx[first + l] and an image's index is read with v_readlane.  A per-image index load made the
+// image-row loads that depend on it wait (s_waitcnt vmcnt(0)) in the middle of every image.  The
+// launchers cap a workgroup at MAX_IPB = 64 images (one per lane).
+constexpr int MAX_IPB = 64;
+struct BlockIdx {
+  int v;
+  DEV BlockIdx(const int32_t* idx, int first, int count, int B) {
+    const int l = threadIdx.x & 63;
+    v = (l < count && first + l < B) ? idx[first + l] : 0;
+  }
+  DEV int operator[](int t) const { return __builtin_amdgcn_readlane(v, t); }
+};
+
 // MFMA fragment of KV ones (bias-gradient column) / zeros
 template <typename T>
 DEV typename Mma<T>::Frag ones_frag() {
@@ -96,7 +110,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   T* p2s = reinterpret_cast<T*>(smem + S::OFF_P2);
   uint8_t* m2s = reinterpret_cast<uint8_t*>(smem + S::OFF_M2);
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
-  const int32_t* idx = br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride;
+  const BlockIdx bidx(br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride, blockIdx.x * ipb, ipb, br.B);
   const T* pack = reinterpret_cast<const T*>(cb.pack);
   const float* prm = cb.params;
   // optional wall-clock stamps (profiling): [0] start, [1] setup, 3 per image for images 0..3, [14] loop end
@@ -112,17 +126,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   // ALIGNED 16-byte stores: xs[s][y][8g..8g+7] = xpad[y][8g+s..8g+s+7].  Rows 0,1,30,31 stay zero.
   struct Raw { uint32_t d[5]; };
   const int sy = 2 + (tid >> 3), sg = (tid >> 1) & 3, sh = tid & 1;
+  // Branch-free: every lane issues the same 5 loads, addresses clamped into the image; the words are
+  // kept raw (selecting on a loaded value right after the load made the wave wait for it).  Words
+  // loaded for out-of-image columns only feed pixels the stage masks (`in`), lanes >= 224 do not
+  // stage, and images past the batch are masked with `valid`.
   auto fetch = [&](int t) -> Raw {  // software pipeline: image t+1's bytes are in flight during image t
-    Raw r{{0u, 0u, 0u, 0u, 0u}};
-    const int bb = blockIdx.x * ipb + t;
-    if (tid >= 224 || t >= ipb || bb >= br.B) return r;
-    const int im = idx[bb];
-    const uint8_t* rowp = br.images + (size_t)im * 784 + (sy - 2) * 28;
+    Raw r;
+    const bool live = t < ipb && blockIdx.x * ipb + t < br.B;  // wave-uniform
+    const uint8_t* rowp = br.images + (size_t)bidx[live ? t : 0] * 784 + min(sy - 2, 27) * 28;
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
-      const int c = 8 * sg - 4 + 4 * k;
-      if (c >= 0 && c < 28) r.d[k] = *reinterpret_cast<const uint32_t*>(rowp + c);
-    }
+    for (int k = 0; k < 5; ++k) r.d[k] = *reinterpret_cast<const uint32_t*>(rowp + min(max(8 * sg - 4 + 4 * k, 0), 24));
     return r;
   };
   Raw u_next = fetch(0);  // issued before the setup below, so its latency overlaps it
@@ -233,8 +246,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
     const int b = blockIdx.x * ipb + t;
     const bool valid = b < br.B;
     const Raw u = u_next;
-    u_next = fetch(t + 1);
-    flush_p2(t > 0 ? b - 1 : -1);
     // ---- stage: normalise once, 4 aligned 16-byte plane stores per thread
     if (tid < 224 && !(cb.ablate & 1)) {
       float f[16];
@@ -286,6 +297,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
     }
     __syncthreads();
     if (t < 4) stamp(2 + 3 * t);
+    // next image's pixels (and the previous image's pool2 flush) are issued here, a whole conv1 +
+    // conv2 before their consumer, with no global operation in between
+    u_next = fetch(t + 1);
+    flush_p2(t > 0 ? b - 1 : -1);
 
     // ---- conv1 + bias + ReLU + maxpool: 7 two-row tiles per wave
     if (!(cb.ablate & 2)) {
@@ -397,7 +412,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   uint8_t* m1s = reinterpret_cast<uint8_t*>(smem + S::OFF_M1);
   float* red = reinterpret_cast<float*>(smem + S::OFF_RED);
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
-  const int32_t* idx = br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride;
+  const BlockIdx bidx(br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride, blockIdx.x * ipb, ipb, br.B);
   const T* pack = reinterpret_cast<const T*>(cb.pack);
   const T* dp2 = reinterpret_cast<const T*>(cb.dp2);
   const T* p1g = reinterpret_cast<const T*>(cb.p1);
@@ -420,47 +435,35 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     uint4 p[PV];      // pool1 row (16 positions of one channel)
     uint4 m;          // 16 pool1 codes
     uint32_t c[2];    // pool2 codes for scatter items tid, tid + 256
-    float g[2];       // pool2 grads
+    T g[2];           // pool2 grads (raw; converted where used, so no load result is needed at issue)
   };
+  // Branch-free: every lane issues the same loads (addresses clamped into range, values of lanes
+  // without the role / of images past the batch zeroed at use), so vmcnt accounting stays exact.
   auto fetch = [&](int t) -> Pre {
     Pre f;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) f.u[k] = 0;
-#pragma unroll
-    for (int k = 0; k < PV; ++k) f.p[k] = make_uint4(0, 0, 0, 0);
-    f.m = make_uint4(0, 0, 0, 0);
-    f.c[0] = f.c[1] = 0; f.g[0] = f.g[1] = 0.f;
-    const int bb = blockIdx.x * ipb + t;
-    if (t >= ipb || bb >= br.B) return f;
+    const bool live = t < ipb && blockIdx.x * ipb + t < br.B;  // wave-uniform
+    const int bb = min(blockIdx.x * ipb + t, br.B - 1);
     if constexpr (HD) {
-      const int im = idx[bb];
-      if (tid < 112) {
-        const uint8_t* rowp = br.images + (size_t)im * 784 + (tid >> 2) * 28;
+      const uint8_t* rowp = br.images + (size_t)bidx[live ? t : 0] * 784 + ((tid >> 2) % 28) * 28;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int col = 8 * (tid & 3) - 4 + 4 * k;
-          if (col >= 0 && col < 28) f.u[k] = *reinterpret_cast<const uint32_t*>(rowp + col);
-        }
+      for (int k = 0; k < 4; ++k) {
+        const int col = 8 * (tid & 3) - 4 + 4 * k;
+        f.u[k] = *reinterpret_cast<const uint32_t*>(rowp + min(max(col, 0), 24));
       }
-      if (tid >= 112 && tid < 112 + M1IMG / 16)
-        f.m = reinterpret_cast<const uint4*>(cb.m1 + (size_t)bb * M1IMG)[tid - 112];
+      f.m = reinterpret_cast<const uint4*>(cb.m1 + (size_t)bb * M1IMG)[min(max(tid - 112, 0), M1IMG / 16 - 1)];
     }
     if constexpr (HW) {
-      if (tid >= 128 && tid < 128 + 84) {
-        const int i = tid - 128, c = i / 14, y = i - 14 * c;
-        const uint4* ps = reinterpret_cast<const uint4*>(p1g + (size_t)bb * P1IMG + c * P1CP + y * 16);
+      const int i = min(max(tid - 128, 0), 83), c = i / 14, y = i - 14 * c;
+      const uint4* ps = reinterpret_cast<const uint4*>(p1g + (size_t)bb * P1IMG + c * P1CP + y * 16);
 #pragma unroll
-        for (int k = 0; k < PV; ++k) f.p[k] = ps[k];
-      }
+      for (int k = 0; k < PV; ++k) f.p[k] = ps[k];
     }
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
-      const int e = tid + 256 * r;
-      if (e < 400) {
-        const int n = e & 15, p = e >> 4;
-        f.c[r] = cb.m2[(size_t)bb * 400 + n * 25 + p];
-        f.g[r] = to_f(dp2[(size_t)bb * K0P + n * 25 + p]);
-      }
+      const int e = min(tid + 256 * r, 399);
+      const int n = e & 15, p = e >> 4;
+      f.c[r] = cb.m2[(size_t)bb * 400 + n * 25 + p];
+      f.g[r] = dp2[(size_t)bb * K0P + n * 25 + p];
     }
     return f;
   };
@@ -545,7 +548,6 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     const int b = blockIdx.x * ipb + t;
     const bool valid = b < br.B;
     const Pre cur = nxt;
-    nxt = fetch(t + 1);
     // ---- phase A: stage input (5 shifted copies), pool1 (5 shifted channel-major copies),
     //      pool1 codes, and the pool2 un-pooling scatter into DYS / DY2T
     if (HD && tid < 112 && !(cb.ablate & 8)) {
@@ -556,7 +558,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const uint32_t byte = (cur.u[i >> 2] >> (8 * (i & 3))) & 255u;
-        const bool in = valid && (unsigned)(8 * g - 4 + i) < 28u;
+        const bool in = valid && (unsigned)(8 * g - 4 + i) < 28u;  // also masks the clamped (duplicate) words
         wv[i] = in ? mnist_norm(byte) : 0.f;
       }
       T* dst = xs + y * 32 + 8 * g;
@@ -589,13 +591,14 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
       }
     }
     if (HD && tid >= 112 && tid < 112 + M1IMG / 16 && !(cb.ablate & 8))
-      reinterpret_cast<uint4*>(m1s)[tid - 112] = cur.m;
+      reinterpret_cast<uint4*>(m1s)[tid - 112] = valid ? cur.m : make_uint4(0, 0, 0, 0);
     if (HW && tid >= 128 && tid < 128 + 84 && !(cb.ablate & 8)) {
       // P1T: row y of planes (kw, c), kw = 0..4: p1t[kw*6+c][y][x] = pool1[y][x + kw][c], 0 for x + kw >= 14
       const int i = tid - 128, c = i / 14, y = i - 14 * c;
       T pv[16];
 #pragma unroll
-      for (int k = 0; k < PV; ++k) *reinterpret_cast<uint4*>(pv + k * (16 / (int)sizeof(T))) = cur.p[k];
+      for (int k = 0; k < PV; ++k)
+        *reinterpret_cast<uint4*>(pv + k * (16 / (int)sizeof(T))) = valid ? cur.p[k] : make_uint4(0, 0, 0, 0);
       T* dst = p1t + c * S::P1P + y * 16;
       if constexpr (sizeof(T) == 2) {
         uint32_t D[10];
@@ -634,8 +637,8 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
       const int e = tid + 256 * r;
       if (e >= 400 || (cb.ablate & 32)) break;
       const int n = e & 15, p = e >> 4, py = p / 5, px = p % 5;  // channel fastest: conflict-free DYS writes
-      const uint32_t code = cur.c[r];
-      const float g = cur.g[r];
+      const uint32_t code = valid ? cur.c[r] : 0u;  // code 0: ReLU blocked, every window gets 0
+      const float g = to_f(cur.g[r]);
 #pragma unroll
       for (int win = 0; win < 4; ++win) {
         const int oh = 2 * py + (win >> 1), ow = 2 * px + (win & 1);
@@ -646,6 +649,9 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     }
     __syncthreads();
     if (t < 4) stamp(2 + 3 * t);
+    // next image's inputs are issued here, a whole phase B + C before phase A consumes them; the loop
+    // has no other global operation, so that phase's vmcnt wait is for these loads only
+    nxt = fetch(t + 1);
 
     // ---- phase B1: conv2 wgrad  dW2[n][tap*8+c] += sum_pos dY2[pos][n] * pool1[pos + tap][c]
     for (int kc = 0; kc < ((!HW || (cb.ablate & 64)) ? 0 : W2CH); ++kc) {
@@ -768,7 +774,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
 
 }  // namespace
 
-static int fwd_ipb(int B) { return std::max(1, (B + 1023) / 1024); }
+static int fwd_ipb(int B) { return std::min(MAX_IPB, std::max(1, (B + 1023) / 1024)); }
 static int default_bwd_target() {
   static const int def = [] {
     const char* e = std::getenv("MNIST_AMD_BWD_BLOCKS");  // tuning knob: default target block count
@@ -779,7 +785,7 @@ static int default_bwd_target() {
 
 static int bwd_ipb(int B, int target) {
   const int div = target > 0 ? target : default_bwd_target();
-  return std::max(1, (B + div - 1) / div);
+  return std::min(MAX_IPB, std::max(1, (B + div - 1) / div));
 }
 
 int lenet_conv_bwd_blocks(int B, int target) {
@@ -790,7 +796,8 @@ int lenet_conv_bwd_blocks(int B, int target) {
 // Upper bound of lenet_conv_bwd_blocks(b, target) over every b <= B (partial last batches included):
 // ceil(b / ceil(b / t)) <= min(b, t).  Size the conv slab with this, not with the full-batch grid.
 int lenet_conv_bwd_max_blocks(int B, int target) {
-  return std::max(1, std::min(B, target > 0 ? target : default_bwd_target()));
+  // MAX_IPB caps the images per workgroup, so huge batches use more than `target` workgroups
+  return std::max({1, std::min(B, target > 0 ? target : default_bwd_target()), (B + MAX_IPB - 1) / MAX_IPB});
 }
 
 void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetConvBuffers& cb, hipStream_t s) {
