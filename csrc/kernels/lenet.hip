@@ -516,6 +516,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   for (int i = 0; i < NWT; ++i) {
     const int kcol = (n0w + i) * 16 + row, tap = kcol / 6, c = kcol - 6 * tap;
     w2off[i] = kcol < 150 ? ((tap % 5) * 6 + c) * S::P1P + (tap / 5) * 16 : (kcol == 150 ? 31 : 30) * S::P1P;
+    if (i >= nw) w2off[i] = 30 * S::P1P;  // no third tile on this wave: zero plane
   }
   int w1off[2], w1sel[2];  // conv1 wgrad B: tiles over kcol = tap (25 = bias)
 #pragma unroll
@@ -653,14 +654,34 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     // has no other global operation, so that phase's vmcnt wait is for these loads only
     nxt = fetch(t + 1);
 
-    // ---- phase B1: conv2 wgrad  dW2[n][tap*8+c] += sum_pos dY2[pos][n] * pool1[pos + tap][c]
-    for (int kc = 0; kc < ((!HW || (cb.ablate & 64)) ? 0 : W2CH); ++kc) {
-      const int p0 = kc * KC + grp * KV, oh = p0 >> 4, ow0 = p0 & 15;
-      const Frag a = M::load(dy2t + row * S::D2P + p0);
-      // the tile count is wave-uniform (w comes from readfirstlane), so the third tile is a scalar branch
+    // ---- phase B1: conv2 wgrad  dW2[n][(tap, c)] += sum_pos dY2[pos][n] * pool1[pos + tap][c]
+    //      Straight-line (constant trip counts, the ablation test outside the loop) with the next
+    //      chunk's fragments loaded before this chunk's MFMAs: a runtime trip count kept the loop
+    //      rolled and every chunk waited for its own LDS reads.  Waves with two tiles run the third on
+    //      the zero plane (unconditional loads keep the lgkmcnt bookkeeping exact).
+    if (HW && !(cb.ablate & 64)) {
+      auto ld_a = [&](int kc) { return M::load(dy2t + row * S::D2P + kc * KC + grp * KV); };
+      auto ld_b = [&](int kc, int i) {
+        const int p0 = kc * KC + grp * KV;
+        return M::load(p1t + w2off[i] + (p0 >> 4) * 16 + (p0 & 15));
+      };
+      Frag a = ld_a(0), b[NWT];
 #pragma unroll
-      for (int i = 0; i < NWT; ++i)
-        if (i < nw) M::mma(accW2[i], a, M::load(p1t + w2off[i] + oh * 16 + ow0));
+      for (int i = 0; i < NWT; ++i) b[i] = ld_b(0, i);
+#pragma unroll
+      for (int kc = 0; kc < W2CH; ++kc) {
+        Frag an = a, bn[NWT];
+        if (kc + 1 < W2CH) {
+          an = ld_a(kc + 1);
+#pragma unroll
+          for (int i = 0; i < NWT; ++i) bn[i] = ld_b(kc + 1, i);
+        }
+#pragma unroll
+        for (int i = 0; i < NWT; ++i) M::mma(accW2[i], a, b[i]);
+        a = an;
+#pragma unroll
+        for (int i = 0; i < NWT; ++i) b[i] = bn[i];
+      }
     }
 
     // ---- phase B2: conv2 dgrad, one tile = image rows (y, y+1) x 16 columns x (r, c):
@@ -705,11 +726,18 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
           const T* a0 = dys + ((y0 + 4) * 18 + x + 4) * 16;
           const T* a1 = dys + ((y1 + 4) * 18 + x + 4) * 16;
           f32x4 acc0 = zero4(), acc1 = zero4();
+          Frag fb = M::load(bq), fa0 = M::load(a0 + doff[0]), fa1 = M::load(a1 + doff[0]);
 #pragma unroll
-          for (int kc = 0; kc < D2CH; ++kc) {
-            const Frag fb = M::load(bq + kc * KC);
-            M::mma(acc0, M::load(a0 + doff[kc]), fb);
-            M::mma(acc1, M::load(a1 + doff[kc]), fb);
+          for (int kc = 0; kc < D2CH; ++kc) {  // next chunk's fragments in flight during this one's MFMAs
+            Frag nb = fb, na0 = fa0, na1 = fa1;
+            if (kc + 1 < D2CH) {
+              nb = M::load(bq + (kc + 1) * KC);
+              na0 = M::load(a0 + doff[kc + 1]);
+              na1 = M::load(a1 + doff[kc + 1]);
+            }
+            M::mma(acc0, fa0, fb);
+            M::mma(acc1, fa1, fb);
+            fb = nb; fa0 = na0; fa1 = na1;
           }
           dgrad_tile_epi(y0, acc0);
           dgrad_tile_epi(y1, acc1);
@@ -717,8 +745,17 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
           const int y0 = 2 * q0;
           const T* a0 = dys + ((y0 + 4) * 18 + x + 4) * 16;
           f32x4 acc0 = zero4();
+          Frag fb = M::load(bq), fa0 = M::load(a0 + doff[0]);
 #pragma unroll
-          for (int kc = 0; kc < D2CH; ++kc) M::mma(acc0, M::load(a0 + doff[kc]), M::load(bq + kc * KC));
+          for (int kc = 0; kc < D2CH; ++kc) {
+            Frag nb = fb, na0 = fa0;
+            if (kc + 1 < D2CH) {
+              nb = M::load(bq + (kc + 1) * KC);
+              na0 = M::load(a0 + doff[kc + 1]);
+            }
+            M::mma(acc0, fa0, fb);
+            fb = nb; fa0 = na0;
+          }
           dgrad_tile_epi(y0, acc0);
         }
       }
@@ -728,11 +765,28 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
 
     // ---- phase C: conv1 wgrad  dW1[n][tap] += sum_pos dY1[pos][n] * xpad[pos + tap]
     if constexpr (HD) {
-      for (int kc = w; kc < ((cb.ablate & 512) ? 0 : W1CH); kc += 4) {
-        const int p0 = kc * KC + grp * KV, oh = p0 >> 5, ow0 = p0 & 31;
-        const Frag a = M::load(dy1t + min(row, 7) * S::D1P + p0);  // rows 6..15: DY1T rows 6/7 are zero
+      // chunks kc = w, w + 4, ... (W1CH / 4 per wave), straight-line with one chunk of prefetch
+      static_assert(W1CH % 4 == 0, "conv1 wgrad chunks split evenly over the 4 waves");
+      if (!(cb.ablate & 512)) {
+        auto ld_a = [&](int kc) { return M::load(dy1t + min(row, 7) * S::D1P + kc * KC + grp * KV); };  // rows 6..15: zero rows
+        auto ld_b = [&](int kc, int nt) {
+          const int p0 = kc * KC + grp * KV;
+          return M::load(xs + w1off[nt] + (p0 >> 5) * 32 + (p0 & 31));
+        };
+        Frag a = ld_a(w), b0 = ld_b(w, 0), b1 = ld_b(w, 1);
 #pragma unroll
-        for (int nt = 0; nt < 2; ++nt) M::mma(accW1[nt], a, M::load(xs + w1off[nt] + oh * 32 + ow0));
+        for (int j = 0; j < W1CH / 4; ++j) {
+          Frag an = a, bn0 = b0, bn1 = b1;
+          if (j + 1 < W1CH / 4) {
+            const int kn = w + 4 * (j + 1);
+            an = ld_a(kn);
+            bn0 = ld_b(kn, 0);
+            bn1 = ld_b(kn, 1);
+          }
+          M::mma(accW1[0], a, b0);
+          M::mma(accW1[1], a, b1);
+          a = an; b0 = bn0; b1 = bn1;
+        }
       }
       __syncthreads();
       if (t < 4) stamp(4 + 3 * t);
