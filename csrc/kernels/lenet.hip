@@ -20,6 +20,7 @@
 // bit 2 = pooled pre-activation > 0 (ReLU passes the gradient).
 #include <cstdlib>
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 #include "launch.h"
@@ -201,18 +202,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
       }
     }
   };
-  auto c2_acc = [&](int mt, f32x4& acc) {
+  auto c2_base = [&](int mt) {  // im2col row of tile mt for this lane: pooled position x window element
     const int q = row >> 2, e = row & 3;
     const int p = min(mt * 4 + q, 24), py = p / 5, px = p % 5;
-    const int base = ((2 * py + (e >> 1)) * 14 + 2 * px + (e & 1)) * 8;
+    return ((2 * py + (e >> 1)) * 14 + 2 * px + (e & 1)) * 8;
+  };
+  auto c2_a = [&](int base, int kc) {  // A fragment of K-chunk kc (8 taps x 8 channels ... per lane group)
+    int pos, c0;
+    if constexpr (KV == 8) { pos = kc * 4 + grp; c0 = 0; }
+    else { pos = kc * 2 + (grp >> 1); c0 = (grp & 1) * 4; }
+    pos = min(pos, 24);
+    const int kh = pos / 5, kw = pos % 5;
+    return M::load(p1s + base + (kh * 14 + kw) * 8 + c0);
+  };
+  // NT tiles (1 or 2) sharing the B fragments, next chunk's A fragments in flight during this chunk's
+  // MFMAs (the rolled-up form waited for every A read before its MFMA)
+  auto c2_acc = [&](auto ntc, const int* mts, f32x4* acc) {
+    constexpr int NT = decltype(ntc)::value;
+    int base[NT];
+    Frag a[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      base[j] = c2_base(mts[j]);
+      a[j] = c2_a(base[j], 0);
+    }
 #pragma unroll
     for (int kc = 0; kc < C2CH; ++kc) {
-      int pos, c0;
-      if constexpr (KV == 8) { pos = kc * 4 + grp; c0 = 0; }
-      else { pos = kc * 2 + (grp >> 1); c0 = (grp & 1) * 4; }
-      pos = min(pos, 24);
-      const int kh = pos / 5, kw = pos % 5;
-      M::mma(acc, M::load(p1s + base + (kh * 14 + kw) * 8 + c0), M::load(w2s + row * S::W2P + kc * KC + grp * KV));
+      Frag an[NT];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) an[j] = kc + 1 < C2CH ? c2_a(base[j], kc + 1) : a[j];
+      const Frag b = M::load(w2s + row * S::W2P + kc * KC + grp * KV);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) M::mma(acc[j], a[j], b);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) a[j] = an[j];
     }
   };
   auto c2_epi = [&](int mt, const f32x4& acc) {
@@ -335,15 +358,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
     // ---- conv2 + bias + ReLU + maxpool: 100 rows (25 pooled x 4) = 7 M-tiles, N = 16
     if (!(cb.ablate & 4)) {
       if (w < 3) {  // waves 0-2: tiles (2w, 2w+1) as a pair; wave 3: tile 6
-        f32x4 accA = zero4(), accB = zero4();
-        c2_acc(2 * w, accA);
-        c2_acc(2 * w + 1, accB);
-        c2_epi(2 * w, accA);
-        c2_epi(2 * w + 1, accB);
+        const int mts[2] = {2 * w, 2 * w + 1};
+        f32x4 acc[2] = {zero4(), zero4()};
+        c2_acc(std::integral_constant<int, 2>{}, mts, acc);
+        c2_epi(2 * w, acc[0]);
+        c2_epi(2 * w + 1, acc[1]);
       } else {
-        f32x4 acc = zero4();
-        c2_acc(6, acc);
-        c2_epi(6, acc);
+        const int mts[1] = {6};
+        f32x4 acc[1] = {zero4()};
+        c2_acc(std::integral_constant<int, 1>{}, mts, acc);
+        c2_epi(6, acc[0]);
       }
     }
     __syncthreads();
