@@ -50,8 +50,10 @@ def parse(argv=None):
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--momentum", type=float, default=0.9)
     ap.add_argument("--comm", default="rccl", choices=["rccl", "torch"])
-    ap.add_argument("--plan", default="auto", choices=["auto", "join", "split"],
-                    help="multi-GPU step plan (auto = time the candidates at start-up and keep the fastest)")
+    ap.add_argument("--plan", default="auto", choices=["auto", "join", "split", "fixed"],
+                    help="step plan: auto = time the candidates at start-up and keep the fastest "
+                         "(multi-GPU plans, or the single-GPU schedules); join/split = that multi-GPU plan; "
+                         "fixed = no calibration, defaults")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--comm-world1", action="store_true",
                     help="attach a world-1 RCCL communicator (runs the multi-GPU step schedule on one GPU)")
@@ -156,9 +158,7 @@ def main(argv=None) -> int:
             rccl_version = C.rccl_version()
             tr.attach_comm(comm, W)
             tr.broadcast_params(0)
-            if a.plan == "auto":
-                tune = tr.autotune_plan(reduce_max=ctx.all_reduce_max)
-            else:
+            if a.plan != "auto":
                 tr.set_plan(a.plan)
         else:
             import torch.distributed as dist
@@ -166,6 +166,10 @@ def main(argv=None) -> int:
             tr.load_flat(tr.params.clone())
 
     use_graph = not a.no_graph and a.comm == "rccl"
+    # start-up schedule calibration (multi-GPU plan on the communicator, or the single-GPU
+    # schedule): a few captured-step replays per candidate, state restored, choice in the JSON
+    if use_graph and a.plan == "auto" and (comm is not None or W == 1):
+        tune = tr.autotune_plan(reduce_max=ctx.all_reduce_max)
 
     def one_step():
         if a.comm == "rccl" or W == 1:

@@ -121,6 +121,8 @@ PYBIND11_MODULE(_C, m) {
       .def("buckets", &Trainer::buckets)
       .def("set_plan", &Trainer::set_plan)
       .def_property_readonly("plan", &Trainer::plan)
+      .def("set_concurrent", &Trainer::set_concurrent)
+      .def_property_readonly("concurrent", &Trainer::concurrent)
       .def("set_bwd_blocks", &Trainer::set_bwd_blocks)
       .def_property_readonly("bwd_blocks", &Trainer::bwd_blocks)
       .def_property_readonly("bwd_grid", &Trainer::bwd_grid)

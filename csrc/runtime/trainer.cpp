@@ -41,7 +41,8 @@ void post_launch(hipStream_t s) {
     if (st == hipStreamCaptureStatusNone) HIP_CHECK(hipStreamSynchronize(s));
   }
 }
-// MNIST_AMD_CONCURRENT: 0 = serial step, otherwise (default) FC wgrad || conv_bwd (see launch_step)
+// MNIST_AMD_CONCURRENT: initial value of the single-GPU schedule (0 = serial, otherwise FC wgrad ||
+// conv_bwd); set_concurrent() changes it at run time (NativeTrainer.autotune_plan times both)
 int concurrent_mode() {
   static const int m = [] {
     const char* e = std::getenv("MNIST_AMD_CONCURRENT");
@@ -81,6 +82,7 @@ Trainer::Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const
   if (ld_b < ((batch + 63) / 64) * 64) throw std::invalid_argument("ld_b must be >= batch rounded up to 64");
   nparam_ = model_nparam(model_);
   max_conv_slabs_ = model_ == ModelKind::LENET ? lenet_conv_bwd_max_blocks(batch_, 0) : 0;
+  concurrent_ = concurrent_mode() != 0;
   const int cp = model_conv_params(model_);
   if (cp > 0) {
     buckets_.push_back({cp, nparam_, 0});
@@ -254,7 +256,7 @@ void Trainer::launch_step(int B, hipStream_t s) {
   const int hrows = launch_head(model_, dtype_, true, br, hb, head_rows_per_block(model_, dtype_, batch_), s);
   post_launch(s);
 
-  if (model_ == ModelKind::LENET && (comm_ || concurrent_mode() != 0)) {
+  if (model_ == ModelKind::LENET && (comm_ || concurrent_)) {
     // fork: conv_bwd on the main stream (enqueued first, so its one-round grid is dispatched whole:
     // measured wgrad-first 0.1692 ms/step, conv_bwd-first 0.1565, serial 0.1671), the FC wgrad (no LDS,
     // 320 small blocks) on the aux stream beside it

@@ -55,6 +55,9 @@ class Trainer {
     invalidate();
   }
   int plan() const { return static_cast<int>(plan_); }
+  // single-GPU LeNet schedule: FC wgrad + FC update on the aux stream beside conv_bwd (true) or serial
+  void set_concurrent(bool on) { concurrent_ = on; invalidate(); }
+  bool concurrent() const { return concurrent_; }
   // conv_bwd workgroup target (0 = default); the grid actually used for the full batch is bwd_grid()
   void set_bwd_blocks(int n) {
     n = n < 0 ? 0 : n;
@@ -112,6 +115,7 @@ class Trainer {
   uint32_t seed_ = 1234;
   int world_ = 1;
   Plan plan_ = Plan::JOIN;
+  bool concurrent_ = true;
   int bwd_blocks_ = 0;
   int max_conv_slabs_ = 0;  // rows of the conv slab (lenet_conv_bwd_max_blocks(batch) at the default target)
   std::shared_ptr<RcclComm> comm_;

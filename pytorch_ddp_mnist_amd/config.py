@@ -107,8 +107,8 @@ def _add_extra_flags(p: argparse.ArgumentParser, defaults: TrainConfig) -> None:
     add("--tqdm", action="store_true", help="rank-0 progress bars with the batch loss (reference: tqdm per batch)")
     add("--progress_every", type=int, default=None, help="--tqdm update period in batches (one device sync each)")
     add("--shard_eval", action="store_true", help="shard the test set across ranks (reference: every rank evaluates all)")
-    add("--plan", type=str, default=None, choices=["auto", "join", "split"],
-        help="multi-GPU step plan (auto: time the candidates on the communicator at start-up)")
+    add("--plan", type=str, default=None, choices=["auto", "join", "split", "fixed"],
+        help="step plan (auto: time the candidate schedules at start-up; join/split: multi-GPU plan; fixed: defaults)")
     add("--io_mode", type=str, default=None, choices=["bulk", "per_sample"],
         help="netCDF input: bulk pread (default) or the reference's per-sample __getitem__ reads, timed (MB/s)")
     add("--resume", type=str, default=None,

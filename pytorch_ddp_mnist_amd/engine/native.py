@@ -197,7 +197,7 @@ class NativeTrainer:
     def plan_info(self) -> dict:
         """What a full-batch step runs: plan, conv_bwd grid, and the collectives in issue order."""
         coll = [(b.p0, b.p1) for b in self.rt.issued_collectives()]
-        return {"plan": self.plan if self.comm is not None else "local",
+        return {"plan": self.plan if self.comm is not None else ("local" if self.rt.concurrent else "local-serial"),
                 "conv_bwd_grid": self.rt.bwd_grid if self.model_name == "lenet5" else None,
                 "collectives": [{"params": [a, b], "bytes": 4 * (b - a)} for a, b in coll]}
 
@@ -222,30 +222,43 @@ class NativeTrainer:
             self.comm.abort()
             raise CollectiveError(f"RCCL communicator error on rank {self.comm.rank}: {err}")
 
+    def apply_plan(self, cfg: dict) -> None:
+        """Install one candidate of :meth:`autotune_plan` ({plan, bwd_blocks, concurrent})."""
+        if "concurrent" in cfg:
+            self.rt.set_concurrent(bool(cfg["concurrent"]))
+        if "plan" in cfg or "bwd_blocks" in cfg:
+            self.set_plan(cfg.get("plan", self.plan), int(cfg.get("bwd_blocks", 0)))
+
     def autotune_plan(self, candidates=None, iters: int = 12, warmup: int = 3, reduce_max=None,
                       margin: float = 0.015, log=None) -> dict:
-        """Time each candidate plan on the attached communicator and keep the fastest.
+        """Time each candidate step schedule and keep the fastest (a start-up calibration, like
+        cudnn.benchmark).
 
-        Every candidate replays the captured step ``warmup + iters`` times on batch 0 of the loaded
-        epoch order (the device step counter is rewound after each replay), so all ranks issue the
-        same collectives in the same order; per-replay GPU times come from events on the step
-        stream and ``reduce_max`` (e.g. a gloo MAX all-reduce) makes the decision identical on every
-        rank.  Parameters, momentum, counters and metrics are restored afterwards.
-        ``MNIST_AMD_MG_SCHED=join|split`` skips the search.
+        With a communicator the candidates are the multi-GPU plans (JOIN / SPLIT / SPLIT with a
+        capped conv_bwd grid, :func:`~pytorch_ddp_mnist_amd.parallel.ddp.default_plan_candidates`),
+        timed on the real communicator; without one, the single-GPU LeNet schedules
+        (:func:`~pytorch_ddp_mnist_amd.parallel.ddp.local_plan_candidates`).  Every candidate replays
+        the captured step ``warmup + iters`` times on batch 0 of the loaded epoch order (the device
+        step counter is rewound after each replay), so all ranks issue the same collectives in the
+        same order; per-replay GPU times come from events on the step stream and ``reduce_max``
+        (e.g. a gloo MAX all-reduce) makes the decision identical on every rank.  Parameters,
+        momentum, counters and metrics are restored afterwards.  ``MNIST_AMD_MG_SCHED=join|split``
+        pins the multi-GPU plan.
         """
-        from ..parallel.ddp import choose_plan, default_plan_candidates
+        from ..parallel.ddp import choose_plan, default_plan_candidates, local_plan_candidates
         forced = os.environ.get("MNIST_AMD_MG_SCHED")
-        if self.comm is None:
-            return {"chosen": "local", "timings_ms": {}}
-        if forced:
+        if self.comm is not None and forced:
             self.set_plan(forced, 0)
             return {"chosen": forced, "timings_ms": {}, "forced": True}
         if self.model_name != "lenet5":
-            self.set_plan("join", 0)
-            return {"chosen": "join", "timings_ms": {}}
+            return {"chosen": "join" if self.comm is not None else "local", "timings_ms": {}}
         if candidates is None:
-            ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
-            candidates = default_plan_candidates(self.C.conv_bwd_blocks(self.batch), ncu)
+            if self.comm is not None:
+                ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+                candidates = default_plan_candidates(self.C.conv_bwd_blocks(self.batch), ncu)
+            else:
+                candidates = local_plan_candidates()
+        prefer = "join" if self.comm is not None else "concurrent"
         if getattr(self, "n_epoch", 0) < max(2, self.host_step + 1) * self.batch:
             raise RuntimeError("autotune_plan: the loaded epoch order needs >= 2 full batches beyond the current step")
         self.synchronize()
@@ -253,8 +266,8 @@ class NativeTrainer:
         self._sync_in()
         timings = {}
         st = self.stream
-        for name, (plan, blocks) in candidates.items():
-            self.set_plan(plan, blocks)
+        for name, cfg in candidates.items():
+            self.apply_plan(cfg)
             self.capture()
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                   for _ in range(warmup + iters)]
@@ -274,11 +287,11 @@ class NativeTrainer:
             for dst, src in zip((self.params, self.mom, self.grad, self.step_ctr, self.metrics), saved):
                 dst.copy_(src)
         self.rt.pack(st.cuda_stream)
-        chosen = choose_plan(timings, margin=margin)
-        self.set_plan(*candidates[chosen])
+        chosen = choose_plan(timings, prefer=prefer, margin=margin)
+        self.apply_plan(candidates[chosen])
         self.synchronize()
         out = {"chosen": chosen, "timings_ms": {k: round(v, 4) for k, v in timings.items()},
-               "candidates": {k: {"plan": p, "bwd_blocks": b} for k, (p, b) in candidates.items()}}
+               "candidates": candidates}
         if log is not None:
             log(out)
         return out

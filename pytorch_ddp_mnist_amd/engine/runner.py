@@ -62,7 +62,7 @@ class NativeEngine:
         self.use_graph = cfg.graph and not self.torch_comm
         self.fault = FaultInjector(ctx.rank)
         self.plan_forced = None if cfg.plan == "auto" else cfg.plan
-        self.tuned = self.tr.comm is None
+        self.tuned = not self.use_graph  # the calibration times captured steps
         self.tune = None
 
     def _load_rows(self, dst_x: torch.Tensor, dst_y: torch.Tensor, x: np.ndarray, y: np.ndarray) -> None:
@@ -109,12 +109,14 @@ class NativeEngine:
             self.tr.step(b, use_graph=self.use_graph)
 
     def _maybe_tune(self, nfull: int) -> None:
-        """First epoch with a communicator: pick the multi-GPU step plan by timing the candidates."""
-        if self.tuned or nfull < 1:
+        """First epoch: pick the step schedule by timing the candidates (multi-GPU plans on the
+        communicator, or the single-GPU schedules)."""
+        if self.tuned or nfull < 2:
             return
         self.tuned = True
         if self.plan_forced:
-            self.tr.set_plan(self.plan_forced)
+            if self.tr.comm is not None:
+                self.tr.set_plan(self.plan_forced)
             return
         self.tune = self.tr.autotune_plan(reduce_max=self.ctx.all_reduce_max)
         if self.ctx.rank == 0:

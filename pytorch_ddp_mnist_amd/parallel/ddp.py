@@ -61,18 +61,22 @@ def plan_buckets(phases: Sequence[Tuple[int, int]], cap_bytes: Optional[int] = N
     return out
 
 
-def default_plan_candidates(default_grid: int, n_cu: int, reserve_cus=(16,)) -> Dict[str, Tuple[str, int]]:
-    """Candidate plans: name -> (plan, conv_bwd target workgroups; 0 = default one full round).
-
-    ``split_rN`` caps conv_bwd to the workgroups that fit on ``n_cu - N`` CUs at the default
-    workgroups-per-CU, so N CUs stay free for RCCL's kernels while conv_bwd runs.
-    """
-    out: Dict[str, Tuple[str, int]] = {"join": ("join", 0), "split": ("split", 0)}
+def default_plan_candidates(default_grid: int, n_cu: int, reserve_cus=(16,)) -> Dict[str, dict]:
+    """Multi-GPU candidates: name -> {plan, bwd_blocks (conv_bwd target workgroups; 0 = default one
+    full round)}.  ``split_rN`` caps conv_bwd to the workgroups that fit on ``n_cu - N`` CUs at the
+    default workgroups-per-CU, so N CUs stay free for RCCL's kernels while conv_bwd runs."""
+    out: Dict[str, dict] = {"join": dict(plan="join", bwd_blocks=0), "split": dict(plan="split", bwd_blocks=0)}
     per_cu = max(1, round(default_grid / max(1, n_cu)))
     for r in reserve_cus:
         if 0 < r < n_cu and default_grid >= n_cu:
-            out[f"split_r{r}"] = ("split", per_cu * (n_cu - r))
+            out[f"split_r{r}"] = dict(plan="split", bwd_blocks=per_cu * (n_cu - r))
     return out
+
+
+def local_plan_candidates() -> Dict[str, dict]:
+    """Single-GPU LeNet schedules: the FC weight gradient + FC update on an aux stream beside
+    conv_bwd (``concurrent``, the default) or after it (``serial``)."""
+    return {"concurrent": dict(concurrent=True), "serial": dict(concurrent=False)}
 
 
 def choose_plan(timings_ms: Dict[str, float], prefer: str = "join", margin: float = 0.015) -> str:

@@ -59,6 +59,7 @@ def test_choose_plan_is_rank_consistent():
 
 def test_default_plan_candidates():
     c = default_plan_candidates(512, 256)
-    assert c["join"] == ("join", 0) and c["split"] == ("split", 0)
-    assert c["split_r16"] == ("split", 2 * (256 - 16))
+    assert c["join"] == dict(plan="join", bwd_blocks=0) and c["split"] == dict(plan="split", bwd_blocks=0)
+    assert c["split_r16"] == dict(plan="split", bwd_blocks=2 * (256 - 16))
     assert set(default_plan_candidates(64, 256)) == {"join", "split"}   # small batch: no capped variant
+    assert choose_plan({"concurrent": 0.13, "serial": 0.1285}, prefer="concurrent") == "concurrent"

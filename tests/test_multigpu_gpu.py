@@ -104,6 +104,7 @@ def test_autotune_plan_restores_state(native, small_mnist):
     assert set(out["timings_ms"]) >= {"join", "split"}
     info = tr.plan_info()
     assert info["plan"] == out["candidates"][out["chosen"]]["plan"]
+    assert tr.rt.bwd_grid == tr.C.conv_bwd_blocks(512, out["candidates"][out["chosen"]]["bwd_blocks"])
     assert sum(c["bytes"] for c in info["collectives"]) == 4 * tr.nparam
     tr.step(512)                                    # the installed plan trains
     tr.synchronize()
