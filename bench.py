@@ -171,25 +171,24 @@ def main(argv=None) -> int:
     if use_graph and a.plan == "auto" and (comm is not None or W == 1):
         tune = tr.autotune_plan(reduce_max=ctx.all_reduce_max)
 
-    def one_step():
+    def run(n):
         if a.comm == "rccl" or W == 1:
-            tr.step(a.batch, use_graph=use_graph)
-        else:
-            import torch.distributed as dist
+            tr.run_steps(n, use_graph=use_graph)  # k-step graphs (MNIST_AMD_GRAPH_STEPS), then single steps
+            return
+        import torch.distributed as dist
+        for _ in range(n):
             tr.forward_backward(a.batch)
             with torch.cuda.stream(tr.stream):
                 dist.all_reduce(tr.grad)
             tr.optimizer_step(1.0 / W)
 
     tr.reset_metrics()
-    for _ in range(a.warmup):
-        one_step()
+    run(a.warmup)
     tr.synchronize()
     ctx.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        one_step()
+    run(a.steps)
     tr.synchronize()
     torch.cuda.synchronize(dev)
     ctx.barrier()

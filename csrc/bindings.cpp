@@ -138,6 +138,9 @@ PYBIND11_MODULE(_C, m) {
       .def("eval_batch", &Trainer::eval_batch)
       .def("capture", &Trainer::capture)
       .def("replay", &Trainer::replay)
+      .def("capture_multi", &Trainer::capture_multi)
+      .def("replay_multi", &Trainer::replay_multi)
+      .def_property_readonly("multi_steps", &Trainer::multi_steps)
       .def("invalidate", &Trainer::invalidate)
       .def_property_readonly("captured", &Trainer::captured)
       .def_property_readonly("nparam", &Trainer::nparam)

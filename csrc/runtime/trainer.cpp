@@ -101,6 +101,8 @@ Trainer::Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const
 Trainer::~Trainer() {
   if (exec_) hipGraphExecDestroy(exec_);
   if (graph_) hipGraphDestroy(graph_);
+  if (multi_exec_) hipGraphExecDestroy(multi_exec_);
+  if (multi_graph_) hipGraphDestroy(multi_graph_);
   for (auto& e : events_) hipEventDestroy(e);
   if (comm_stream_) hipStreamDestroy(comm_stream_);
   if (aux_stream_) hipStreamDestroy(aux_stream_);
@@ -114,6 +116,9 @@ int Trainer::conv_slabs() const { return model_ == ModelKind::LENET ? lenet_conv
 void Trainer::invalidate() {
   if (exec_) { hipGraphExecDestroy(exec_); exec_ = nullptr; }
   if (graph_) { hipGraphDestroy(graph_); graph_ = nullptr; }
+  if (multi_exec_) { hipGraphExecDestroy(multi_exec_); multi_exec_ = nullptr; }
+  if (multi_graph_) { hipGraphDestroy(multi_graph_); multi_graph_ = nullptr; }
+  multi_steps_ = 0;
 }
 
 BatchRef Trainer::batch_ref(int B) const {
@@ -399,13 +404,11 @@ void Trainer::eval_batch(uintptr_t images, uintptr_t labels, uintptr_t idx, int 
   post_launch(s);
 }
 
-void Trainer::capture(uintptr_t stream) {
-  invalidate();
-  hipStream_t s = S(stream);
+void Trainer::capture_into(hipStream_t s, int nsteps, hipGraph_t* graph, hipGraphExec_t* exec) {
   trace("capture: begin");
   HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
   try {
-    launch_step(batch_, s);
+    for (int i = 0; i < nsteps; ++i) launch_step(batch_, s);
   } catch (...) {
     hipGraph_t g = nullptr;
     hipStreamEndCapture(s, &g);
@@ -413,14 +416,36 @@ void Trainer::capture(uintptr_t stream) {
     throw;
   }
   trace("capture: end");
-  HIP_CHECK(hipStreamEndCapture(s, &graph_));
+  HIP_CHECK(hipStreamEndCapture(s, graph));
   trace("capture: instantiate");
-  HIP_CHECK(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
+  HIP_CHECK(hipGraphInstantiate(exec, *graph, nullptr, nullptr, 0));
   trace("capture: done");
+}
+
+void Trainer::capture(uintptr_t stream) {
+  invalidate();
+  capture_into(S(stream), 1, &graph_, &exec_);
+}
+
+// k consecutive steps in ONE graph: consecutive steps are plain stream-order edges inside it, so the
+// per-launch gap between graphs (~5 us measured between step graphs) is paid once per k steps; the
+// device step counter addresses every step's batch, so the graph stays valid for any k-step window.
+void Trainer::capture_multi(uintptr_t stream, int k) {
+  if (k < 1) throw std::invalid_argument("capture_multi: k must be >= 1");
+  if (multi_exec_) { hipGraphExecDestroy(multi_exec_); multi_exec_ = nullptr; }
+  if (multi_graph_) { hipGraphDestroy(multi_graph_); multi_graph_ = nullptr; }
+  capture_into(S(stream), k, &multi_graph_, &multi_exec_);
+  multi_steps_ = k;
 }
 
 void Trainer::replay(uintptr_t stream) {
   if (!exec_) throw std::runtime_error("replay: no captured graph");
   HIP_CHECK(hipGraphLaunch(exec_, S(stream)));
+  if (sync_debug()) HIP_CHECK(hipStreamSynchronize(S(stream)));
+}
+
+void Trainer::replay_multi(uintptr_t stream) {
+  if (!multi_exec_) throw std::runtime_error("replay_multi: no captured multi-step graph");
+  HIP_CHECK(hipGraphLaunch(multi_exec_, S(stream)));
   if (sync_debug()) HIP_CHECK(hipStreamSynchronize(S(stream)));
 }

@@ -90,6 +90,10 @@ class Trainer {
   void capture(uintptr_t stream);
   void replay(uintptr_t stream);
   bool captured() const { return exec_ != nullptr; }
+  // k consecutive full-batch steps in one hipGraph (one launch per k steps)
+  void capture_multi(uintptr_t stream, int k);
+  void replay_multi(uintptr_t stream);
+  int multi_steps() const { return multi_steps_; }
   void invalidate();
 
   int nparam() const { return nparam_; }
@@ -104,6 +108,7 @@ class Trainer {
   LenetConvBuffers conv_buffers() const;
   void launch_step(int B, hipStream_t s);
   void launch_lenet_comm_tail(int B, int nslab, int splits, hipStream_t s);
+  void capture_into(hipStream_t s, int nsteps, hipGraph_t* graph, hipGraphExec_t* exec);
   std::vector<Bucket> coalesced_buckets() const;
   void all_reduce(const std::vector<Bucket>& bs, int phase, hipStream_t s);
 
@@ -125,6 +130,9 @@ class Trainer {
   std::vector<hipEvent_t> events_;
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t exec_ = nullptr;
+  hipGraph_t multi_graph_ = nullptr;
+  hipGraphExec_t multi_exec_ = nullptr;
+  int multi_steps_ = 0;
   int zero_step_dev_ = 0;
   int32_t* zero_counter_ = nullptr;  // device {0,0} for eval batch addressing
 };

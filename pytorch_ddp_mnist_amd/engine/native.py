@@ -342,15 +342,36 @@ class NativeTrainer:
         else:
             self.rt.train_step(B, self.stream.cuda_stream)
 
+    def run_steps(self, n: int, use_graph: bool = True, k: Optional[int] = None) -> None:
+        """``n`` consecutive full-batch steps.  With graphs, runs of ``k`` steps are ONE hipGraph launch
+        (``MNIST_AMD_GRAPH_STEPS``, default 8; the graph launch gap is paid once per k steps), the
+        remainder single-step graphs.  Same kernels, same order, same results as ``n`` x :meth:`step`."""
+        k = int(os.environ.get("MNIST_AMD_GRAPH_STEPS", "8")) if k is None else int(k)
+        if not use_graph or k <= 1:
+            for _ in range(n):
+                self.step(self.batch, use_graph)
+            return
+        while n >= k:
+            if getattr(self, "n_epoch", 0) < (self.host_step + k) * self.batch:
+                break  # the k-step window would run past the loaded order: finish with single steps
+            if self.rt.multi_steps != k:
+                self.rt.capture_multi(self.stream.cuda_stream, k)
+            self.rt.replay_multi(self.stream.cuda_stream)
+            self.host_step += k
+            n -= k
+        for _ in range(n):
+            self.step(self.batch, use_graph)
+
     def train_epoch(self, indices: torch.Tensor, use_graph: bool = True, progress=None) -> EpochStats:
         self.set_epoch_indices(indices)
         self.reset_metrics()
         n = indices.numel()
         nfull, last = divmod(n, self.batch)
-        for i in range(nfull):
+        if progress is None:
+            self.run_steps(nfull, use_graph)
+        for i in range(nfull if progress is not None else 0):
             self.step(self.batch, use_graph)
-            if progress is not None:
-                progress(i)
+            progress(i)
         if last:
             self.step(last, use_graph=False)
         return self.read_metrics("train")

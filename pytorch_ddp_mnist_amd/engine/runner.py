@@ -142,7 +142,12 @@ class NativeEngine:
         every = getattr(progress, "every", 0) if progress is not None else 0
         prev = 0.0
         with range_("train_full_batches"):
-            for i in range(nfull):
+            if not every and not self.torch_comm:
+                tr.run_steps(nfull, use_graph=self.use_graph)   # k-step graph launches
+                nfull_loop = 0
+            else:
+                nfull_loop = nfull
+            for i in range(nfull_loop):
                 self._step(B)
                 if every and ((i + 1) % every == 0 or i + 1 == nfull):
                     k = (i % every) + 1

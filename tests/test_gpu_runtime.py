@@ -122,3 +122,30 @@ def test_reference_mlp_on_gpu_matches_cpu_engine(tmp_path):
     lc = re.search(r"global_train_loss=([0-9.]+).*val_loss=([0-9.]+) val_acc=([0-9.]+)", out_cpu).groups()
     for a, b in zip(lg, lc):
         assert abs(float(a) - float(b)) < 2e-3, (out_gpu, out_cpu)
+
+@pytest.mark.parametrize("with_comm", [False, True])
+@pytest.mark.parametrize("model_name", ["mlp", "lenet5"])
+def test_multi_step_graph_matches_single_steps(native, small_mnist, model_name, with_comm):
+    """run_steps: k steps in one hipGraph (plus single-step remainder) == the same steps one graph each,
+    bitwise (same kernels, same order); the loaded order bounds the k-step windows."""
+    from pytorch_ddp_mnist_amd.engine.native import NativeTrainer
+    from pytorch_ddp_mnist_amd.models import build_model
+    x, y, _, _ = small_mnist
+    torch.manual_seed(0)
+    m = build_model(model_name)
+    idx = torch.randperm(len(y), generator=torch.Generator().manual_seed(2))[:128 * 11].to(torch.int32)
+    out = []
+    for k in (1, 4):
+        tr = NativeTrainer(model_name, "bf16", 128, torch.from_numpy(x.reshape(-1, 784)), torch.from_numpy(y),
+                           dropout=0.0, init=m)
+        if with_comm:
+            tr.attach_comm(native.RcclComm(native.RcclComm.make_unique_id(), 0, 1, 0), 1)
+            tr.broadcast_params(0)
+        tr.set_epoch_indices(idx)
+        tr.run_steps(11, use_graph=True, k=k)   # k=4: two 4-step graphs + 3 single steps
+        tr.synchronize()
+        assert tr.host_step == 11
+        out.append((tr.params.cpu(), tr.read_metrics().loss_sum))
+        if k == 4:
+            assert tr.rt.multi_steps == 4
+    assert torch.equal(out[0][0], out[1][0]) and out[0][1] == out[1][1]
