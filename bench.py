@@ -182,6 +182,8 @@ def main(argv=None) -> int:
                 dist.all_reduce(tr.grad)
             tr.optimizer_step(1.0 / W)
 
+    if use_graph and (a.comm == "rccl" or W == 1):
+        tr.prepare_graphs()   # capture + instantiate the 1-step and k-step graphs before the clock
     tr.reset_metrics()
     run(a.warmup)
     tr.synchronize()

@@ -87,8 +87,10 @@ struct FwdSmem {
   static constexpr int OFF_P2 = rup(OFF_M1 + M1IMG, 16);                  // [400] T      pool2 output (NCHW)
   static constexpr int OFF_M2 = rup(OFF_P2 + 400 * (int)sizeof(T), 16);   // [400] u8     pool2 codes
   static constexpr int W2P = 232;                                          // C2F row pitch (224 + 8)
+  // conv2's B operand: registers for bf16 (7 chunks = 28 VGPRs), an LDS image for f32 (13 chunks)
+  static constexpr bool W2LDS = sizeof(T) != 2;
   static constexpr int OFF_W2 = rup(OFF_M2 + 400, 16);                     // [16][W2P] T  conv2 B operand
-  static constexpr int TOTAL = rup(OFF_W2 + 16 * W2P * (int)sizeof(T), 16);
+  static constexpr int TOTAL = W2LDS ? rup(OFF_W2 + 16 * W2P * (int)sizeof(T), 16) : OFF_W2;
 };
 
 // Coalesced 16-byte copy of a staged LDS image to global memory (both 16-byte aligned).
@@ -143,9 +145,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
 
   constexpr int C1CH = 64 / KC;                 // conv1 K = 5 rows x 8 (kw padded)
   constexpr int C2CH = (25 * 8 + KC - 1) / KC;  // conv2 K = 25 taps x 8 ch (7 bf16 / 13 f32 chunks)
-  // conv1's B operand lives in registers; conv2's (7 chunks) is staged once per block in LDS, which
-  // keeps the kernel at <= 128 registers (4 waves per SIMD: the whole 1024-block grid co-resident)
-  T* w2s = reinterpret_cast<T*>(smem + S::OFF_W2);
+  // conv1's B operand lives in registers, and so does conv2's for bf16 (7 chunks; the kernel stays
+  // well under 128 VGPRs, 4 waves per SIMD: the whole 1024-block grid co-resident)
+  T* w2s = reinterpret_cast<T*>(smem + S::OFF_W2);  // (f32 only)
   // conv1 B operand for TWO pooled rows per tile: column (r, c) = (row >> 3, row & 7), k = kh'*8 + kw
   // with kh' = kh + 2r in 0..7, so B[(kh', kw)][(r, c)] = W1[c][kh' - 2r][kw] (zero outside 0..4)
   // (a lane's KV k-values never straddle a kernel row, so each fragment is one 16-byte load or zero)
@@ -158,12 +160,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
       b1[kc] = (c1 < 6 && kh >= 0 && kh <= 4) ? M::load(pack + L::C1 + c1 * 64 + kh * 8 + (k0 & 7)) : M::zero();
     }
   }
-  {
+  Frag b2r[S::W2LDS ? 1 : C2CH];
+  if constexpr (S::W2LDS) {
     constexpr int VE = 16 / (int)sizeof(T);
     for (int e = tid; e < 16 * 224 / VE; e += 256) {
       const int r = e / (224 / VE), c = (e % (224 / VE)) * VE;
       *reinterpret_cast<uint4*>(w2s + r * S::W2P + c) = *reinterpret_cast<const uint4*>(pack + L::C2F + r * 224 + c);
     }
+  } else {
+#pragma unroll
+    for (int kc = 0; kc < C2CH; ++kc) b2r[kc] = M::load(pack + L::C2F + row * 224 + kc * KC + grp * KV);
   }
   const float bias1 = (row & 7) < 6 ? prm[L::CB1 + (row & 7)] : 0.f;
   const float bias2 = prm[L::CB2 + row];
@@ -231,7 +237,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
       Frag an[NT];
 #pragma unroll
       for (int j = 0; j < NT; ++j) an[j] = kc + 1 < C2CH ? c2_a(base[j], kc + 1) : a[j];
-      const Frag b = M::load(w2s + row * S::W2P + kc * KC + grp * KV);
+      Frag b;
+      if constexpr (S::W2LDS) b = M::load(w2s + row * S::W2P + kc * KC + grp * KV);
+      else b = b2r[kc];
 #pragma unroll
       for (int j = 0; j < NT; ++j) M::mma(acc[j], a[j], b);
 #pragma unroll
@@ -329,6 +337,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
     if (!(cb.ablate & 2)) {
       // software pipeline: tile t+1's fragments are loaded and tile t's MFMAs issued BEFORE tile
       // t-1's epilogue (the compiler cannot hoist xs loads over the epilogue's p1s stores itself)
+      // Tile t+1 starts 4 input rows below tile t and K spans 8 rows, so its first half of K chunks
+      // (rows kh' = 0..3) IS tile t's second half (kh' = 4..7): c1base[kc + C1CH/2] = c1base[kc] + 128.
+      // Only the second half is read per tile (8 instead of 14 A reads per wave and image, bf16).
+      constexpr int HC = C1CH / 2;
       Frag fa[C1CH];
 #pragma unroll
       for (int kc = 0; kc < C1CH; ++kc) fa[kc] = M::load(xs + c1base[kc]);
@@ -340,7 +352,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
         for (int kc = 0; kc < C1CH; ++kc) M::mma(acc, fa[kc], b1[kc]);
         if (t + 1 < 7) {
 #pragma unroll
-          for (int kc = 0; kc < C1CH; ++kc) fa[kc] = M::load(xs + c1base[kc] + (t + 1) * 128);
+          for (int kc = 0; kc < HC; ++kc) fa[kc] = fa[kc + HC];
+#pragma unroll
+          for (int kc = HC; kc < C1CH; ++kc) fa[kc] = M::load(xs + c1base[kc] + (t + 1) * 128);
         }
         if (t > 0) c1_epi(t - 1, prev);
         prev = acc;

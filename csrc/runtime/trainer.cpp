@@ -99,10 +99,7 @@ Trainer::Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const
 }
 
 Trainer::~Trainer() {
-  if (exec_) hipGraphExecDestroy(exec_);
-  if (graph_) hipGraphDestroy(graph_);
-  if (multi_exec_) hipGraphExecDestroy(multi_exec_);
-  if (multi_graph_) hipGraphDestroy(multi_graph_);
+  invalidate();
   for (auto& e : events_) hipEventDestroy(e);
   if (comm_stream_) hipStreamDestroy(comm_stream_);
   if (aux_stream_) hipStreamDestroy(aux_stream_);
@@ -114,11 +111,12 @@ int Trainer::conv_params() const { return model_conv_params(model_); }
 int Trainer::conv_slabs() const { return model_ == ModelKind::LENET ? lenet_conv_bwd_blocks(batch_, bwd_blocks_) : 0; }
 
 void Trainer::invalidate() {
-  if (exec_) { hipGraphExecDestroy(exec_); exec_ = nullptr; }
-  if (graph_) { hipGraphDestroy(graph_); graph_ = nullptr; }
-  if (multi_exec_) { hipGraphExecDestroy(multi_exec_); multi_exec_ = nullptr; }
-  if (multi_graph_) { hipGraphDestroy(multi_graph_); multi_graph_ = nullptr; }
-  multi_steps_ = 0;
+  if (graphs_.empty()) return;
+  // a replay of one of these graphs may still be running: let it drain before its exec is destroyed
+  // (configuration changes only, never in the step loop)
+  (void)hipDeviceSynchronize();
+  for (auto& kv : graphs_) drop(kv.second);
+  graphs_.clear();
 }
 
 BatchRef Trainer::batch_ref(int B) const {
@@ -422,30 +420,58 @@ void Trainer::capture_into(hipStream_t s, int nsteps, hipGraph_t* graph, hipGrap
   trace("capture: done");
 }
 
+void Trainer::drop(GraphSlot& g) {
+  if (g.exec) hipGraphExecDestroy(g.exec);
+  if (g.graph) hipGraphDestroy(g.graph);
+  g = GraphSlot{};
+}
+
+// Graphs are cached per (schedule, steps): switching plan / concurrent / conv_bwd grid selects a
+// different cached graph instead of re-capturing, so a calibration can interleave the candidates'
+// replays back to back; anything that changes the kernels' arguments clears the cache (invalidate).
+uint64_t Trainer::schedule_key(int nsteps) const {
+  return (static_cast<uint64_t>(nsteps) << 32) | (static_cast<uint64_t>(bwd_blocks_) << 3) |
+         (static_cast<uint64_t>(concurrent_) << 2) | static_cast<uint64_t>(plan_);
+}
+
+const Trainer::GraphSlot* Trainer::find_graph(int nsteps) const {
+  auto it = graphs_.find(schedule_key(nsteps));
+  return it == graphs_.end() || !it->second.exec ? nullptr : &it->second;
+}
+
 void Trainer::capture(uintptr_t stream) {
-  invalidate();
-  capture_into(S(stream), 1, &graph_, &exec_);
+  GraphSlot& g = graphs_[schedule_key(1)];
+  if (g.exec) HIP_CHECK(hipStreamSynchronize(S(stream)));  // re-capture: the old exec may be in flight
+  drop(g);
+  capture_into(S(stream), 1, &g.graph, &g.exec);
 }
 
 // k consecutive steps in ONE graph: consecutive steps are plain stream-order edges inside it, so the
-// per-launch gap between graphs (~5 us measured between step graphs) is paid once per k steps; the
-// device step counter addresses every step's batch, so the graph stays valid for any k-step window.
+// per-launch gap between graphs is paid once per k steps; the device step counter addresses every
+// step's batch, so the graph stays valid for any k-step window.
 void Trainer::capture_multi(uintptr_t stream, int k) {
-  if (k < 1) throw std::invalid_argument("capture_multi: k must be >= 1");
-  if (multi_exec_) { hipGraphExecDestroy(multi_exec_); multi_exec_ = nullptr; }
-  if (multi_graph_) { hipGraphDestroy(multi_graph_); multi_graph_ = nullptr; }
-  capture_into(S(stream), k, &multi_graph_, &multi_exec_);
-  multi_steps_ = k;
+  if (k < 2) throw std::invalid_argument("capture_multi: k must be >= 2");
+  GraphSlot& g = graphs_[schedule_key(k)];
+  if (g.exec) HIP_CHECK(hipStreamSynchronize(S(stream)));
+  drop(g);
+  capture_into(S(stream), k, &g.graph, &g.exec);
+  multi_k_ = k;
 }
 
+int Trainer::multi_steps() const { return multi_k_ > 1 && find_graph(multi_k_) ? multi_k_ : 0; }
+
+bool Trainer::captured() const { return find_graph(1) != nullptr; }
+
 void Trainer::replay(uintptr_t stream) {
-  if (!exec_) throw std::runtime_error("replay: no captured graph");
-  HIP_CHECK(hipGraphLaunch(exec_, S(stream)));
+  const GraphSlot* g = find_graph(1);
+  if (!g) throw std::runtime_error("replay: no captured graph for the current schedule");
+  HIP_CHECK(hipGraphLaunch(g->exec, S(stream)));
   if (sync_debug()) HIP_CHECK(hipStreamSynchronize(S(stream)));
 }
 
 void Trainer::replay_multi(uintptr_t stream) {
-  if (!multi_exec_) throw std::runtime_error("replay_multi: no captured multi-step graph");
-  HIP_CHECK(hipGraphLaunch(multi_exec_, S(stream)));
+  const GraphSlot* g = multi_k_ > 1 ? find_graph(multi_k_) : nullptr;
+  if (!g) throw std::runtime_error("replay_multi: no captured multi-step graph for the current schedule");
+  HIP_CHECK(hipGraphLaunch(g->exec, S(stream)));
   if (sync_debug()) HIP_CHECK(hipStreamSynchronize(S(stream)));
 }

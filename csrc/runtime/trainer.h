@@ -43,8 +43,8 @@ class Trainer {
   Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const TrainerPtrs& p);
   ~Trainer();
 
-  void set_comm(std::shared_ptr<RcclComm> c) { comm_ = std::move(c); }
-  void set_world(int w) { world_ = w; }
+  void set_comm(std::shared_ptr<RcclComm> c) { comm_ = std::move(c); invalidate(); }
+  void set_world(int w) { world_ = w; invalidate(); }
   void set_optimizer(float lr, float momentum) { lr_ = lr; momentum_ = momentum; invalidate(); }
   void set_dropout(float p, uint32_t seed) { drop_p_ = p; seed_ = seed; invalidate(); }
   void set_buckets(const std::vector<Bucket>& b) { buckets_ = b; invalidate(); }
@@ -52,11 +52,10 @@ class Trainer {
   void set_plan(int p) {
     if (p != 0 && p != 1) throw std::invalid_argument("plan must be 0 (join) or 1 (split)");
     plan_ = static_cast<Plan>(p);
-    invalidate();
   }
   int plan() const { return static_cast<int>(plan_); }
   // single-GPU LeNet schedule: FC wgrad + FC update on the aux stream beside conv_bwd (true) or serial
-  void set_concurrent(bool on) { concurrent_ = on; invalidate(); }
+  void set_concurrent(bool on) { concurrent_ = on; }
   bool concurrent() const { return concurrent_; }
   // conv_bwd workgroup target (0 = default); the grid actually used for the full batch is bwd_grid()
   void set_bwd_blocks(int n) {
@@ -64,7 +63,6 @@ class Trainer {
     if (lenet_conv_bwd_max_blocks(batch_, n) > max_conv_slabs_)
       throw std::invalid_argument("set_bwd_blocks: more conv_bwd workgroups than conv slab rows");
     bwd_blocks_ = n;
-    invalidate();
   }
   int bwd_blocks() const { return bwd_blocks_; }
   int bwd_grid() const;
@@ -86,15 +84,16 @@ class Trainer {
   void eval_batch(uintptr_t images, uintptr_t labels, uintptr_t idx, int B, uintptr_t metrics,
                   uintptr_t stream);
 
-  // hipGraph of train_step(batch) captured on `stream`, replayed by replay().
+  // hipGraph of train_step(batch) under the current schedule (plan, concurrent, conv_bwd grid),
+  // captured on `stream`, replayed by replay().  Graphs are cached per schedule.
   void capture(uintptr_t stream);
   void replay(uintptr_t stream);
-  bool captured() const { return exec_ != nullptr; }
+  bool captured() const;
   // k consecutive full-batch steps in one hipGraph (one launch per k steps)
   void capture_multi(uintptr_t stream, int k);
   void replay_multi(uintptr_t stream);
-  int multi_steps() const { return multi_steps_; }
-  void invalidate();
+  int multi_steps() const;  // k of the multi-step graph of the current schedule, 0 if none
+  void invalidate();        // drop every cached graph
 
   int nparam() const { return nparam_; }
   int pack_size() const;
@@ -108,7 +107,14 @@ class Trainer {
   LenetConvBuffers conv_buffers() const;
   void launch_step(int B, hipStream_t s);
   void launch_lenet_comm_tail(int B, int nslab, int splits, hipStream_t s);
+  struct GraphSlot {
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+  };
   void capture_into(hipStream_t s, int nsteps, hipGraph_t* graph, hipGraphExec_t* exec);
+  static void drop(GraphSlot& g);
+  uint64_t schedule_key(int nsteps) const;
+  const GraphSlot* find_graph(int nsteps) const;
   std::vector<Bucket> coalesced_buckets() const;
   void all_reduce(const std::vector<Bucket>& bs, int phase, hipStream_t s);
 
@@ -128,11 +134,8 @@ class Trainer {
   hipStream_t comm_stream_ = nullptr;
   hipStream_t aux_stream_ = nullptr;  // concurrent FC wgrad branch (fork/join inside the step graph)
   std::vector<hipEvent_t> events_;
-  hipGraph_t graph_ = nullptr;
-  hipGraphExec_t exec_ = nullptr;
-  hipGraph_t multi_graph_ = nullptr;
-  hipGraphExec_t multi_exec_ = nullptr;
-  int multi_steps_ = 0;
+  std::map<uint64_t, GraphSlot> graphs_;
+  int multi_k_ = 0;
   int zero_step_dev_ = 0;
   int32_t* zero_counter_ = nullptr;  // device {0,0} for eval batch addressing
 };

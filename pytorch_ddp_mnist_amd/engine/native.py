@@ -229,7 +229,7 @@ class NativeTrainer:
         if "plan" in cfg or "bwd_blocks" in cfg:
             self.set_plan(cfg.get("plan", self.plan), int(cfg.get("bwd_blocks", 0)))
 
-    def autotune_plan(self, candidates=None, iters: int = 12, warmup: int = 3, reduce_max=None,
+    def autotune_plan(self, candidates=None, iters: int = 16, warmup: int = 3, reduce_max=None,
                       margin: float = 0.015, log=None) -> dict:
         """Time each candidate step schedule and keep the fastest (a start-up calibration, like
         cudnn.benchmark).
@@ -237,13 +237,18 @@ class NativeTrainer:
         With a communicator the candidates are the multi-GPU plans (JOIN / SPLIT / SPLIT with a
         capped conv_bwd grid, :func:`~pytorch_ddp_mnist_amd.parallel.ddp.default_plan_candidates`),
         timed on the real communicator; without one, the single-GPU LeNet schedules
-        (:func:`~pytorch_ddp_mnist_amd.parallel.ddp.local_plan_candidates`).  Every candidate replays
-        the captured step ``warmup + iters`` times on batch 0 of the loaded epoch order (the device
-        step counter is rewound after each replay), so all ranks issue the same collectives in the
-        same order; per-replay GPU times come from events on the step stream and ``reduce_max``
-        (e.g. a gloo MAX all-reduce) makes the decision identical on every rank.  Parameters,
-        momentum, counters and metrics are restored afterwards.  ``MNIST_AMD_MG_SCHED=join|split``
-        pins the multi-GPU plan.
+        (:func:`~pytorch_ddp_mnist_amd.parallel.ddp.local_plan_candidates`).
+
+        Every candidate's step graph (and its k-step graph) is captured first -- graphs are cached
+        per schedule -- and then the candidates' replays are INTERLEAVED round-robin (rotating the
+        order each round) with no host sync in between: the GPU clock ramps up during the first
+        milliseconds of work, and timing candidate A entirely before candidate B would hand B the
+        faster clock.  Each replay trains on batch 0 of the loaded epoch order (the device step
+        counter is rewound), so all ranks issue the same collectives in the same order; per-replay
+        GPU times come from events on the step stream and ``reduce_max`` (e.g. a gloo MAX
+        all-reduce) makes the decision identical on every rank.  Parameters, momentum, counters and
+        metrics are restored afterwards, and the chosen schedule's graphs are left ready to replay.
+        ``MNIST_AMD_MG_SCHED=join|split`` pins the multi-GPU plan.
         """
         from ..parallel.ddp import choose_plan, default_plan_candidates, local_plan_candidates
         forced = os.environ.get("MNIST_AMD_MG_SCHED")
@@ -264,23 +269,30 @@ class NativeTrainer:
         self.synchronize()
         saved = [t.clone() for t in (self.params, self.mom, self.grad, self.step_ctr, self.metrics)]
         self._sync_in()
-        timings = {}
         st = self.stream
-        for name, cfg in candidates.items():
-            self.apply_plan(cfg)
-            self.capture()
-            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                  for _ in range(warmup + iters)]
-            with torch.cuda.stream(st):
-                self.step_ctr[0].zero_()  # every replay trains on batch 0 of the loaded order
-            for a, b in ev:
+        names = list(candidates)
+        for name in names:                 # all captures (host work) before any timed replay
+            self.apply_plan(candidates[name])
+            self.prepare_graphs()
+        ev = {name: [] for name in names}
+        with torch.cuda.stream(st):
+            self.step_ctr[0].zero_()       # every replay trains on batch 0 of the loaded order
+        for r in range(warmup + iters):
+            order = names[r % len(names):] + names[:r % len(names)]
+            for name in order:
+                self.apply_plan(candidates[name])   # host-side switch to the cached graph
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record(st)
                 self.rt.replay(st.cuda_stream)
                 b.record(st)
                 with torch.cuda.stream(st):
                     self.step_ctr[0].zero_()
-            self.synchronize()
-            ts = sorted(a.elapsed_time(b) for a, b in ev[warmup:])
+                if r >= warmup:
+                    ev[name].append((a, b))
+        self.synchronize()
+        timings = {}
+        for name in names:
+            ts = sorted(a.elapsed_time(b) for a, b in ev[name])
             med = ts[len(ts) // 2]
             timings[name] = reduce_max(med) if reduce_max is not None else med
         with torch.cuda.stream(st):
@@ -289,9 +301,8 @@ class NativeTrainer:
         self.rt.pack(st.cuda_stream)
         chosen = choose_plan(timings, prefer=prefer, margin=margin)
         self.apply_plan(candidates[chosen])
-        self.synchronize()
         out = {"chosen": chosen, "timings_ms": {k: round(v, 4) for k, v in timings.items()},
-               "candidates": candidates}
+               "candidates": candidates, "replays_per_candidate": iters, "interleaved": True}
         if log is not None:
             log(out)
         return out
@@ -342,11 +353,23 @@ class NativeTrainer:
         else:
             self.rt.train_step(B, self.stream.cuda_stream)
 
+    @staticmethod
+    def graph_steps() -> int:
+        return int(os.environ.get("MNIST_AMD_GRAPH_STEPS", "8"))
+
+    def prepare_graphs(self, k: Optional[int] = None) -> None:
+        """Capture + instantiate the single-step and the k-step graph now (setup, not step time)."""
+        k = self.graph_steps() if k is None else int(k)
+        if not self.rt.captured:
+            self.capture()
+        if k > 1 and self.rt.multi_steps != k:
+            self.rt.capture_multi(self.stream.cuda_stream, k)
+
     def run_steps(self, n: int, use_graph: bool = True, k: Optional[int] = None) -> None:
         """``n`` consecutive full-batch steps.  With graphs, runs of ``k`` steps are ONE hipGraph launch
         (``MNIST_AMD_GRAPH_STEPS``, default 8; the graph launch gap is paid once per k steps), the
         remainder single-step graphs.  Same kernels, same order, same results as ``n`` x :meth:`step`."""
-        k = int(os.environ.get("MNIST_AMD_GRAPH_STEPS", "8")) if k is None else int(k)
+        k = self.graph_steps() if k is None else int(k)
         if not use_graph or k <= 1:
             for _ in range(n):
                 self.step(self.batch, use_graph)

@@ -142,8 +142,11 @@ class NativeEngine:
         every = getattr(progress, "every", 0) if progress is not None else 0
         prev = 0.0
         with range_("train_full_batches"):
-            if not every and not self.torch_comm:
+            if not every and not self.torch_comm and not self.fault.active:
+                if self.use_graph:
+                    tr.prepare_graphs()
                 tr.run_steps(nfull, use_graph=self.use_graph)   # k-step graph launches
+                self.fault.step += nfull
                 nfull_loop = 0
             else:
                 nfull_loop = nfull

@@ -148,4 +148,5 @@ def test_multi_step_graph_matches_single_steps(native, small_mnist, model_name, 
         out.append((tr.params.cpu(), tr.read_metrics().loss_sum))
         if k == 4:
             assert tr.rt.multi_steps == 4
-    assert torch.equal(out[0][0], out[1][0]) and out[0][1] == out[1][1]
+    assert torch.equal(out[0][0], out[1][0])
+    assert out[0][1] == pytest.approx(out[1][1], rel=1e-6)   # loss sum: float atomics, order-dependent
