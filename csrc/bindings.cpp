@@ -138,6 +138,7 @@ PYBIND11_MODULE(_C, m) {
       .def("eval_batch", &Trainer::eval_batch)
       .def("capture", &Trainer::capture)
       .def("replay", &Trainer::replay)
+      .def_property("fuse_wgrad_sgd", &Trainer::fuse_wgrad_sgd, &Trainer::set_fuse_wgrad_sgd)
       .def("capture_multi", &Trainer::capture_multi)
       .def("replay_multi", &Trainer::replay_multi)
       .def_property_readonly("multi_steps", &Trainer::multi_steps)

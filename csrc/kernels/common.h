@@ -86,7 +86,40 @@ DEV float mnist_norm(uint32_t u8) { return (float(u8) * (1.0f / 255.0f) - 0.1307
 DEV int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
 // wave-level reductions (64 lanes)
+// DPP lane exchanges inside a 16-lane row (a few cycles each; __shfl_xor is a ds_bpermute through the
+// LDS crossbar, ~100 cycles).  Butterfly for row reductions: quad xor 1, quad xor 2, half-row mirror,
+// row mirror -- every lane of the row ends with the same (commutatively combined) value.
+template <int CTRL>
+DEV int dpp_i(int v) { return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false); }
+template <int CTRL>
+DEV float dpp_f(float v) { return __builtin_bit_cast(float, dpp_i<CTRL>(__builtin_bit_cast(int, v))); }
+constexpr int DPP_QXOR1 = 0xB1, DPP_QXOR2 = 0x4E, DPP_HMIRROR = 0x141, DPP_MIRROR = 0x140;
+
+DEV float row16_max(float v) {
+  v = fmaxf(v, dpp_f<DPP_QXOR1>(v));
+  v = fmaxf(v, dpp_f<DPP_QXOR2>(v));
+  v = fmaxf(v, dpp_f<DPP_HMIRROR>(v));
+  return fmaxf(v, dpp_f<DPP_MIRROR>(v));
+}
+DEV float row16_sum(float v) {
+  v += dpp_f<DPP_QXOR1>(v);
+  v += dpp_f<DPP_QXOR2>(v);
+  v += dpp_f<DPP_HMIRROR>(v);
+  return v + dpp_f<DPP_MIRROR>(v);
+}
+DEV int row16_min(int v) {
+  v = min(v, dpp_i<DPP_QXOR1>(v));
+  v = min(v, dpp_i<DPP_QXOR2>(v));
+  v = min(v, dpp_i<DPP_HMIRROR>(v));
+  return min(v, dpp_i<DPP_MIRROR>(v));
+}
+
+DEV float lane_f(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+
+// sum over the 64 lanes (every lane active); the result is wave-uniform
 DEV float wave_sum(float v) {
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v = row16_sum(v);
+  return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48));
 }

@@ -17,6 +17,7 @@
 // masks, padding and the transposed global stores.
 #include <algorithm>
 #include <cstdlib>
+#include <stdexcept>
 
 #include "common.h"
 #include "launch.h"
@@ -24,15 +25,19 @@
 
 namespace {
 
-template <typename T, class H, int MT>
+template <typename T, class H, int MT, bool PRE = false>
 struct HeadSmem {
   static constexpr int R = MT * 16;
+  // fp32 (one k per MFMA input register): the dgrad products read W2 / W3 themselves with a k-strided
+  // access, so their transposed images are not staged (FT) and the weights fit in LDS next to the tile
+  static constexpr bool FT = sizeof(T) == 4;
   static constexpr int PX = H::K0P + 8;
+  static constexpr int XROWS = PRE ? 0 : R;  // PRE: layer 1 ran in l1_split_kernel, X is never staged
   static constexpr int P1 = H::N1P + 8;
   static constexpr int P2 = H::N2P + 8;
   static constexpr int PD = H::NCK + 8;
   static constexpr int OFF_X = 0;
-  static constexpr int OFF_H1 = rup(OFF_X + R * PX * (int)sizeof(T), 16);
+  static constexpr int OFF_H1 = rup(OFF_X + XROWS * PX * (int)sizeof(T), 16);
   static constexpr int OFF_H2 = rup(OFF_H1 + R * P1 * (int)sizeof(T), 16);
   static constexpr int OFF_D = rup(OFF_H2 + R * P2 * (int)sizeof(T), 16);
   static constexpr int OFF_L = rup(OFF_D + R * PD * (int)sizeof(T), 16);
@@ -44,12 +49,14 @@ struct HeadSmem {
   // Layer-2/3 weights (forward and dgrad operand images) staged once per workgroup, rows padded by 8
   // elements (<= 2-way ds_read_b128 conflicts), when they fit beside the activations: every phase
   // after L1 then reads its B operand from LDS instead of waiting on an L2/MALL round trip.
-  static constexpr int PW2 = H::N1P + 8, PW2T = H::N2P + 8, PW3 = H::N2P + 8, PW3T = H::NCK + 8;
+  // (FT: pitch = 4 mod 8 dwords, so the 4 k-rows a k-strided fragment spans land on different banks)
+  static constexpr int PW2 = H::N1P + (FT ? 4 : 8), PW2T = H::N2P + 8, PW3 = H::N2P + (FT ? 4 : 8),
+                       PW3T = H::NCK + 8;
   static constexpr int OFF_W2 = BASE_END;                                          // [N2P][PW2]
-  static constexpr int OFF_W2T = rup(OFF_W2 + H::N2P * PW2 * (int)sizeof(T), 16);  // [N1P][PW2T]
-  static constexpr int OFF_W3 = rup(OFF_W2T + H::N1P * PW2T * (int)sizeof(T), 16); // [16][PW3]
-  static constexpr int OFF_W3T = rup(OFF_W3 + 16 * PW3 * (int)sizeof(T), 16);      // [N2P][PW3T]
-  static constexpr int W_END = rup(OFF_W3T + H::N2P * PW3T * (int)sizeof(T), 16);
+  static constexpr int OFF_W2T = rup(OFF_W2 + H::N2P * PW2 * (int)sizeof(T), 16);  // [N1P][PW2T] (not FT)
+  static constexpr int OFF_W3 = rup(OFF_W2T + (FT ? 0 : H::N1P * PW2T * (int)sizeof(T)), 16); // [16][PW3]
+  static constexpr int OFF_W3T = rup(OFF_W3 + 16 * PW3 * (int)sizeof(T), 16);      // [N2P][PW3T] (not FT)
+  static constexpr int W_END = rup(OFF_W3T + (FT ? 0 : H::N2P * PW3T * (int)sizeof(T)), 16);
   static constexpr bool WLDS = W_END <= 160 * 1024;
   static constexpr int TOTAL = WLDS ? W_END : BASE_END;
   static constexpr bool FITS = TOTAL <= 160 * 1024;
@@ -66,14 +73,30 @@ DEV void store_col4(T* base, float a, float b, float c, float d) {
   }
 }
 
-// copy a [rows][cols] T matrix (cols a multiple of 16 B) into LDS with row pitch `pitch`
-template <typename T, int NT>
-DEV void stage_rows(T* dst, const T* src, int rows, int cols, int pitch, int tid) {
-  constexpr int VE = 16 / (int)sizeof(T);
-  const int cv = cols / VE;
-  for (int e = tid; e < rows * cv; e += NT) {
-    const int r = e / cv, c = (e % cv) * VE;
-    *reinterpret_cast<uint4*>(dst + r * pitch + c) = *reinterpret_cast<const uint4*>(src + r * cols + c);
+// MFMA B fragment whose KV consecutive k values sit `pitch` elements apart (one k per row)
+template <typename T>
+DEV typename Mma<T>::Frag load_kstrided(const T* p, int pitch) {
+  typename Mma<T>::Frag f;
+#pragma unroll
+  for (int j = 0; j < Mma<T>::KV; ++j) Mma<T>::set(f, j, to_f(p[j * pitch]));
+  return f;
+}
+
+// copy a [ROWS][COLS] T matrix (COLS a multiple of 16 B) into LDS with row pitch PITCH: every global
+// load of the thread is issued before its first LDS store (one latency, not one per row chunk)
+template <typename T, int NT, int ROWS, int COLS, int PITCH>
+DEV void stage_rows(T* dst, const T* src, int tid) {
+  constexpr int VE = 16 / (int)sizeof(T), CV = COLS / VE, N = ROWS * CV, IT = (N + NT - 1) / NT;
+  uint4 v[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int e = min(tid + i * NT, N - 1);
+    v[i] = *reinterpret_cast<const uint4*>(src + (e / CV) * COLS + (e % CV) * VE);
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int e = tid + i * NT;
+    if (e < N) *reinterpret_cast<uint4*>(dst + (e / CV) * PITCH + (e % CV) * VE) = v[i];
   }
 }
 
@@ -84,7 +107,7 @@ DEV void stage_rows(T* dst, const T* src, int rows, int cols, int pitch, int tid
 //   largest) are fetched into registers while softmax, dH2 and dH1 run.
 template <typename T, class H, int MT, bool TRAIN, bool PRE, int NWV = 4>
 __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers hb) {
-  using S = HeadSmem<T, H, MT>;
+  using S = HeadSmem<T, H, MT, PRE>;
   using M = Mma<T>;
   using Frag = typename M::Frag;
   constexpr int R = S::R, KV = M::KV, KC = M::KC, NTH = NWV * 64;
@@ -127,6 +150,19 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   constexpr int LW2 = S::WLDS ? S::PW2 : H::N1P, LW2T = S::WLDS ? S::PW2T : H::N2P;
   constexpr int LW3 = S::WLDS ? S::PW3 : H::N2P, LW3T = S::WLDS ? S::PW3T : H::NCK;
 
+  // ---- PRE: this thread's layer-1 partial sums (written by l1_split_kernel), issued first: their
+  //      latency overlaps the weight staging instead of following it
+  constexpr int PE = PRE ? (H::N1P * R + NTH - 1) / NTH : 1;
+  float zpre[PE][L1_KSPLIT];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int j = 0; j < PE; ++j) {
+      const int e = min(tid + j * NTH, H::N1P * R - 1), n = e / R, rg = r0 + e % R;
+#pragma unroll
+      for (int q = 0; q < L1_KSPLIT; ++q) zpre[j][q] = hb.z1p[((size_t)q * H::N1P + n) * ldB + rg];
+    }
+  }
+
   // ---- L1 operands of this wave's first n-tile: issued first, in flight during the staging
   constexpr int NT1 = H::N1P / 16, KCH1 = H::K0P / KC;
   constexpr bool PF1 = !PRE && KCH1 <= 16;  // <= 64 VGPRs of prefetched fragments (LeNet bf16: 13 chunks)
@@ -142,12 +178,12 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   // ---- staging: indices, weights, biases (+ the input tile; the MLP gather needs sIdx first)
   if (tid < R) sIdx[tid] = (r0 + tid < B) ? idx[r0 + tid] : -1;
   if constexpr (S::WLDS) {
-    stage_rows<T, NTH>(reinterpret_cast<T*>(smem + S::OFF_W2), pack + H::F2, H::N2P, H::N1P, S::PW2, tid);
-    if constexpr (TRAIN) {
-      stage_rows<T, NTH>(reinterpret_cast<T*>(smem + S::OFF_W2T), pack + H::F2T, H::N1P, H::N2P, S::PW2T, tid);
-      stage_rows<T, NTH>(reinterpret_cast<T*>(smem + S::OFF_W3T), pack + H::F3T, H::N2P, H::NCK, S::PW3T, tid);
+    stage_rows<T, NTH, H::N2P, H::N1P, S::PW2>(reinterpret_cast<T*>(smem + S::OFF_W2), pack + H::F2, tid);
+    if constexpr (TRAIN && !S::FT) {
+      stage_rows<T, NTH, H::N1P, H::N2P, S::PW2T>(reinterpret_cast<T*>(smem + S::OFF_W2T), pack + H::F2T, tid);
+      stage_rows<T, NTH, H::N2P, H::NCK, S::PW3T>(reinterpret_cast<T*>(smem + S::OFF_W3T), pack + H::F3T, tid);
     }
-    stage_rows<T, NTH>(reinterpret_cast<T*>(smem + S::OFF_W3), pack + H::F3, 16, H::N2P, S::PW3, tid);
+    stage_rows<T, NTH, 16, H::N2P, S::PW3>(reinterpret_cast<T*>(smem + S::OFF_W3), pack + H::F3, tid);
   }
   for (int e = tid; e < H::N1P + H::N2P + 16; e += NTH) {
     float v = 0.f;
@@ -218,12 +254,14 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   if constexpr (PRE) {
     // sum the L1_KSPLIT partial products in a fixed order, then the same bias/ReLU/dropout epilogue
     T* h1T = reinterpret_cast<T*>(hb.h1T);
-    const float* zp = hb.z1p;
-    for (int e = tid; e < H::N1P * R; e += NTH) {
+#pragma unroll
+    for (int j = 0; j < PE; ++j) {
+      const int e = tid + j * NTH;
+      if (e >= H::N1P * R) break;
       const int n = e / R, r = e % R, rg = r0 + r;
       float z = 0.f;
 #pragma unroll
-      for (int q = 0; q < L1_KSPLIT; ++q) z += zp[((size_t)q * H::N1P + n) * ldB + rg];
+      for (int q = 0; q < L1_KSPLIT; ++q) z += zpre[j][q];
       float x = fmaxf(z + sB1[n], 0.f);
       if constexpr (H::DROPOUT && TRAIN) {
         const uint32_t h = hash4(hb.seed, (uint32_t)gstep, (uint32_t)rg, (uint32_t)n);
@@ -359,18 +397,13 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       const int r = t >> 4, c = t & 15, rg = r0 + r;
       const bool valid = rg < B;
       const float z = c < H::NC ? sLog[r * 16 + c] : -INFINITY;
-      float mx = z;
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 16));
-      int am = z == mx ? c : 16;
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) am = min(am, __shfl_xor(am, o, 16));
+      // row reductions over the 16 lanes of the row with DPP (the ds_bpermute shuffles were the phase)
+      const float mx = row16_max(z);
+      const int am = row16_min(z == mx ? c : 16);
       const float e = c < H::NC ? __expf(z - mx) : 0.f;
-      float se = e;
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) se += __shfl_xor(se, o, 16);
+      const float se = row16_sum(e);
       const int y = sLab[r];
-      const float zy = __shfl(z, (lane & 48) | y, 64);
+      const float zy = sLog[r * 16 + y];
       if (c == 0 && valid) {
         loss += mx + __logf(se) - zy;
         corr += (am == y) ? 1.f : 0.f;
@@ -414,17 +447,20 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
 
   // ---------------------------------------------------------------- dH2 = (dZ W3) * [H2 > 0]
   {
-    constexpr int NT = H::N2P / 16, KCH = H::NCK / KC;
+    // (FT: B[k = c][n] = W3[c][n] read k-strided from the W3 image; the zero dZ columns c >= 16
+    //  contribute nothing, so only the 16 staged rows are read)
+    constexpr bool TW3 = S::FT && S::WLDS;
+    constexpr int NT = H::N2P / 16, KCH = (TW3 ? H::NCP : H::NCK) / KC;
     T* dy2T = reinterpret_cast<T*>(hb.dy2T);
     for (int nt = w; nt < NT; nt += NWV) {
       f32x4 acc[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = zero4();
-      const T* bp = bW3T + (nt * 16 + row) * LW3T + grp * KV;
+      const T* bp = TW3 ? bW3 + grp * KV * LW3 + nt * 16 + row : bW3T + (nt * 16 + row) * LW3T + grp * KV;
       const T* ap = sD + row * S::PD + grp * KV;
 #pragma unroll
       for (int kc = 0; kc < KCH; ++kc) {
-        const Frag b = M::load(bp + kc * KC);
+        const Frag b = TW3 ? load_kstrided<T>(bp + kc * KC * LW3, LW3) : M::load(bp + kc * KC);
 #pragma unroll
         for (int m = 0; m < MT; ++m) M::mma(acc[m], M::load(ap + m * 16 * S::PD + kc * KC), b);
       }
@@ -455,17 +491,18 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
 
   // ---------------------------------------------------------------- dH1 = (dH2 W2) * [H1 > 0] / keep
   {
+    constexpr bool TW2 = S::FT && S::WLDS;  // B[k = n2][n = n1] = W2[n2][n1], k-strided from the W2 image
     constexpr int NT = H::N1P / 16, KCH = H::N2P / KC;
     T* dy1T = reinterpret_cast<T*>(hb.dy1T);
     for (int nt = w; nt < NT; nt += NWV) {
       f32x4 acc[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = zero4();
-      const T* bp = bW2T + (nt * 16 + row) * LW2T + grp * KV;
+      const T* bp = TW2 ? bW2 + grp * KV * LW2 + nt * 16 + row : bW2T + (nt * 16 + row) * LW2T + grp * KV;
       const T* ap = sH2 + row * S::P2 + grp * KV;
 #pragma unroll
       for (int kc = 0; kc < KCH; ++kc) {
-        const Frag b = M::load(bp + kc * KC);
+        const Frag b = TW2 ? load_kstrided<T>(bp + kc * KC * LW2, LW2) : M::load(bp + kc * KC);
 #pragma unroll
         for (int m = 0; m < MT; ++m) M::mma(acc[m], M::load(ap + m * 16 * S::P2 + kc * KC), b);
       }
@@ -543,6 +580,15 @@ __global__ __launch_bounds__(256) void l1_split_kernel(BatchRef br, HeadBuffers 
   const int B = br.B, ldB = hb.ldB;
   T* xT = reinterpret_cast<T*>(hb.xT);
   const bool write_xT = TRAIN && ng == 0;
+  // this wave's W1 fragments of the K range, issued first: their latency hides behind the X gather
+  using Frag = typename M::Frag;
+  const int nt = ng * 4 + w;
+  const bool has_nt = nt * 16 < H::N1P;  // wave-uniform
+  const T* pack = reinterpret_cast<const T*>(hb.pack);
+  const T* bp = pack + H::F1 + (size_t)(min(nt, H::N1P / 16 - 1) * 16 + row) * H::K0P + grp * KV;
+  Frag bpre[QCH];
+#pragma unroll
+  for (int i = 0; i < QCH; ++i) bpre[i] = M::load(bp + min(c0 + i, KCH - 1) * KC);  // clamped: unused past c1
 
   for (int e = tid; e < 16 * (klen / 8); e += 256) {
     const int r = e & 15, kk = (e >> 4) * 8, k = k0 + kk, rg = r0 + r;
@@ -574,14 +620,20 @@ __global__ __launch_bounds__(256) void l1_split_kernel(BatchRef br, HeadBuffers 
   }
   __syncthreads();
 
-  const int nt = ng * 4 + w;
-  if (nt * 16 >= H::N1P) return;
-  const T* pack = reinterpret_cast<const T*>(hb.pack);
-  const T* bp = pack + H::F1 + (size_t)(nt * 16 + row) * H::K0P + grp * KV;
+  if (!has_nt) return;
   const T* ap = sX + row * XP + grp * KV;
-  f32x4 acc = zero4();
-#pragma unroll 4
-  for (int c = c0; c < c1; ++c) M::mma(acc, M::load(ap + (c - c0) * KC), M::load(bp + c * KC));
+  // two accumulators (even / odd chunks): half the dependent-MFMA chain
+  f32x4 acc0 = zero4(), acc1 = zero4();
+#pragma unroll
+  for (int i = 0; i < QCH; ++i) {
+    if (c0 + i < c1) {  // uniform: only the last K range is shorter
+      if (i & 1) M::mma(acc1, M::load(ap + i * KC), bpre[i]);
+      else M::mma(acc0, M::load(ap + i * KC), bpre[i]);
+    }
+  }
+  f32x4 acc;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = acc0[j] + acc1[j];
   float* out = hb.z1p + ((size_t)q * H::N1P + nt * 16 + row) * ldB + r0 + grp * 4;
   *reinterpret_cast<f32x4*>(out) = acc;
 }
@@ -607,9 +659,11 @@ struct WgArgs {
   // xcd_ch rows (= head rows per workgroup) -- so its operands hit the XCD's own L2.
   int xcd_ch, nch, sx;  // chunk rows, chunk count, splits per XCD
   float* slab;
+  SgdFuse sgd;          // used when fuse != 0 (then splits == 1)
+  int fuse;
 };
 
-template <typename T>
+template <typename T, class Model>
 __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
   using M = Mma<T>;
   using Frag = typename M::Frag;
@@ -691,6 +745,9 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
   }
 
   float* out = a.slab + (size_t)split * a.slab_ld + J.out_off;
+  // output element (mi, ni, i) -> parameter index within the job (slab rows are laid out by parameter
+  // index), -1 for padding
+  int qi[2][2][4];
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -699,15 +756,60 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int n = n0 + mi * 16 + grp * 4 + i;
-        if (n >= J.N) continue;
-        if (k < J.K) out[(size_t)n * J.K + k] = acc[mi][ni][i];
-        else if (k == J.K && J.bias) out[(size_t)J.N * J.K + n] = acc[mi][ni][i];
+        qi[mi][ni][i] = n >= J.N ? -1 : (k < J.K ? n * J.K + k : (k == J.K && J.bias ? J.N * J.K + n : -1));
       }
     }
+  if (!a.fuse) {
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (qi[mi][ni][i] >= 0) out[qi[mi][ni][i]] = acc[mi][ni][i];
+  } else {
+    // SGD epilogue: every parameter / momentum load of the tile is issued before the first store (the
+    // stores could alias later loads, so the compiler would otherwise serialise 16 round trips)
+    float pv[2][2][4], mv[2][2][4];
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int p = J.out_off + max(qi[mi][ni][i], 0);
+          pv[mi][ni][i] = a.sgd.params[p];
+          mv[mi][ni][i] = a.sgd.mom ? a.sgd.mom[p] : 0.f;
+        }
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (qi[mi][ni][i] < 0) continue;
+          const int p = J.out_off + qi[mi][ni][i];
+          float g = (0.f + acc[mi][ni][i]) * a.sgd.scale;  // = reduce_sgd over one slab
+          a.sgd.grad[p] = g;
+          if (a.sgd.mom) {
+            const float b = a.sgd.momentum * mv[mi][ni][i] + g;
+            a.sgd.mom[p] = b;
+            g = b;
+          }
+          const float nv = pv[mi][ni][i] - a.sgd.lr * g;
+          a.sgd.params[p] = nv;
+          Packer<Model, T>::pack(p, nv, reinterpret_cast<T*>(a.sgd.pack));
+        }
+  }
+  if (a.fuse && a.sgd.step_ptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    a.sgd.step_ptr[0] += 1;  // nothing after the head reads the batch counter in this step
+    a.sgd.step_ptr[1] += 1;
+  }
 }
 
-template <typename T, class H>
-int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab_ld, int xcd_ch, hipStream_t s) {
+template <typename T, class H, class Model>
+int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab_ld, int xcd_ch, hipStream_t s,
+                 const SgdFuse* fuse) {
   WgArgs<T> a{};
   auto mk = [&](int i, const void* dy, const void* x, int N, int K, int NP, bool bias, int off, int& blk) {
     WgJob<T>& J = a.job[i];
@@ -729,6 +831,11 @@ int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab
   splits = std::max(1, std::min(splits, a.Bp / KC));
   a.rlen = rup((a.Bp + splits - 1) / splits, KC);
   splits = (a.Bp + a.rlen - 1) / a.rlen;
+  if (fuse) {
+    if (splits != 1) throw std::invalid_argument("wgrad with the SGD epilogue needs one batch split");
+    a.sgd = *fuse;
+    a.fuse = 1;
+  }
   a.slab = slab;
   a.slab_ld = slab_ld;
   a.xcd_ch = 0;
@@ -738,9 +845,9 @@ int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab
     a.xcd_ch = xcd_ch;
     a.nch = (a.Bp + xcd_ch - 1) / xcd_ch;
     a.sx = splits / 8;
-    hipLaunchKernelGGL(wgrad_kernel<T>, dim3(blk * splits), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((wgrad_kernel<T, Model>), dim3(blk * splits), dim3(256), 0, s, a);
   } else {
-    hipLaunchKernelGGL(wgrad_kernel<T>, dim3(blk, splits), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((wgrad_kernel<T, Model>), dim3(blk, splits), dim3(256), 0, s, a);
   }
   return splits;
 }
@@ -847,12 +954,14 @@ int launch_head(ModelKind m, DType t, bool train, const BatchRef& br, const Head
 }
 
 int launch_head_wgrad(ModelKind m, DType t, const HeadBuffers& hb, int B, int splits, float* slab,
-                      int slab_ld, hipStream_t s, int head_rows) {
+                      int slab_ld, hipStream_t s, int head_rows, const SgdFuse* fuse) {
   // head_rows: batch rows per head workgroup for this B (0 = unknown: contiguous split mapping)
   if (m == ModelKind::MLP) {
-    if (t == DType::F32) return wgrad_launch<float, MlpModel::Head>(hb, B, splits, slab, slab_ld, head_rows, s);
-    return wgrad_launch<bf16, MlpModel::Head>(hb, B, splits, slab, slab_ld, head_rows, s);
+    if (t == DType::F32)
+      return wgrad_launch<float, MlpModel::Head, MlpModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse);
+    return wgrad_launch<bf16, MlpModel::Head, MlpModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse);
   }
-  if (t == DType::F32) return wgrad_launch<float, LenetModel::Head>(hb, B, splits, slab, slab_ld, head_rows, s);
-  return wgrad_launch<bf16, LenetModel::Head>(hb, B, splits, slab, slab_ld, head_rows, s);
+  if (t == DType::F32)
+    return wgrad_launch<float, LenetModel::Head, LenetModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse);
+  return wgrad_launch<bf16, LenetModel::Head, LenetModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse);
 }

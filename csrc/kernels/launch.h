@@ -62,8 +62,21 @@ int launch_head(ModelKind m, DType t, bool train, const BatchRef& br, const Head
                  int rows_per_block, hipStream_t s);
 
 // Grouped weight-gradient GEMM over the batch (split-K over rows): writes S slabs, returns S.
+// Optional SGD epilogue of the weight-gradient GEMM (one GPU, ONE batch split: each output element is
+// the whole gradient): g = scale * dW, momentum, parameter, packed operand images and the device step
+// counters updated in place -- the separate reduce + SGD kernel and its boundary disappear.  Bitwise
+// equal to the wgrad -> reduce_sgd pair (a one-slab reduce is scale * dW).
+struct SgdFuse {
+  float scale, lr, momentum;
+  float* params;
+  float* grad;
+  float* mom;
+  void* pack;
+  int32_t* step_ptr;
+};
+
 int launch_head_wgrad(ModelKind m, DType t, const HeadBuffers& hb, int B, int splits, float* slab,
-                       int slab_ld, hipStream_t s, int head_rows = 0);
+                       int slab_ld, hipStream_t s, int head_rows = 0, const SgdFuse* fuse = nullptr);
 
 void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetConvBuffers& cb,
                            hipStream_t s);

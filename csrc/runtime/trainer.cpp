@@ -294,6 +294,15 @@ void Trainer::launch_step(int B, hipStream_t s) {
     return;
   }
 
+  if (model_ == ModelKind::MLP && !comm_ && fc_splits_ == 1 && fuse_wgrad_sgd_) {
+    // one GPU, one batch split: the SGD update is the wgrad kernel's epilogue (no reduce_sgd kernel)
+    const SgdFuse f{scale, lr_, momentum_, ptr<float>(p_.params), ptr<float>(p_.grad),
+                    momentum_ != 0.f ? ptr<float>(p_.mom) : nullptr,  // as launch_reduce_sgd
+                    ptr<void>(p_.pack), ptr<int32_t>(p_.step)};
+    launch_head_wgrad(model_, dtype_, hb, B, 1, ptr<float>(p_.slab_fc), nparam_, s, hrows, &f);
+    post_launch(s);
+    return;
+  }
   const int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s, hrows);
   post_launch(s);
   int nslab = 0;

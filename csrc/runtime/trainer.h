@@ -57,6 +57,9 @@ class Trainer {
   // single-GPU LeNet schedule: FC wgrad + FC update on the aux stream beside conv_bwd (true) or serial
   void set_concurrent(bool on) { concurrent_ = on; }
   bool concurrent() const { return concurrent_; }
+  // MLP, one GPU, one FC batch split: SGD as the wgrad kernel's epilogue (true) or wgrad + reduce_sgd
+  void set_fuse_wgrad_sgd(bool on) { fuse_wgrad_sgd_ = on; invalidate(); }
+  bool fuse_wgrad_sgd() const { return fuse_wgrad_sgd_; }
   // conv_bwd workgroup target (0 = default); the grid actually used for the full batch is bwd_grid()
   void set_bwd_blocks(int n) {
     n = n < 0 ? 0 : n;
@@ -127,6 +130,7 @@ class Trainer {
   int world_ = 1;
   Plan plan_ = Plan::JOIN;
   bool concurrent_ = true;
+  bool fuse_wgrad_sgd_ = true;
   int bwd_blocks_ = 0;
   int max_conv_slabs_ = 0;  // rows of the conv slab (lenet_conv_bwd_max_blocks(batch) at the default target)
   std::shared_ptr<RcclComm> comm_;

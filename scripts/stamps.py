@@ -19,9 +19,10 @@ from pytorch_ddp_mnist_amd.models import build_model  # noqa: E402
 
 B = int(os.environ.get("STAMP_BATCH", "8192"))
 model = os.environ.get("STAMP_MODEL", "lenet5")
+dtype = os.environ.get("STAMP_DTYPE", "bf16")
 x, y = make_split(60000, seed=1)
 dev = torch.device("cuda", 0)
-tr = NativeTrainer(model, "bf16", B, torch.from_numpy(x.reshape(-1, 784)).to(dev), torch.from_numpy(y).to(dev),
+tr = NativeTrainer(model, dtype, B, torch.from_numpy(x.reshape(-1, 784)).to(dev), torch.from_numpy(y).to(dev),
                    device=dev, lr=0.05, momentum=0.9, dropout=0.0, init=build_model(model))
 tr.set_epoch_indices(torch.randperm(60000, dtype=torch.int32)[: (60000 // B) * B])
 tr.reset_metrics()
@@ -45,8 +46,13 @@ def report(title, st, names, last):
     print(f"  {'total':16s} mean {tot.mean():7.2f} us  min {tot.min():7.2f}  max {tot.max():7.2f}")
 
 
-nblk = (B + 63) // 64
-report("head", allst[:nblk], ["idx+stage X", "L1", "L2", "L3", "softmax", "dH2", "dH1", "dX"], 8)
+rows = 16 if B <= tr.C.L1_SPLIT_MAX_B else 64  # split path: 16-row tiles
+nblk = (B + rows - 1) // rows
+if model == "lenet5":
+    report("head", allst[:nblk], ["idx+stage X", "L1", "L2", "L3", "softmax", "dH2", "dH1", "dX"], 8)
+else:  # no dX phase: stamp 7 is never written, dH1 ends at stamp 8
+    allst[:nblk, 7] = allst[:nblk, 8]
+    report("head", allst[:nblk], ["idx+stage X", "L1", "L2", "L3", "softmax", "dH2", "dH1"], 8)
 if model == "lenet5":
     per_img = []
     for t in range(4):

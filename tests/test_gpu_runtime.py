@@ -150,3 +150,29 @@ def test_multi_step_graph_matches_single_steps(native, small_mnist, model_name, 
             assert tr.rt.multi_steps == 4
     assert torch.equal(out[0][0], out[1][0])
     assert out[0][1] == pytest.approx(out[1][1], rel=1e-6)   # loss sum: float atomics, order-dependent
+
+
+@pytest.mark.parametrize("momentum", [0.0, 0.9])
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_mlp_fused_wgrad_sgd_matches_separate_update(native, small_mnist, dtype, momentum):
+    """MLP one-GPU step with the SGD update as the wgrad epilogue == wgrad + reduce_sgd kernels, bitwise
+    (params, momentum, step counters), over full and partial batches, eager and captured."""
+    from pytorch_ddp_mnist_amd.engine.native import NativeTrainer
+    from pytorch_ddp_mnist_amd.models import build_model
+    x, y, _, _ = small_mnist
+    torch.manual_seed(0)
+    m = build_model("mlp")
+    idx = torch.randperm(len(y), generator=torch.Generator().manual_seed(3))[:128 * 4 + 40].to(torch.int32)
+    out = []
+    for fuse in (False, True):
+        tr = NativeTrainer("mlp", dtype, 128, torch.from_numpy(x.reshape(-1, 784)), torch.from_numpy(y),
+                           dropout=0.2, init=m, fc_splits=1, momentum=momentum)
+        tr.rt.fuse_wgrad_sgd = fuse
+        tr.set_epoch_indices(idx)
+        tr.run_steps(3, use_graph=True)
+        tr.step(128, use_graph=False)
+        tr.step(40, use_graph=False)
+        tr.synchronize()
+        out.append((tr.params.cpu(), tr.mom.cpu(), tr.step_ctr.cpu()))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    assert torch.equal(out[0][2], out[1][2]) and out[1][2].tolist()[:2] == [5, 5]
