@@ -574,6 +574,11 @@ __global__ __launch_bounds__(256) void l1_split_kernel(BatchRef br, HeadBuffers 
   __shared__ __attribute__((aligned(16))) T sX[16 * XP];
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
   const int r0 = blockIdx.x * 16, ng = blockIdx.y, q = blockIdx.z;
+  const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  auto stamp = [&](int k) {
+    if (hb.stamps && tid == 0 && lin < 512) hb.stamps[(3584 + lin) * 16 + k] = wall_clock64();
+  };
+  stamp(0);
   const int c0 = q * QCH, c1 = min(KCH, c0 + QCH);
   if (c0 >= c1) return;  // uniform per block
   const int k0 = c0 * KC, klen = (c1 - c0) * KC;
@@ -590,21 +595,33 @@ __global__ __launch_bounds__(256) void l1_split_kernel(BatchRef br, HeadBuffers 
 #pragma unroll
   for (int i = 0; i < QCH; ++i) bpre[i] = M::load(bp + min(c0 + i, KCH - 1) * KC);  // clamped: unused past c1
 
-  for (int e = tid; e < 16 * (klen / 8); e += 256) {
+  // MLP gather: a thread's row is tid & 15 in every iteration, so its sample index is loaded ONCE and
+  // every pixel load of the thread is issued before the first conversion (one idx -> pixels latency
+  // chain instead of one per iteration); addresses are clamped, invalid values masked at use
+  constexpr int GIT = (16 * (QCH * KC / 8) + 255) / 256;
+  uint2 gu[H::GATHER ? GIT : 1];
+  if constexpr (H::GATHER) {
+    const int32_t* idx = br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride;
+    const int sidx = idx[min(r0 + (tid & 15), B - 1)];
+#pragma unroll
+    for (int it = 0; it < GIT; ++it) {
+      const int k = k0 + ((tid + it * 256) >> 4) * 8;
+      gu[it] = *reinterpret_cast<const uint2*>(br.images + (size_t)sidx * 784 + min(k, H::K0 - 8));
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < (H::GATHER ? GIT : (16 * (QCH * KC / 8) + 255) / 256); ++it) {
+    const int e = tid + it * 256;
+    if (e >= 16 * (klen / 8)) break;
     const int r = e & 15, kk = (e >> 4) * 8, k = k0 + kk, rg = r0 + r;
     float v[8];
     if constexpr (H::GATHER) {
-      if (rg < B && k < H::K0) {
-        const int32_t* idx = br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride;
-        const uint2 u = *reinterpret_cast<const uint2*>(br.images + (size_t)idx[rg] * 784 + k);
+      const uint2 u = gu[H::GATHER ? it : 0];
+      const bool in = rg < B && k < H::K0;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          v[j] = mnist_norm((u.x >> (8 * j)) & 255u);
-          v[j + 4] = mnist_norm((u.y >> (8 * j)) & 255u);
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = 0.f;
+      for (int j = 0; j < 4; ++j) {
+        v[j] = in ? mnist_norm((u.x >> (8 * j)) & 255u) : 0.f;
+        v[j + 4] = in ? mnist_norm((u.y >> (8 * j)) & 255u) : 0.f;
       }
     } else {
       const T* xin = reinterpret_cast<const T*>(hb.xin);
@@ -619,6 +636,7 @@ __global__ __launch_bounds__(256) void l1_split_kernel(BatchRef br, HeadBuffers 
     }
   }
   __syncthreads();
+  stamp(1);
 
   if (!has_nt) return;
   const T* ap = sX + row * XP + grp * KV;
@@ -636,6 +654,7 @@ __global__ __launch_bounds__(256) void l1_split_kernel(BatchRef br, HeadBuffers 
   for (int j = 0; j < 4; ++j) acc[j] = acc0[j] + acc1[j];
   float* out = hb.z1p + ((size_t)q * H::N1P + nt * 16 + row) * ldB + r0 + grp * 4;
   *reinterpret_cast<f32x4*>(out) = acc;
+  stamp(2);
 }
 
 // ====================================================================================
@@ -661,9 +680,10 @@ struct WgArgs {
   float* slab;
   SgdFuse sgd;          // used when fuse != 0 (then splits == 1)
   int fuse;
+  unsigned long long* stamps;  // optional phase stamps (MNIST_AMD_STAMPS): slots [3072 + block][16]
 };
 
-template <typename T, class Model>
+template <typename T>
 __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
   using M = Mma<T>;
   using Frag = typename M::Frag;
@@ -759,66 +779,115 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
         qi[mi][ni][i] = n >= J.N ? -1 : (k < J.K ? n * J.K + k : (k == J.K && J.bias ? J.N * J.K + n : -1));
       }
     }
-  if (!a.fuse) {
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
+  for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
+    for (int ni = 0; ni < 2; ++ni)
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (qi[mi][ni][i] >= 0) out[qi[mi][ni][i]] = acc[mi][ni][i];
-  } else {
-    // SGD epilogue: every parameter / momentum load of the tile is issued before the first store (the
-    // stores could alias later loads, so the compiler would otherwise serialise 16 round trips)
-    float pv[2][2][4], mv[2][2][4];
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int p = J.out_off + max(qi[mi][ni][i], 0);
-          pv[mi][ni][i] = a.sgd.params[p];
-          mv[mi][ni][i] = a.sgd.mom ? a.sgd.mom[p] : 0.f;
-        }
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          if (qi[mi][ni][i] < 0) continue;
-          const int p = J.out_off + qi[mi][ni][i];
-          float g = (0.f + acc[mi][ni][i]) * a.sgd.scale;  // = reduce_sgd over one slab
-          a.sgd.grad[p] = g;
-          if (a.sgd.mom) {
-            const float b = a.sgd.momentum * mv[mi][ni][i] + g;
-            a.sgd.mom[p] = b;
-            g = b;
-          }
-          const float nv = pv[mi][ni][i] - a.sgd.lr * g;
-          a.sgd.params[p] = nv;
-          Packer<Model, T>::pack(p, nv, reinterpret_cast<T*>(a.sgd.pack));
-        }
-  }
-  if (a.fuse && a.sgd.step_ptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+      for (int i = 0; i < 4; ++i)
+        if (qi[mi][ni][i] >= 0) out[qi[mi][ni][i]] = acc[mi][ni][i];
+}
+
+// Weight-gradient GEMM + SGD update for one GPU and ONE batch split (small batches): every output
+// element is the whole gradient, so the update is the epilogue -- g = scale * dW, momentum, parameter,
+// packed operand images, device step counters -- and the separate reduce + SGD kernel disappears
+// (bitwise equal to wgrad -> reduce_sgd: a one-slab reduce is (0 + dW) * scale).  One 16x16 output tile
+// per wave and a 32x32 tile per block: few MFMAs and few memory operations per wave, so the whole K
+// range is prefetched at once and the epilogue's stores stay within one wave's outstanding-operation
+// budget (the 32x32-per-wave variant stalled on it).
+template <typename T, class Model>
+__global__ __launch_bounds__(256) void wgrad_sgd_kernel(WgArgs<T> a) {
+  using M = Mma<T>;
+  using Frag = typename M::Frag;
+  constexpr int KV = M::KV, KC = M::KC, FPS = 8;
+  const int lane = threadIdx.x & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
+  auto stamp = [&](int k) {
+    if (a.stamps && threadIdx.x == 0 && blockIdx.x < 512) a.stamps[(3072 + blockIdx.x) * 16 + k] = wall_clock64();
+  };
+  stamp(0);
+  const int tile = blockIdx.x;
+  if (a.sgd.step_ptr && tile == 0 && threadIdx.x == 0) {
     a.sgd.step_ptr[0] += 1;  // nothing after the head reads the batch counter in this step
     a.sgd.step_ptr[1] += 1;
   }
+  int j = 0;
+  while (j + 1 < a.njobs && tile >= a.job[j + 1].blk_begin) ++j;
+  const WgJob<T>& J = a.job[j];
+  const int lb = tile - J.blk_begin;
+  const int bn = lb / J.nblk_k, bk = lb % J.nblk_k;
+  const int n0 = bn * 32 + (w >> 1) * 16, k0 = bk * 32 + (w & 1) * 16;
+  const int Kb = J.K + (J.bias ? 1 : 0);
+  if (n0 >= J.N || k0 >= Kb) return;  // wave-uniform
+  const int nsteps = a.Bp / KC;
+
+  const T* ap = J.dyT + (size_t)(n0 + row) * a.ldB + grp * KV;  // rows < NP (zero padded)
+  const int kk = k0 + row;
+  const T* bp = J.xT + (size_t)min(kk, J.K > 0 ? J.K - 1 : 0) * a.ldB + grp * KV;
+  const int sel = kk < J.K ? 0 : (kk == J.K && J.bias ? 1 : 2);
+  Frag ones;
+#pragma unroll
+  for (int q = 0; q < KV; ++q) M::set(ones, q, 1.f);
+  const Frag zf = M::zero();
+
+  // the first FPS K-steps' fragments, then the SGD operands (the MFMAs wait only for the former)
+  Frag fa[FPS], fb[FPS];
+#pragma unroll
+  for (int st = 0; st < FPS; ++st) {
+    const int rc = min(st, nsteps - 1) * KC;
+    fa[st] = M::load(ap + rc);
+    fb[st] = M::load(bp + rc);
+  }
+  int pidx[4];
+  float pv[4], mv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int n = n0 + grp * 4 + i;
+    const int q = n >= J.N ? -1 : (kk < J.K ? n * J.K + kk : (kk == J.K && J.bias ? J.N * J.K + n : -1));
+    pidx[i] = q < 0 ? -1 : J.out_off + q;
+    const int p = max(pidx[i], 0);
+    pv[i] = a.sgd.params[p];
+    mv[i] = a.sgd.mom ? a.sgd.mom[p] : 0.f;
+  }
+  f32x4 acc = zero4();
+#pragma unroll
+  for (int st = 0; st < FPS; ++st)
+    if (st < nsteps) M::mma(acc, fa[st], sel == 0 ? fb[st] : (sel == 1 ? ones : zf));
+  for (int st = FPS; st < nsteps; ++st) {  // longer batches: the rest, one step at a time
+    const Frag x = M::load(ap + st * KC), y = M::load(bp + st * KC);
+    M::mma(acc, x, sel == 0 ? y : (sel == 1 ? ones : zf));
+  }
+  stamp(1);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (pidx[i] < 0) continue;
+    const int p = pidx[i];
+    float g = (0.f + acc[i]) * a.sgd.scale;  // = reduce_sgd over one slab
+    a.sgd.grad[p] = g;
+    if (a.sgd.mom) {
+      const float b = a.sgd.momentum * mv[i] + g;
+      a.sgd.mom[p] = b;
+      g = b;
+    }
+    const float nv = pv[i] - a.sgd.lr * g;
+    a.sgd.params[p] = nv;
+    Packer<Model, T>::pack(p, nv, reinterpret_cast<T*>(a.sgd.pack));
+  }
+  stamp(2);
 }
 
 template <typename T, class H, class Model>
 int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab_ld, int xcd_ch, hipStream_t s,
                  const SgdFuse* fuse) {
   WgArgs<T> a{};
+  const int BT = fuse ? 32 : 64;  // output tile per block (wgrad_sgd_kernel: 32, wgrad_kernel: 64)
   auto mk = [&](int i, const void* dy, const void* x, int N, int K, int NP, bool bias, int off, int& blk) {
     WgJob<T>& J = a.job[i];
     J.dyT = reinterpret_cast<const T*>(dy);
     J.xT = reinterpret_cast<const T*>(x);
     J.N = N; J.K = K; J.NP = NP; J.bias = bias ? 1 : 0; J.out_off = off;
-    J.nblk_k = (K + (bias ? 1 : 0) + 63) / 64;
+    J.nblk_k = (K + (bias ? 1 : 0) + BT - 1) / BT;
     J.blk_begin = blk;
-    blk += ((N + 63) / 64) * J.nblk_k;
+    blk += ((N + BT - 1) / BT) * J.nblk_k;
   };
   int blk = 0;
   mk(0, hb.dy1T, hb.xT, H::N1, H::K0, H::N1P, true, H::W1, blk);
@@ -838,16 +907,19 @@ int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab
   }
   a.slab = slab;
   a.slab_ld = slab_ld;
+  a.stamps = hb.stamps;
   a.xcd_ch = 0;
   static const bool xcd_off = std::getenv("MNIST_AMD_NO_XCD") != nullptr;  // A/B knob
   // XCD-aware mapping when the head's row tiling is known and the split count divides over 8 XCDs
-  if (!xcd_off && xcd_ch > 0 && xcd_ch % KC == 0 && splits % 8 == 0) {
+  if (!fuse && !xcd_off && xcd_ch > 0 && xcd_ch % KC == 0 && splits % 8 == 0) {
     a.xcd_ch = xcd_ch;
     a.nch = (a.Bp + xcd_ch - 1) / xcd_ch;
     a.sx = splits / 8;
-    hipLaunchKernelGGL((wgrad_kernel<T, Model>), dim3(blk * splits), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(wgrad_kernel<T>, dim3(blk * splits), dim3(256), 0, s, a);
+  } else if (a.fuse) {
+    hipLaunchKernelGGL((wgrad_sgd_kernel<T, Model>), dim3(blk), dim3(256), 0, s, a);
   } else {
-    hipLaunchKernelGGL((wgrad_kernel<T, Model>), dim3(blk, splits), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(wgrad_kernel<T>, dim3(blk, splits), dim3(256), 0, s, a);
   }
   return splits;
 }

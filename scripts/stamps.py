@@ -64,3 +64,14 @@ if model == "lenet5":
     for t in range(4):
         bnames += [f"img{t} A (stage)", f"img{t} B (w2+dgrad)", f"img{t} C (w1)"]
     report("conv_bwd", allst[1024:1024 + nb], bnames + [None, "slab write"], 15)
+
+if model == "mlp":
+    def live(st):
+        return st[st[:, 0] > 0]
+    report("wgrad", live(allst[3072:3584]), ["GEMM", "epilogue"], 2)
+    report("l1_split", live(allst[3584:4096]), ["stage X", "GEMM"], 2)
+    l1s, hs, wgs = live(allst[3584:4096]), allst[:nblk], live(allst[3072:3584])
+    T0 = l1s[:, 0].min()
+    for name, st, last in (("l1_split", l1s, 2), ("head", hs, 8), ("wgrad", wgs, 2)):
+        print(f"{name:9s} first start {(st[:, 0].min() - T0) * 10 / 1000:6.2f} us  last start "
+              f"{(st[:, 0].max() - T0) * 10 / 1000:6.2f}  last end {(st[:, last].max() - T0) * 10 / 1000:6.2f}")
