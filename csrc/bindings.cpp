@@ -70,7 +70,7 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init<>())
 #define RW(f) .def_readwrite(#f, &TrainerPtrs::f)
       RW(images) RW(labels) RW(idx) RW(step) RW(params) RW(grad) RW(mom) RW(pack) RW(slab_fc) RW(slab_conv)
-      RW(metrics) RW(xT) RW(h1T) RW(h2T) RW(dy1T) RW(dy2T) RW(dy3T) RW(p1) RW(m1) RW(p2) RW(m2) RW(dp2) RW(z1p) RW(stamps);
+      RW(metrics) RW(xT) RW(h1T) RW(h2T) RW(dy1T) RW(dy2T) RW(dy3T) RW(p1) RW(m1) RW(p2) RW(m2) RW(dp2) RW(z1p) RW(stamps) RW(xnext) RW(ynext);
 #undef RW
 
   py::class_<Bucket>(m, "Bucket")
@@ -138,6 +138,7 @@ PYBIND11_MODULE(_C, m) {
       .def("eval_batch", &Trainer::eval_batch)
       .def("capture", &Trainer::capture)
       .def("replay", &Trainer::replay)
+      .def("prime_next", &Trainer::prime_next)
       .def_property("fuse_wgrad_sgd", &Trainer::fuse_wgrad_sgd, &Trainer::set_fuse_wgrad_sgd)
       .def("capture_multi", &Trainer::capture_multi)
       .def("replay_multi", &Trainer::replay_multi)

@@ -175,8 +175,20 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
     }
   }
 
+  // ---- look-ahead (small-batch MLP training): this step's labels come from ynext (gathered by the
+  //      previous step), and this kernel gathers the NEXT step's rows of its tile into xnext / ynext
+  //      (consumed by the next l1_split / head; this step's l1_split has already read xnext)
+  constexpr bool LOOK = PRE && H::GATHER && TRAIN;
+  const bool look = LOOK && br.xnext != nullptr;  // uniform
+  constexpr int GCH = R * 49, GIT2 = LOOK ? (GCH + NTH - 1) / NTH : 1;  // 16-byte chunks of the tile's rows
+  int gidx[GIT2];
+
   // ---- staging: indices, weights, biases (+ the input tile; the MLP gather needs sIdx first)
-  if (tid < R) sIdx[tid] = (r0 + tid < B) ? idx[r0 + tid] : -1;
+  if (look) {
+    if (tid < R) sLab[tid] = (r0 + tid < B) ? (int)br.ynext[r0 + tid] : 0;
+  } else if (tid < R) {
+    sIdx[tid] = (r0 + tid < B) ? idx[r0 + tid] : -1;
+  }
   if constexpr (S::WLDS) {
     stage_rows<T, NTH, H::N2P, H::N1P, S::PW2>(reinterpret_cast<T*>(smem + S::OFF_W2), pack + H::F2, tid);
     if constexpr (TRAIN && !S::FT) {
@@ -191,6 +203,18 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
     else if (e < H::N1P + H::N2P) v = (e - H::N1P) < H::N2 ? prm[H::B2 + e - H::N1P] : 0.f;
     else v = (H::BIAS3 && e - H::N1P - H::N2P < H::NC) ? prm[H::B3 + e - H::N1P - H::N2P] : 0.f;
     sB1[e] = v;
+  }
+  // look-ahead indices: issued after every load the staging barrier waits for (in-order vmcnt)
+  if constexpr (LOOK) {
+    if (look) {
+      const int nidx = br.step_ptr[2];
+#pragma unroll
+      for (int j = 0; j < GIT2; ++j) {
+        const int e = tid + j * NTH, r = e / 49;
+        const int g = (step + 1) * br.batch_stride + r0 + r;
+        gidx[j] = (e < GCH && r0 + r < br.batch_stride && g < nidx) ? br.idx_epoch[g] : -1;
+      }
+    }
   }
   if constexpr (H::GATHER && !PRE) __syncthreads();
 
@@ -242,9 +266,23 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   __syncthreads();
   stamp(1);
   // labels: fetched by the LAST threads of the block (idle in L1 when NWV > NT1), used after 3 barriers
-  {
+  if (!look) {
     const int t = tid - (NTH - R);
     if (t >= 0) sLab[t] = sIdx[t] >= 0 ? (int)br.labels[sIdx[t]] : 0;
+  }
+  // look-ahead: the next step's pixels / labels (indices were loaded during the staging)
+  uint4 gv[GIT2];
+  int glab[GIT2];
+  if constexpr (LOOK) {
+    if (look) {
+#pragma unroll
+      for (int j = 0; j < GIT2; ++j) {
+        const int e = tid + j * NTH, c = e % 49;
+        gv[j] = gidx[j] >= 0 ? *reinterpret_cast<const uint4*>(br.images + (size_t)gidx[j] * 784 + c * 16)
+                             : make_uint4(0, 0, 0, 0);
+        glab[j] = (gidx[j] >= 0 && c == 0) ? (int)br.labels[gidx[j]] : 0;
+      }
+    }
   }
 
   const float keep_scale = H::DROPOUT ? 1.0f / (1.0f - hb.drop_p) : 1.0f;
@@ -554,6 +592,18 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       }
     }
   }
+  if constexpr (LOOK) {
+    if (look) {  // ordered after every read of this step's ynext by the softmax barrier
+#pragma unroll
+      for (int j = 0; j < GIT2; ++j) {
+        const int e = tid + j * NTH, r = e / 49, c = e % 49;
+        if (gidx[j] >= 0) {
+          *reinterpret_cast<uint4*>(br.xnext + (size_t)(r0 + r) * 784 + c * 16) = gv[j];
+          if (c == 0) br.ynext[r0 + r] = (uint8_t)glab[j];
+        }
+      }
+    }
+  }
   stamp(8);
   flush_metrics();
 }
@@ -601,12 +651,18 @@ __global__ __launch_bounds__(256) void l1_split_kernel(BatchRef br, HeadBuffers 
   constexpr int GIT = (16 * (QCH * KC / 8) + 255) / 256;
   uint2 gu[H::GATHER ? GIT : 1];
   if constexpr (H::GATHER) {
-    const int32_t* idx = br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride;
-    const int sidx = idx[min(r0 + (tid & 15), B - 1)];
+    // training with the look-ahead: the rows were gathered into xnext by the previous step's head
+    const uint8_t* src;
+    if (TRAIN && br.xnext) {
+      src = br.xnext + (size_t)(r0 + (tid & 15)) * 784;
+    } else {
+      const int32_t* idx = br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride;
+      src = br.images + (size_t)idx[min(r0 + (tid & 15), B - 1)] * 784;
+    }
 #pragma unroll
     for (int it = 0; it < GIT; ++it) {
       const int k = k0 + ((tid + it * 256) >> 4) * 8;
-      gu[it] = *reinterpret_cast<const uint2*>(br.images + (size_t)sidx * 784 + min(k, H::K0 - 8));
+      gu[it] = *reinterpret_cast<const uint2*>(src + min(k, H::K0 - 8));
     }
   }
 #pragma unroll
@@ -999,7 +1055,25 @@ int head_launch_t(bool train, const BatchRef& br, const HeadBuffers& hb, int row
   return 64;
 }
 
+// Rows of the CURRENT step (step_ptr[0]) -> xnext / ynext: primes the look-ahead after the host set the
+// step counter (set_epoch_indices); every training step's head keeps it one step ahead after that.
+__global__ __launch_bounds__(256) void gather_next_kernel(BatchRef br) {
+  const int e = blockIdx.x * 256 + threadIdx.x, r = e / 49, c = e % 49;
+  if (r >= br.batch_stride) return;
+  const int g = br.step_ptr[0] * br.batch_stride + r;
+  const bool valid = g < br.step_ptr[2];
+  const int gi = valid ? br.idx_epoch[g] : 0;
+  const uint4 v = valid ? *reinterpret_cast<const uint4*>(br.images + (size_t)gi * 784 + c * 16) : make_uint4(0, 0, 0, 0);
+  *reinterpret_cast<uint4*>(br.xnext + (size_t)r * 784 + c * 16) = v;
+  if (c == 0) br.ynext[r] = valid ? br.labels[gi] : 0;
+}
+
 }  // namespace
+
+void launch_gather_next(const BatchRef& br, hipStream_t s) {
+  if (!br.xnext || br.batch_stride <= 0) return;
+  hipLaunchKernelGGL(gather_next_kernel, dim3((br.batch_stride * 49 + 255) / 256), dim3(256), 0, s, br);
+}
 
 int head_rows_per_block(ModelKind m, DType t, int B) {
   static const int forced = [] {

@@ -17,7 +17,17 @@ struct BatchRef {
   const int32_t* step_ptr;   // device step counter
   int32_t batch_stride;      // regular batch size
   int32_t B;                 // rows in this batch (<= batch_stride)
+  // Small-batch MLP training (layer-1 split path): the batch's samples gathered one step AHEAD, by the
+  // previous step's head kernel (or launch_gather_next after the step counter is set): [batch][784]
+  // raw pixels and [batch] labels of step step_ptr[0].  step_ptr[2] = number of loaded indices.
+  // Null: every kernel gathers through idx_epoch itself.
+  uint8_t* xnext = nullptr;
+  uint8_t* ynext = nullptr;
 };
+
+// Gather the rows of the CURRENT step (step_ptr[0]) into br.xnext / br.ynext (primes the look-ahead
+// after the step counter was set from the host).
+void launch_gather_next(const BatchRef& br, hipStream_t s);
 
 struct HeadBuffers {
   const float* params;   // fp32 master slab

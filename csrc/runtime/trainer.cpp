@@ -127,7 +127,15 @@ BatchRef Trainer::batch_ref(int B) const {
   br.step_ptr = ptr<const int32_t>(p_.step);
   br.batch_stride = batch_;
   br.B = B;
+  br.xnext = ptr<uint8_t>(p_.xnext);
+  br.ynext = ptr<uint8_t>(p_.ynext);
   return br;
+}
+
+void Trainer::prime_next(uintptr_t stream) {
+  if (!p_.xnext) return;
+  launch_gather_next(batch_ref(batch_), S(stream));
+  post_launch(S(stream));
 }
 
 HeadBuffers Trainer::head_buffers(float* metrics) const {

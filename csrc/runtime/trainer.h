@@ -22,6 +22,7 @@ struct TrainerPtrs {
   uintptr_t p1 = 0, m1 = 0, p2 = 0, m2 = 0, dp2 = 0;
   uintptr_t z1p = 0;  // optional: enables the small-batch layer-1 split path
   uintptr_t stamps = 0;  // optional: per-block phase timestamps of the head kernel (profiling)
+  uintptr_t xnext = 0, ynext = 0;  // optional: small-batch MLP look-ahead gather buffers (BatchRef)
 };
 
 // A gradient bucket = contiguous range of the flat grad slab, all-reduced as one RCCL call as
@@ -77,6 +78,8 @@ class Trainer {
   void spin(double seconds, uintptr_t stream);
 
   void pack(uintptr_t stream);
+  // re-gather the look-ahead buffers for the current device step (after the host set the counter)
+  void prime_next(uintptr_t stream);
   // Full eager step for a batch of B rows (B <= batch).
   void train_step(int B, uintptr_t stream);
   // Phases (used by the torch.distributed comm path and by tests).

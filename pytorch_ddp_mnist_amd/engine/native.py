@@ -103,7 +103,9 @@ class NativeTrainer:
         self.mom = z(self.nparam, dt=torch.float32)
         self.pack_buf = z(C.model_pack_size(mid))
         self.idx = torch.zeros(n_max, dtype=torch.int32, device=dev)
-        self.step_ctr = torch.zeros(2, dtype=torch.int32, device=dev)
+        # device counters: [0] step within the epoch (batch addressing), [1] global step (dropout stream),
+        # [2] loaded indices of the epoch (look-ahead gather bound)
+        self.step_ctr = torch.zeros(4, dtype=torch.int32, device=dev)
         self.metrics = z(3, dt=torch.float32)
         self.eval_metrics = z(3, dt=torch.float32)
         self.xT, self.h1T, self.h2T = z(K0P, self.ld_b), z(N1P, self.ld_b), z(N2P, self.ld_b)
@@ -123,6 +125,11 @@ class NativeTrainer:
             self.p1 = self.m1 = self.p2 = self.m2 = self.dp2 = None
         # layer-1 K-split partials for the small-batch path (csrc/kernels/head.hip l1_split_kernel)
         self.z1p = z(C.L1_KSPLIT * N1P * self.ld_b, dt=torch.float32) if self.batch <= C.L1_SPLIT_MAX_B else None
+        # small-batch MLP: the next step's pixels / labels, gathered one step ahead by the head kernel
+        # (rows padded to the 16-row tiles that read them)
+        look = model == "mlp" and self.z1p is not None and not os.environ.get("MNIST_AMD_NO_LOOKAHEAD")
+        self.xnext = z(_rup(self.batch, 32) * 784, dt=torch.uint8) if look else None
+        self.ynext = z(_rup(self.batch, 32), dt=torch.uint8) if look else None
 
         P = C.TrainerPtrs()
         ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
@@ -133,6 +140,7 @@ class NativeTrainer:
         P.dy1T, P.dy2T, P.dy3T = ptr(self.dy1T), ptr(self.dy2T), ptr(self.dy3T)
         P.p1, P.m1, P.p2, P.m2, P.dp2 = ptr(self.p1), ptr(self.m1), ptr(self.p2), ptr(self.m2), ptr(self.dp2)
         P.z1p = ptr(self.z1p)
+        P.xnext, P.ynext = ptr(self.xnext), ptr(self.ynext)
         # MNIST_AMD_STAMPS=1: per-workgroup phase timestamps (wall clock, 100 MHz), 16 slots per workgroup:
         # head blocks [0, 1024), conv_bwd [1024, 2048), conv_fwd [2048, 3072) (later workgroups skip)
         self.stamps = z(4096 * 16, dt=torch.int64) if os.environ.get("MNIST_AMD_STAMPS") else None
@@ -318,6 +326,8 @@ class NativeTrainer:
         with torch.cuda.stream(self.stream):
             self.idx[:n].copy_(src, non_blocking=True)
             self.step_ctr[0].zero_()
+            self.step_ctr[2].fill_(n)
+        self.rt.prime_next(self.stream.cuda_stream)  # look-ahead rows of step 0 (no-op without it)
         self.n_epoch = n
         self.host_step = 0  # mirror of the device step counter: every launch is bounds-checked on the host
 

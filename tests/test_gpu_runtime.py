@@ -176,3 +176,37 @@ def test_mlp_fused_wgrad_sgd_matches_separate_update(native, small_mnist, dtype,
         out.append((tr.params.cpu(), tr.mom.cpu(), tr.step_ctr.cpu()))
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
     assert torch.equal(out[0][2], out[1][2]) and out[1][2].tolist()[:2] == [5, 5]
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_mlp_lookahead_gather_matches_direct_gather(native, small_mnist, dtype, monkeypatch):
+    """Small-batch MLP: the rows gathered one step ahead (by the previous head kernel / the prime after
+    set_epoch_indices) give bitwise the same training as gathering through the index order in place --
+    over graph and eager steps, a partial last batch and a second epoch with a new order."""
+    from pytorch_ddp_mnist_amd.engine.native import NativeTrainer
+    from pytorch_ddp_mnist_amd.models import build_model
+    x, y, _, _ = small_mnist
+    torch.manual_seed(0)
+    m = build_model("mlp")
+    g = torch.Generator().manual_seed(7)
+    orders = [torch.randperm(len(y), generator=g)[:128 * 5 + 40].to(torch.int32) for _ in range(2)]
+    out = []
+    for look in (False, True):
+        if look:
+            monkeypatch.delenv("MNIST_AMD_NO_LOOKAHEAD", raising=False)
+        else:
+            monkeypatch.setenv("MNIST_AMD_NO_LOOKAHEAD", "1")
+        tr = NativeTrainer("mlp", dtype, 128, torch.from_numpy(x.reshape(-1, 784)), torch.from_numpy(y),
+                           dropout=0.2, init=m, momentum=0.9)
+        assert (tr.xnext is not None) == look
+        for order in orders:
+            tr.set_epoch_indices(order)
+            tr.reset_metrics()
+            tr.run_steps(3, use_graph=True)
+            tr.step(128, use_graph=False)
+            tr.step(128, use_graph=True)
+            tr.step(40, use_graph=False)
+        tr.synchronize()
+        out.append((tr.params.cpu(), tr.read_metrics().correct))
+    assert torch.equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1]
