@@ -60,6 +60,8 @@ def parse(argv=None):
     ap.add_argument("--eval", action="store_true", default=True)
     ap.add_argument("--no-eval", dest="eval", action="store_false")
     ap.add_argument("--json-out", default=None)
+    ap.add_argument("--digest", action="store_true",
+                    help="every rank prints a sha256 of its final parameters to stderr (replica consistency check)")
     ap.add_argument("--dry-run", action="store_true",
                     help="check the launch wiring only: every rank validates its env, rank 0 prints a JSON line, no GPU")
     return ap.parse_args(argv)
@@ -245,6 +247,11 @@ def main(argv=None) -> int:
         "top1": None if top1 is None else round(top1, 4),
         "train_loss_mean": round(train.mean_loss, 4),
     }
+    if a.digest:
+        import hashlib
+        tr.synchronize()
+        print(f"digest rank={rank} {hashlib.sha256(tr.params.cpu().numpy().tobytes()).hexdigest()}",
+              file=sys.stderr, flush=True)
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
