@@ -65,6 +65,12 @@ template <> struct Mma<bf16> {
 template <typename T> DEV T to_t(float x) { return (T)x; }
 template <typename T> DEV float to_f(T x) { return (float)x; }
 
+// s_waitcnt vmcnt(0) (expcnt / lgkmcnt left at their maxima; gfx9 encoding).  Placed after loads of
+// loop-invariant operands and before the loop: the wait-insertion pass cannot prove across the loop's
+// back edge that such registers have arrived, so without it every use inside the loop gets a
+// vmcnt(N) that -- in-order counting -- also waits for the loop's own prefetch loads.
+DEV void wait_vm_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 DEV int lane_id() { return threadIdx.x & 63; }
 DEV int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 

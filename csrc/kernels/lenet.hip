@@ -271,6 +271,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
     zero_lds<T>(p1c, P1IMG);
     zero_lds<uint8_t>(m1s, M1IMG);
   }
+  // b1 / b2r / biases are loop-invariant registers loaded from global memory above (image 0's pixels
+  // are also in flight and consumed right after this barrier anyway)
+  wait_vm_all();
   __syncthreads();
   stamp(1);
   for (int t = 0; t < ipb; ++t) {
@@ -579,6 +582,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   for (int i = 0; i < NWT; ++i) accW2[i] = zero4();
   accW1[0] = zero4();
   accW1[1] = zero4();
+  wait_vm_all();  // loop-invariant loads done here (image 0's inputs, also in flight, are consumed next)
   __syncthreads();
   stamp(1);
 
