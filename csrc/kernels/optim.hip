@@ -137,6 +137,12 @@ __global__ __launch_bounds__(NW * 64) void reduce_sgd_kernel(const float* __rest
   __shared__ float part[NW][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int p = p0 + blockIdx.x * 64 + lane;
+  // the update's operands first: their latency overlaps the slab loads instead of following the reduction
+  float pv = 0.f, mv = 0.f;
+  if (w == 0 && p < n) {
+    pv = params[p];
+    if (mom) mv = mom[p];
+  }
   float s = 0.f;
   if (p < n) {
     const bool a = p < split;
@@ -154,11 +160,11 @@ __global__ __launch_bounds__(NW * 64) void reduce_sgd_kernel(const float* __rest
     g *= scale;
     grad[p] = g;
     if (mom) {
-      const float b = mu * mom[p] + g;
+      const float b = mu * mv + g;
       mom[p] = b;
       g = b;
     }
-    const float v = params[p] - lr * g;
+    const float v = pv - lr * g;
     params[p] = v;
     Packer<Model, T>::pack(p, v, pack);
   }
@@ -177,14 +183,15 @@ __global__ __launch_bounds__(256) void reduce_sgd_direct_kernel(const float* __r
                                                                 int32_t* step_ptr) {
   const int p = p0 + blockIdx.x * 256 + threadIdx.x;
   if (p < n) {
+    const float pv = params[p], mv = mom ? mom[p] : 0.f;  // issued with the slab loads
     float g = slab_sum_direct(slab, ld, ns, p) * scale;
     grad[p] = g;
     if (mom) {
-      const float b = mu * mom[p] + g;
+      const float b = mu * mv + g;
       mom[p] = b;
       g = b;
     }
-    const float v = params[p] - lr * g;
+    const float v = pv - lr * g;
     params[p] = v;
     Packer<Model, T>::pack(p, v, pack);
   }
