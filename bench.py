@@ -156,7 +156,9 @@ def main(argv=None) -> int:
             C = load_c()
             comm = ctx.rccl
             if comm is None:  # --comm-world1: a world-1 RCCL communicator, no rendezvous needed
-                comm = C.RcclComm(bytes(C.RcclComm.make_unique_id()), 0, 1, ctx.local_rank)
+                from pytorch_ddp_mnist_amd.utils.logging import native_stdout_to_stderr
+                with native_stdout_to_stderr():  # RCCL's init banner must not reach the JSON stdout
+                    comm = C.RcclComm(bytes(C.RcclComm.make_unique_id()), 0, 1, ctx.local_rank)
             rccl_version = C.rccl_version()
             tr.attach_comm(comm, W)
             tr.broadcast_params(0)

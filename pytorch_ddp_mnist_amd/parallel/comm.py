@@ -122,12 +122,14 @@ def init_distributed(method: Optional[str] = None, parallel: bool = True, device
 def make_rccl(ctx: DistContext):
     """Native RCCL communicator; the unique id travels over the c10d TCPStore."""
     from ..ops.native import load_c
+    from ..utils.logging import native_stdout_to_stderr
     C = load_c()
     store = dist.distributed_c10d._get_default_store()
-    if ctx.rank == 0:
-        uid = C.RcclComm.make_unique_id()
-        store.set(UID_KEY, uid)
-    else:
-        store.wait([UID_KEY], datetime.timedelta(seconds=300))
-        uid = store.get(UID_KEY)
-    return C.RcclComm(bytes(uid), ctx.rank, ctx.world, ctx.local_rank)
+    with native_stdout_to_stderr():  # RCCL's init banner goes to stderr
+        if ctx.rank == 0:
+            uid = C.RcclComm.make_unique_id()
+            store.set(UID_KEY, uid)
+        else:
+            store.wait([UID_KEY], datetime.timedelta(seconds=300))
+            uid = store.get(UID_KEY)
+        return C.RcclComm(bytes(uid), ctx.rank, ctx.world, ctx.local_rank)

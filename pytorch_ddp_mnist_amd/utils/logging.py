@@ -10,6 +10,8 @@
 """
 from __future__ import annotations
 
+import contextlib
+import os
 import json
 import socket
 import sys
@@ -108,3 +110,21 @@ class ProgressBar:
             self.bar.close()
         else:
             print(file=self.out)
+
+
+@contextlib.contextmanager
+def native_stdout_to_stderr():
+    """Route file-descriptor-level stdout to stderr for the duration (RCCL prints a version banner on
+    stdout when it initialises, which would corrupt the one-JSON-line contract of bench.py and
+    interleave with the epoch lines)."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        try:
+            sys.stdout.flush()
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
