@@ -501,8 +501,16 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     }
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
-      const int e = min(tid + 256 * r, 399);
-      const int n = e & 15, p = e >> 4;
+      int n, p;
+      if constexpr (sizeof(T) == 2) {  // bf16: thread j < 200 owns channels (2(j%8), 2(j%8)+1) at position j/8
+        const int j = min(tid, 199);
+        n = 2 * (j & 7) + r;
+        p = j >> 3;
+      } else {                          // f32: items tid, tid + 256 of (channel fastest, position)
+        const int e = min(tid + 256 * r, 399);
+        n = e & 15;
+        p = e >> 4;
+      }
       f.c[r] = cb.m2[(size_t)bb * 400 + n * 25 + p];
       f.g[r] = dp2[(size_t)bb * K0P + n * 25 + p];
     }
@@ -675,19 +683,54 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
         }
       }
     }
+    if constexpr (sizeof(T) == 2) {
+      // pool2 un-pooling, two channels per thread: every DYS write is one 32-bit (channel pair) store and
+      // every DY2T write one 32-bit (column pair) store -- half the store instructions of 16-bit writes
+      if (tid < 200 && !(cb.ablate & 32)) {
+        const int n0 = 2 * (tid & 7), p = tid >> 3, py = p / 5, px = p % 5;
+        float v[2][4];  // [channel][window]
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int e = tid + 256 * r;
-      if (e >= 400 || (cb.ablate & 32)) break;
-      const int n = e & 15, p = e >> 4, py = p / 5, px = p % 5;  // channel fastest: conflict-free DYS writes
-      const uint32_t code = valid ? cur.c[r] : 0u;  // code 0: ReLU blocked, every window gets 0
-      const float g = to_f(cur.g[r]);
+        for (int r = 0; r < 2; ++r) {
+          const uint32_t code = valid ? cur.c[r] : 0u;  // code 0: ReLU blocked, every window gets 0
+          const float g = to_f(cur.g[r]);
 #pragma unroll
-      for (int win = 0; win < 4; ++win) {
-        const int oh = 2 * py + (win >> 1), ow = 2 * px + (win & 1);
-        const T v = to_t<T>(((code & 4) && (code & 3) == win) ? g : 0.f);
-        if constexpr (HD) dys[((oh + 4) * 18 + ow + 4) * 16 + n] = v;
-        if constexpr (HW) dy2t[n * S::D2P + oh * 16 + ow] = v;
+          for (int win = 0; win < 4; ++win) v[r][win] = ((code & 4) && (code & 3) == win) ? g : 0.f;
+        }
+        auto pack2 = [](float a, float b) {
+          bf16x2 q;
+          q[0] = (bf16)a;
+          q[1] = (bf16)b;
+          return __builtin_bit_cast(uint32_t, q);
+        };
+#pragma unroll
+        for (int win = 0; win < 4; ++win) {
+          const int oh = 2 * py + (win >> 1), ow = 2 * px + (win & 1);
+          if constexpr (HD) *reinterpret_cast<uint32_t*>(dys + ((oh + 4) * 18 + ow + 4) * 16 + n0) = pack2(v[0][win], v[1][win]);
+        }
+        if constexpr (HW) {
+#pragma unroll
+          for (int r = 0; r < 2; ++r)
+#pragma unroll
+            for (int dy = 0; dy < 2; ++dy)
+              *reinterpret_cast<uint32_t*>(dy2t + (n0 + r) * S::D2P + (2 * py + dy) * 16 + 2 * px) =
+                  pack2(v[r][2 * dy], v[r][2 * dy + 1]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int e = tid + 256 * r;
+        if (e >= 400 || (cb.ablate & 32)) break;
+        const int n = e & 15, p = e >> 4, py = p / 5, px = p % 5;  // channel fastest: conflict-free DYS writes
+        const uint32_t code = valid ? cur.c[r] : 0u;  // code 0: ReLU blocked, every window gets 0
+        const float g = to_f(cur.g[r]);
+#pragma unroll
+        for (int win = 0; win < 4; ++win) {
+          const int oh = 2 * py + (win >> 1), ow = 2 * px + (win & 1);
+          const T v = to_t<T>(((code & 4) && (code & 3) == win) ? g : 0.f);
+          if constexpr (HD) dys[((oh + 4) * 18 + ow + 4) * 16 + n] = v;
+          if constexpr (HW) dy2t[n * S::D2P + oh * 16 + ow] = v;
+        }
       }
     }
     __syncthreads();
