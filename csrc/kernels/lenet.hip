@@ -742,31 +742,36 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     // ---- phase B1: conv2 wgrad  dW2[n][(tap, c)] += sum_pos dY2[pos][n] * pool1[pos + tap][c]
     //      Straight-line (constant trip counts, the ablation test outside the loop) with the next
     //      chunk's fragments loaded before this chunk's MFMAs: a runtime trip count kept the loop
-    //      rolled and every chunk waited for its own LDS reads.  Waves with two tiles run the third on
-    //      the zero plane (unconditional loads keep the lgkmcnt bookkeeping exact).
+    //      rolled and every chunk waited for its own LDS reads.
     if (HW && !(cb.ablate & 64)) {
       auto ld_a = [&](int kc) { return M::load(dy2t + row * S::D2P + kc * KC + grp * KV); };
       auto ld_b = [&](int kc, int i) {
         const int p0 = kc * KC + grp * KV;
         return M::load(p1t + w2off[i] + (p0 >> 4) * 16 + (p0 & 15));
       };
-      Frag a = ld_a(0), b[NWT];
+      // NT real tiles on this wave (2 on waves 0-1, 3 on waves 2-3): no zero-plane filler tile
+      auto wgrad2 = [&](auto ntc) {
+        constexpr int NT = decltype(ntc)::value;
+        Frag a = ld_a(0), b[NT];
 #pragma unroll
-      for (int i = 0; i < NWT; ++i) b[i] = ld_b(0, i);
+        for (int i = 0; i < NT; ++i) b[i] = ld_b(0, i);
 #pragma unroll
-      for (int kc = 0; kc < W2CH; ++kc) {
-        Frag an = a, bn[NWT];
-        if (kc + 1 < W2CH) {
-          an = ld_a(kc + 1);
+        for (int kc = 0; kc < W2CH; ++kc) {
+          Frag an = a, bn[NT];
+          if (kc + 1 < W2CH) {
+            an = ld_a(kc + 1);
 #pragma unroll
-          for (int i = 0; i < NWT; ++i) bn[i] = ld_b(kc + 1, i);
+            for (int i = 0; i < NT; ++i) bn[i] = ld_b(kc + 1, i);
+          }
+#pragma unroll
+          for (int i = 0; i < NT; ++i) M::mma(accW2[i], a, b[i]);
+          a = an;
+#pragma unroll
+          for (int i = 0; i < NT; ++i) b[i] = bn[i];
         }
-#pragma unroll
-        for (int i = 0; i < NWT; ++i) M::mma(accW2[i], a, b[i]);
-        a = an;
-#pragma unroll
-        for (int i = 0; i < NWT; ++i) b[i] = bn[i];
-      }
+      };
+      if (nw == 2) wgrad2(std::integral_constant<int, 2>{});
+      else wgrad2(std::integral_constant<int, NWT>{});
     }
 
     // ---- phase B2: conv2 dgrad, one tile = image rows (y, y+1) x 16 columns x (r, c):
