@@ -62,6 +62,23 @@ template <> struct Mma<bf16> {
   static DEV float get(const Frag& f, int j) { return (float)f.v[j]; }
 };
 
+// Streaming (non-temporal) global stores for kernel outputs that only a LATER kernel reads: they are not
+// kept dirty in this XCD's L2, so the end-of-kernel L2 write-back (cross-XCD coherence at the kernel
+// boundary) has less to flush before the next kernel may start.
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+#ifndef MNIST_NT_STORES
+#define MNIST_NT_STORES 1
+#endif
+template <typename V>
+DEV void st_stream(V* p, const V& v) {
+#if MNIST_NT_STORES
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+DEV void st_stream16(void* p, const uint4& v) { st_stream(reinterpret_cast<u32x4*>(p), u32x4{v.x, v.y, v.z, v.w}); }
+
 template <typename T> DEV T to_t(float x) { return (T)x; }
 template <typename T> DEV float to_f(T x) { return (float)x; }
 
@@ -70,6 +87,14 @@ template <typename T> DEV float to_f(T x) { return (float)x; }
 // back edge that such registers have arrived, so without it every use inside the loop gets a
 // vmcnt(N) that -- in-order counting -- also waits for the loop's own prefetch loads.
 DEV void wait_vm_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+// Where this wave runs (profiling stamps): XCC id << 32 | HW_ID (cu [11:8], sh [12], se [15:13], simd [5:4]).
+// s_getreg reads of HW_REG_HW_ID (4) and HW_REG_XCC_ID (20), full width.
+DEV unsigned long long hw_location() {
+  const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+  const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+  return ((unsigned long long)(xcc & 15u) << 32) | hw;
+}
 
 DEV int lane_id() { return threadIdx.x & 63; }
 DEV int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }

@@ -605,6 +605,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
     }
   }
   stamp(8);
+  if (hb.stamps && tid == 0 && blockIdx.x < 1024) hb.stamps[blockIdx.x * 16 + 15] = hw_location();
   flush_metrics();
 }
 

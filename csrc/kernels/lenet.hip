@@ -93,10 +93,16 @@ struct FwdSmem {
   static constexpr int TOTAL = W2LDS ? rup(OFF_W2 + 16 * W2P * (int)sizeof(T), 16) : OFF_W2;
 };
 
-// Coalesced 16-byte copy of a staged LDS image to global memory (both 16-byte aligned).
+// Coalesced 16-byte copy of a staged LDS image to global memory (both 16-byte aligned).  STREAM: the
+// output is read only after another kernel has run (pool1 -> conv_bwd), so it is stored non-temporally
+// and is not left dirty in L2 for the kernel-end write-back; pool2 (read by the very next kernel) is not.
+template <bool STREAM = false>
 DEV void copy_out16(void* dst, const void* src, int bytes) {
-  for (int e = threadIdx.x; e < bytes / 16; e += blockDim.x)
-    reinterpret_cast<uint4*>(dst)[e] = reinterpret_cast<const uint4*>(src)[e];
+  for (int e = threadIdx.x; e < bytes / 16; e += blockDim.x) {
+    const uint4 v = reinterpret_cast<const uint4*>(src)[e];
+    if constexpr (STREAM) st_stream16(reinterpret_cast<uint4*>(dst) + e, v);
+    else reinterpret_cast<uint4*>(dst)[e] = v;
+  }
 }
 
 template <typename T, bool TRAIN>
@@ -369,8 +375,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
 
     // ---- pool1 -> HBM for the backward pass (16-byte stores), overlapped with conv2
     if (TRAIN && valid && !(cb.ablate & 1024)) {
-      copy_out16(reinterpret_cast<T*>(cb.p1) + (size_t)b * P1IMG, p1c, P1IMG * (int)sizeof(T));
-      copy_out16(cb.m1 + (size_t)b * M1IMG, m1s, M1IMG);
+      copy_out16<true>(reinterpret_cast<T*>(cb.p1) + (size_t)b * P1IMG, p1c, P1IMG * (int)sizeof(T));
+      copy_out16<true>(cb.m1 + (size_t)b * M1IMG, m1s, M1IMG);
     }
     // ---- conv2 + bias + ReLU + maxpool: 100 rows (25 pooled x 4) = 7 M-tiles, N = 16
     if (!(cb.ablate & 4)) {
@@ -391,6 +397,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
     if (t < 4) stamp(4 + 3 * t);
   }
   stamp(14);
+  if (cb.stamps && tid == 0 && blockIdx.x < 1024) cb.stamps[(1024 + blockIdx.x) * 16 + 15] = hw_location();
   flush_p2(blockIdx.x * ipb + ipb - 1);
 }
 
@@ -914,6 +921,8 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     }
   }
   stamp(15);
+  // (MODE 0 only: the MODE-2 stamp rows hold this block's hardware location)
+  if (MODE == 0 && cb.stamps && tid == 0 && blockIdx.x < 512) cb.stamps[(512 + blockIdx.x) * 16] = hw_location();
 }
 
 }  // namespace

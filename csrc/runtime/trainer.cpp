@@ -434,6 +434,8 @@ void Trainer::capture_into(hipStream_t s, int nsteps, hipGraph_t* graph, hipGrap
   HIP_CHECK(hipStreamEndCapture(s, graph));
   trace("capture: instantiate");
   HIP_CHECK(hipGraphInstantiate(exec, *graph, nullptr, nullptr, 0));
+  // device-side resources of the executable graph are set up now (setup time), not by its first launch
+  HIP_CHECK(hipGraphUpload(*exec, s));
   trace("capture: done");
 }
 

@@ -65,6 +65,34 @@ if model == "lenet5":
         bnames += [f"img{t} A (stage)", f"img{t} B (w2+dgrad)", f"img{t} C (w1)"]
     report("conv_bwd", allst[1024:1024 + nb], bnames + [None, "slab write"], 15)
 
+    def per_cu(title, st, loc, last):
+        """Balance across compute units: each CU's finish time (its last workgroup's final stamp)
+        relative to the kernel's first start.  loc = XCC << 32 | HW_ID per workgroup."""
+        hw = loc & 0xFFFFFFFF
+        key = ((loc >> 32) & 15) * 4096 + ((hw >> 13) & 7) * 512 + ((hw >> 12) & 1) * 256 + ((hw >> 8) & 15)
+        t0 = st[:, 0].min()
+        end = (st[:, last] - t0) * 10 / 1000.0
+        cus = {}
+        for k, e in zip(key.tolist(), end.tolist()):
+            n, m = cus.get(k, (0, 0.0))
+            cus[k] = (n + 1, max(m, e))
+        fin = np.array([m for _, m in cus.values()])
+        nwg = np.array([n for n, _ in cus.values()])
+        xccs = sorted({k // 4096 for k in cus})
+        per_xcc = " ".join(f"x{x}:{max(m for k, (_, m) in cus.items() if k // 4096 == x):.1f}" for x in xccs)
+        print(f"{title} per-CU: {len(cus)} CUs, workgroups/CU min {nwg.min()} max {nwg.max()}; CU finish "
+              f"mean {fin.mean():.2f} us  min {fin.min():.2f}  p90 {np.percentile(fin, 90):.2f}  max {fin.max():.2f}; "
+              f"per-XCC max {per_xcc}")
+
+    # kernel boundaries on the device clock: last workgroup end of one kernel -> first start of the next
+    fw, hd, bw = allst[2048:2048 + min(nf, 1024)], allst[:nblk], allst[1024:1024 + nb]
+    print(f"boundaries: conv_fwd last end -> head first start {(hd[:, 0].min() - fw[:, 14].max()) * 10 / 1000:.2f} us; "
+          f"head last end -> conv_bwd first start {(bw[:, 0].min() - hd[:, 8].max()) * 10 / 1000:.2f} us; "
+          f"conv_fwd first start -> conv_bwd last end {(bw[:, 15].max() - fw[:, 0].min()) * 10 / 1000:.2f} us")
+    per_cu("conv_fwd", allst[2048:2048 + min(nf, 1024)], allst[2048:2048 + min(nf, 1024), 15], 14)
+    per_cu("conv_bwd", allst[1024:1024 + nb], allst[1536:1536 + nb, 0], 15)
+    per_cu("head", allst[:nblk], allst[:nblk, 15], 8)
+
 if model == "mlp":
     def live(st):
         return st[st[:, 0] > 0]
