@@ -66,6 +66,7 @@ template <> struct Mma<bf16> {
 // kept dirty in this XCD's L2, so the end-of-kernel L2 write-back (cross-XCD coherence at the kernel
 // boundary) has less to flush before the next kernel may start.
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
 #ifndef MNIST_NT_STORES
 #define MNIST_NT_STORES 1
 #endif
@@ -95,6 +96,13 @@ DEV unsigned long long hw_location() {
   const unsigned xcc = __builtin_amdgcn_s_getreg((15 << 11) | 20);
   return ((unsigned long long)(xcc & 15u) << 32) | hw;
 }
+
+// Workgroups are dispatched round-robin over the 8 XCDs (workgroup g runs on XCD g % 8, each XCD with its
+// own L2).  xcd_unit maps g to the logical work unit (g % 8) * (grid / 8) + g / 8, so XCD x owns the
+// contiguous units [x * grid / 8, (x + 1) * grid / 8): with the same mapping in consecutive kernels, the
+// rows one kernel writes on an XCD are read by the next kernel on that XCD (L2 hits instead of MALL /
+// HBM after the kernel-boundary write-back).  A bijection of [0, grid); identity when grid % 8 != 0.
+DEV int xcd_unit(int g, int grid, int on) { return (on && (grid & 7) == 0) ? (g & 7) * (grid >> 3) + (g >> 3) : g; }
 
 DEV int lane_id() { return threadIdx.x & 63; }
 DEV int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
+#include <type_traits>
 
 #include "common.h"
 #include "launch.h"
@@ -82,23 +83,30 @@ DEV typename Mma<T>::Frag load_kstrided(const T* p, int pitch) {
   return f;
 }
 
-// copy a [ROWS][COLS] T matrix (COLS a multiple of 16 B) into LDS with row pitch PITCH: every global
-// load of the thread is issued before its first LDS store (one latency, not one per row chunk)
+// copy a [ROWS][COLS] T matrix (COLS a multiple of 16 B) into LDS with row pitch PITCH, in two halves:
+// load() issues the thread's global loads into registers, store() writes them to LDS -- so a kernel can
+// issue the loads of several matrices (and of its input tile) before the first LDS store: one memory
+// round trip for the whole staging phase instead of one per matrix
 template <typename T, int NT, int ROWS, int COLS, int PITCH>
-DEV void stage_rows(T* dst, const T* src, int tid) {
-  constexpr int VE = 16 / (int)sizeof(T), CV = COLS / VE, N = ROWS * CV, IT = (N + NT - 1) / NT;
-  uint4 v[IT];
+struct RowStager {
+  static constexpr int VE = 16 / (int)sizeof(T), CV = COLS / VE, N = ROWS * CV, IT = (N + NT - 1) / NT;
+  // native vector registers (HIP's uint4 class kept the member array on the scratch stack)
+  u32x4 v[IT];
+  DEV void load(const T* src, int tid) {
 #pragma unroll
-  for (int i = 0; i < IT; ++i) {
-    const int e = min(tid + i * NT, N - 1);
-    v[i] = *reinterpret_cast<const uint4*>(src + (e / CV) * COLS + (e % CV) * VE);
+    for (int i = 0; i < IT; ++i) {
+      const int e = min(tid + i * NT, N - 1);
+      v[i] = *reinterpret_cast<const u32x4*>(src + (e / CV) * COLS + (e % CV) * VE);
+    }
   }
+  DEV void store(T* dst, int tid) const {
 #pragma unroll
-  for (int i = 0; i < IT; ++i) {
-    const int e = tid + i * NT;
-    if (e < N) *reinterpret_cast<uint4*>(dst + (e / CV) * PITCH + (e % CV) * VE) = v[i];
+    for (int i = 0; i < IT; ++i) {
+      const int e = tid + i * NT;
+      if (e < N) *reinterpret_cast<u32x4*>(dst + (e / CV) * PITCH + (e % CV) * VE) = v[i];
+    }
   }
-}
+};
 
 // Phase timeline of one workgroup (measured with MNIST_AMD_STAMPS, LeNet bf16 B=8192, 64-row tiles,
 // 16 waves; before this layout every phase was dominated by its B-operand fetch from L2/MALL):
@@ -127,11 +135,11 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
 
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id();
   const int row = lane & 15, grp = lane >> 4;
-  const int r0 = blockIdx.x * R;
+  const int r0 = xcd_unit(blockIdx.x, gridDim.x, br.xcd) * R;  // rows conv_fwd wrote on this XCD
   const int B = br.B;
-  const int step = br.step_ptr[0];
-  const int gstep = br.step_ptr[1];
-  const int32_t* idx = br.idx_epoch + (size_t)step * br.batch_stride;
+  // The device step counters are read where they are needed, not here: a scalar load issued at the top
+  // made every later scalar-operand wait (lgkmcnt(0)) -- the first weight loads included -- wait for it.
+  auto batch_idx = [&] { return br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride; };
   const T* pack = reinterpret_cast<const T*>(hb.pack);
   const float* prm = hb.params;
   const int ldB = hb.ldB;
@@ -184,30 +192,85 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   int gidx[GIT2];
 
   // ---- staging: indices, weights, biases (+ the input tile; the MLP gather needs sIdx first)
+  //      Every global load of the phase is issued before the first LDS / global store (the stores of
+  //      one matrix used to wait for its loads before the next matrix's loads were issued, and the
+  //      input tile's loads could not move above the previous row's xT global stores): one round trip.
+  // (the tile's sample indices: the MLP gather needs them in LDS before its X gather; with a staged
+  //  input tile only the labels need them, and the last wave loads both after the barrier -- the
+  //  step counter -> index chain in wave 0 held its weight loads back and made it the barrier's straggler)
   if (look) {
     if (tid < R) sLab[tid] = (r0 + tid < B) ? (int)br.ynext[r0 + tid] : 0;
-  } else if (tid < R) {
-    sIdx[tid] = (r0 + tid < B) ? idx[r0 + tid] : -1;
+  } else if (H::GATHER && tid < R) {
+    sIdx[tid] = (r0 + tid < B) ? batch_idx()[r0 + tid] : -1;
   }
+  RowStager<T, NTH, H::N2P, H::N1P, S::PW2> st_w2;
+  RowStager<T, NTH, H::N1P, H::N2P, S::PW2T> st_w2t;
+  RowStager<T, NTH, H::N2P, H::NCK, S::PW3T> st_w3t;
+  RowStager<T, NTH, 16, H::N2P, S::PW3> st_w3;
+  constexpr bool STW_T = TRAIN && !S::FT;  // transposed W2 / W3 images staged
   if constexpr (S::WLDS) {
-    stage_rows<T, NTH, H::N2P, H::N1P, S::PW2>(reinterpret_cast<T*>(smem + S::OFF_W2), pack + H::F2, tid);
-    if constexpr (TRAIN && !S::FT) {
-      stage_rows<T, NTH, H::N1P, H::N2P, S::PW2T>(reinterpret_cast<T*>(smem + S::OFF_W2T), pack + H::F2T, tid);
-      stage_rows<T, NTH, H::N2P, H::NCK, S::PW3T>(reinterpret_cast<T*>(smem + S::OFF_W3T), pack + H::F3T, tid);
+    st_w2.load(pack + H::F2, tid);
+    if constexpr (STW_T) {
+      st_w2t.load(pack + H::F2T, tid);
+      st_w3t.load(pack + H::F3T, tid);
     }
-    stage_rows<T, NTH, 16, H::N2P, S::PW3>(reinterpret_cast<T*>(smem + S::OFF_W3), pack + H::F3, tid);
+    st_w3.load(pack + H::F3, tid);
   }
-  for (int e = tid; e < H::N1P + H::N2P + 16; e += NTH) {
-    float v = 0.f;
-    if (e < H::N1P) v = e < H::N1 ? prm[H::B1 + e] : 0.f;
-    else if (e < H::N1P + H::N2P) v = (e - H::N1P) < H::N2 ? prm[H::B2 + e - H::N1P] : 0.f;
-    else v = (H::BIAS3 && e - H::N1P - H::N2P < H::NC) ? prm[H::B3 + e - H::N1P - H::N2P] : 0.f;
-    sB1[e] = v;
+  constexpr int NBIAS = H::N1P + H::N2P + 16, ITB = (NBIAS + NTH - 1) / NTH;
+  // branch-free (a load inside a lane-divergent branch is followed by vmcnt(0) at the branch join, which
+  // serialised the staging loads): every lane loads a clamped address, the value is selected at use
+  float bias_v[ITB];
+  auto bias_src = [](int e, bool& live) {
+    int q;
+    if (e < H::N1P) { live = e < H::N1; q = H::B1 + min(e, H::N1 - 1); }
+    else if (e < H::N1P + H::N2P) { live = e - H::N1P < H::N2; q = H::B2 + min(e - H::N1P, H::N2 - 1); }
+    else if constexpr (H::BIAS3) { live = e < NBIAS && e - H::N1P - H::N2P < H::NC; q = H::B3 + min(max(e - H::N1P - H::N2P, 0), H::NC - 1); }
+    else { live = false; q = H::B1; }  // no layer-3 bias: any in-range address, value unused
+    return q;
+  };
+#pragma unroll
+  for (int i = 0; i < ITB; ++i) {
+    bool live;
+    const int q = bias_src(tid + i * NTH, live);
+    bias_v[i] = prm[q];
   }
+  // input tile rows (LeNet: pool2 rows written by conv_fwd), loaded with the weights.  A thread owns one
+  // 16-byte k-chunk of 4 consecutive rows, so its xT (transposed) stores are 4 rows wide: one 4-element
+  // store per k instead of four 1-element stores (16 lanes of a k cover the 64-row line)
+  constexpr bool XROW = !PRE && !H::GATHER;
+  constexpr int XVE = 16 / (int)sizeof(T), XCH = H::K0P / XVE, NXE = (R / 4) * XCH,
+                ITX = XROW ? (NXE + NTH - 1) / NTH : 1;
+  u32x4 xv[ITX][4];
+  if constexpr (XROW) {
+    const T* xin = reinterpret_cast<const T*>(hb.xin);
+#pragma unroll
+    for (int i = 0; i < ITX; ++i) {
+      const int e = tid + i * NTH, r = (e % (R / 4)) * 4, k = (e / (R / 4)) * XVE;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)  // branch-free: clamped row / chunk, rows past the batch zeroed at use
+        xv[i][q] = *reinterpret_cast<const u32x4*>(xin + (size_t)min(r0 + r + q, B - 1) * H::K0P + min(k, H::K0P - XVE));
+    }
+  }
+  stamp(9);  // every staging load issued
+  if constexpr (S::WLDS) {
+    st_w2.store(reinterpret_cast<T*>(smem + S::OFF_W2), tid);
+    if constexpr (STW_T) {
+      st_w2t.store(reinterpret_cast<T*>(smem + S::OFF_W2T), tid);
+      st_w3t.store(reinterpret_cast<T*>(smem + S::OFF_W3T), tid);
+    }
+    st_w3.store(reinterpret_cast<T*>(smem + S::OFF_W3), tid);
+  }
+#pragma unroll
+  for (int i = 0; i < ITB; ++i) {
+    bool live;
+    (void)bias_src(tid + i * NTH, live);
+    if (tid + i * NTH < NBIAS) sB1[tid + i * NTH] = live ? bias_v[i] : 0.f;
+  }
+  stamp(10);  // weights + biases stored (their loads have arrived)
   // look-ahead indices: issued after every load the staging barrier waits for (in-order vmcnt)
   if constexpr (LOOK) {
     if (look) {
-      const int nidx = br.step_ptr[2];
+      const int nidx = br.step_ptr[2], step = br.step_ptr[0];
 #pragma unroll
       for (int j = 0; j < GIT2; ++j) {
         const int e = tid + j * NTH, r = e / 49;
@@ -247,28 +310,48 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       }
     }
   } else {
-    constexpr int VE = 16 / (int)sizeof(T);
-    constexpr int CH = H::K0P / VE;
-    const T* xin = reinterpret_cast<const T*>(hb.xin);
     T* xT = reinterpret_cast<T*>(hb.xT);
-    for (int e = tid; e < R * CH; e += NTH) {
-      const int r = e % R, k = (e / R) * VE;
-      uint4 u = make_uint4(0, 0, 0, 0);
-      if (r0 + r < B) u = *reinterpret_cast<const uint4*>(xin + (size_t)(r0 + r) * H::K0P + k);
-      *reinterpret_cast<uint4*>(sX + r * S::PX + k) = u;
-      if constexpr (TRAIN) {
-        const T* tv = reinterpret_cast<const T*>(&u);
+    // element j of a 16-byte chunk, as raw bits (register extracts: a pointer-punned read of the chunk
+    // array put it on the scratch stack)
+    auto word = [](const u32x4& v, int w) { return v[w]; };
 #pragma unroll
-        for (int j = 0; j < VE; ++j) xT[(size_t)(k + j) * ldB + r0 + r] = tv[j];
+    for (int i = 0; i < ITX; ++i) {
+      const int e = tid + i * NTH, r = (e % (R / 4)) * 4, k = (e / (R / 4)) * XVE;
+      if (e < NXE) {
+        u32x4 rv[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          rv[q] = r0 + r + q < B ? xv[i][q] : u32x4{0u, 0u, 0u, 0u};
+          *reinterpret_cast<u32x4*>(sX + (r + q) * S::PX + k) = rv[q];
+        }
+        if constexpr (TRAIN) {
+#pragma unroll
+          for (int j = 0; j < XVE; ++j) {
+            T* dst = xT + (size_t)(k + j) * ldB + r0 + r;
+            if constexpr (sizeof(T) == 2) {
+              const int w = j >> 1, sh = 16 * (j & 1);
+              const uint32_t lo = ((word(rv[0], w) >> sh) & 0xFFFFu) | (((word(rv[1], w) >> sh) & 0xFFFFu) << 16);
+              const uint32_t hi = ((word(rv[2], w) >> sh) & 0xFFFFu) | (((word(rv[3], w) >> sh) & 0xFFFFu) << 16);
+              *reinterpret_cast<u32x2*>(dst) = u32x2{lo, hi};
+            } else {
+              *reinterpret_cast<u32x4*>(dst) = u32x4{word(rv[0], j), word(rv[1], j), word(rv[2], j), word(rv[3], j)};
+            }
+          }
+        }
       }
     }
+    stamp(11);  // input tile stored to LDS, xT stores issued
   }
   __syncthreads();
   stamp(1);
   // labels: fetched by the LAST threads of the block (idle in L1 when NWV > NT1), used after 3 barriers
+  const int gstep = br.step_ptr[1];  // dropout stream (read after the staging barrier, see batch_idx)
   if (!look) {
     const int t = tid - (NTH - R);
-    if (t >= 0) sLab[t] = sIdx[t] >= 0 ? (int)br.labels[sIdx[t]] : 0;
+    if (t >= 0) {
+      const int id = H::GATHER ? sIdx[t] : ((r0 + t < B) ? batch_idx()[r0 + t] : -1);
+      sLab[t] = id >= 0 ? (int)br.labels[id] : 0;
+    }
   }
   // look-ahead: the next step's pixels / labels (indices were loaded during the staging)
   uint4 gv[GIT2];
@@ -733,7 +816,9 @@ struct WgArgs {
   // XCD-aware mode (xcd_ch > 0): 1-D grid; workgroup L runs on XCD L % 8 (round-robin dispatch) and
   // reads only the batch rows the head kernel wrote from that XCD -- row chunks c = x, x+8, ... of
   // xcd_ch rows (= head rows per workgroup) -- so its operands hit the XCD's own L2.
-  int xcd_ch, nch, sx;  // chunk rows, chunk count, splits per XCD
+  // contig: the head used the XCD-contiguous mapping (xcd_unit), so XCD x wrote chunks
+  // [x * nch / 8, (x + 1) * nch / 8) instead of x, x + 8, ...
+  int xcd_ch, nch, sx, contig;  // chunk rows, chunk count, splits per XCD
   float* slab;
   SgdFuse sgd;          // used when fuse != 0 (then splits == 1)
   int fuse;
@@ -758,7 +843,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
     tile = q / a.sx;
     const int sub = q % a.sx;
     split = x * a.sx + sub;
-    const int mx = x < a.nch ? (a.nch - x + 7) / 8 : 0;  // chunks owned by XCD x
+    const int mx = a.contig ? a.nch / 8 : (x < a.nch ? (a.nch - x + 7) / 8 : 0);  // chunks owned by XCD x
     m0 = sub * mx / a.sx;
     const int m1 = (sub + 1) * mx / a.sx;
     spc = a.xcd_ch / KC;
@@ -766,7 +851,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
   }
   auto step_row = [&](int st) -> int {  // first batch row of step st (may be >= Bp: skipped)
     if (a.xcd_ch == 0) return rs + st * KC;
-    return (x + 8 * (m0 + st / spc)) * a.xcd_ch + (st % spc) * KC;
+    const int m = m0 + st / spc;
+    return (a.contig ? x * (a.nch / 8) + m : x + 8 * m) * a.xcd_ch + (st % spc) * KC;
   };
   int j = 0;
   while (j + 1 < a.njobs && tile >= a.job[j + 1].blk_begin) ++j;
@@ -972,6 +1058,8 @@ int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab
     a.xcd_ch = xcd_ch;
     a.nch = (a.Bp + xcd_ch - 1) / xcd_ch;
     a.sx = splits / 8;
+    const int head_grid = (rup(B, 32) + xcd_ch - 1) / xcd_ch;  // head_launch_mtw's grid
+    a.contig = hb.xcd && head_grid % 8 == 0 && a.nch == head_grid;
     hipLaunchKernelGGL(wgrad_kernel<T>, dim3(blk * splits), dim3(256), 0, s, a);
   } else if (a.fuse) {
     hipLaunchKernelGGL((wgrad_sgd_kernel<T, Model>), dim3(blk), dim3(256), 0, s, a);

@@ -23,6 +23,9 @@ struct BatchRef {
   // Null: every kernel gathers through idx_epoch itself.
   uint8_t* xnext = nullptr;
   uint8_t* ynext = nullptr;
+  // XCD-contiguous work mapping (xcd_unit in common.h): conv_fwd, the head and conv_bwd give XCD x the
+  // same contiguous eighth of the batch, so a kernel reads what the previous one wrote from its own L2
+  int32_t xcd = 0;
 };
 
 // Gather the rows of the CURRENT step (step_ptr[0]) into br.xnext / br.ynext (primes the look-ahead
@@ -46,6 +49,7 @@ struct HeadBuffers {
   int32_t ldB;
   uint32_t seed;
   float drop_p;
+  int32_t xcd = 0;       // the head kernel used the XCD-contiguous row mapping (BatchRef::xcd)
 };
 
 struct LenetConvBuffers {

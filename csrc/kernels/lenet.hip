@@ -119,7 +119,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   T* p2s = reinterpret_cast<T*>(smem + S::OFF_P2);
   uint8_t* m2s = reinterpret_cast<uint8_t*>(smem + S::OFF_M2);
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
-  const BlockIdx bidx(br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride, blockIdx.x * ipb, ipb, br.B);
+  const int unit = xcd_unit(blockIdx.x, gridDim.x, br.xcd);  // this workgroup's images: [unit * ipb, +ipb)
+  const BlockIdx bidx(br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride, unit * ipb, ipb, br.B);
   const T* pack = reinterpret_cast<const T*>(cb.pack);
   const float* prm = cb.params;
   // optional wall-clock stamps (profiling): [0] start, [1] setup, 3 per image for images 0..3, [14] loop end
@@ -141,7 +142,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   // stage, and images past the batch are masked with `valid`.
   auto fetch = [&](int t) -> Raw {  // software pipeline: image t+1's bytes are in flight during image t
     Raw r;
-    const bool live = t < ipb && blockIdx.x * ipb + t < br.B;  // wave-uniform
+    const bool live = t < ipb && unit * ipb + t < br.B;  // wave-uniform
     const uint8_t* rowp = br.images + (size_t)bidx[live ? t : 0] * 784 + min(sy - 2, 27) * 28;
 #pragma unroll
     for (int k = 0; k < 5; ++k) r.d[k] = *reinterpret_cast<const uint32_t*>(rowp + min(max(8 * sg - 4 + 4 * k, 0), 24));
@@ -283,7 +284,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   __syncthreads();
   stamp(1);
   for (int t = 0; t < ipb; ++t) {
-    const int b = blockIdx.x * ipb + t;
+    const int b = unit * ipb + t;
     const bool valid = b < br.B;
     const Raw u = u_next;
     // ---- stage: normalise once, 4 aligned 16-byte plane stores per thread
@@ -398,7 +399,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   }
   stamp(14);
   if (cb.stamps && tid == 0 && blockIdx.x < 1024) cb.stamps[(1024 + blockIdx.x) * 16 + 15] = hw_location();
-  flush_p2(blockIdx.x * ipb + ipb - 1);
+  flush_p2(unit * ipb + ipb - 1);
 }
 
 // ====================================================================================
@@ -460,7 +461,8 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   uint8_t* m1s = reinterpret_cast<uint8_t*>(smem + S::OFF_M1);
   float* red = reinterpret_cast<float*>(smem + S::OFF_RED);
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
-  const BlockIdx bidx(br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride, blockIdx.x * ipb, ipb, br.B);
+  const int unit = xcd_unit(blockIdx.x, gridDim.x, br.xcd);  // images [unit * ipb, +ipb), slab row unit
+  const BlockIdx bidx(br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride, unit * ipb, ipb, br.B);
   const T* pack = reinterpret_cast<const T*>(cb.pack);
   const T* dp2 = reinterpret_cast<const T*>(cb.dp2);
   const T* p1g = reinterpret_cast<const T*>(cb.p1);
@@ -489,8 +491,8 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   // without the role / of images past the batch zeroed at use), so vmcnt accounting stays exact.
   auto fetch = [&](int t) -> Pre {
     Pre f;
-    const bool live = t < ipb && blockIdx.x * ipb + t < br.B;  // wave-uniform
-    const int bb = min(blockIdx.x * ipb + t, br.B - 1);
+    const bool live = t < ipb && unit * ipb + t < br.B;  // wave-uniform
+    const int bb = min(unit * ipb + t, br.B - 1);
     if constexpr (HD) {
       const uint8_t* rowp = br.images + (size_t)bidx[live ? t : 0] * 784 + ((tid >> 2) % 28) * 28;
 #pragma unroll
@@ -603,7 +605,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
 
 
   for (int t = 0; t < ipb; ++t) {
-    const int b = blockIdx.x * ipb + t;
+    const int b = unit * ipb + t;
     const bool valid = b < br.B;
     const Pre cur = nxt;
     // ---- phase A: stage input (5 shifted copies), pool1 (5 shifted channel-major copies),
@@ -891,8 +893,8 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   }
   stamp(14);
 
-  // ---- write this workgroup's partial gradients (slab row = blockIdx.x)
-  float* out = cb.slab + (size_t)blockIdx.x * L::CONV_PARAMS;
+  // ---- write this workgroup's partial gradients (slab row = unit)
+  float* out = cb.slab + (size_t)unit * L::CONV_PARAMS;
 #pragma unroll
   for (int i = 0; i < NWT; ++i) {
     if (!HW || i >= nw) break;

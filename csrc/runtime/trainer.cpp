@@ -61,6 +61,13 @@ bool split_bwd() {
   }();
   return on;
 }
+// XCD-contiguous work mapping of conv_fwd / head / conv_bwd / FC wgrad (common.h xcd_unit): on unless
+// MNIST_AMD_NO_XCD is set (A/B knob; the mapping changes which images a conv_bwd slab row sums, so the
+// conv gradients differ from the unmapped run by float summation order only)
+int xcd_map() {
+  static const int on = std::getenv("MNIST_AMD_NO_XCD") == nullptr ? 1 : 0;
+  return on;
+}
 // MNIST_AMD_TRACE=1: log every orchestration call of a step to stderr (host-side debugging)
 void trace(const char* what) {
   static const bool on = [] {
@@ -129,6 +136,7 @@ BatchRef Trainer::batch_ref(int B) const {
   br.B = B;
   br.xnext = ptr<uint8_t>(p_.xnext);
   br.ynext = ptr<uint8_t>(p_.ynext);
+  br.xcd = xcd_map();
   return br;
 }
 
@@ -156,6 +164,7 @@ HeadBuffers Trainer::head_buffers(float* metrics) const {
   hb.ldB = ldb_;
   hb.seed = seed_;
   hb.drop_p = drop_p_;
+  hb.xcd = xcd_map();
   return hb;
 }
 

@@ -50,6 +50,10 @@ rows = 16 if B <= tr.C.L1_SPLIT_MAX_B else 64  # split path: 16-row tiles
 nblk = (B + rows - 1) // rows
 if model == "lenet5":
     report("head", allst[:nblk], ["idx+stage X", "L1", "L2", "L3", "softmax", "dH2", "dH1", "dX"], 8)
+    # inside the staging phase: [0] entry -> [9] loads issued -> [10] weights stored -> [11] X stored -> [1] barrier
+    hs = allst[:nblk][:, [0, 9, 10, 11, 1]]
+    if (hs[:, 1:4] > 0).all():
+        report("head staging", hs, ["issue loads", "wait+W stores", "X stores", "barrier"], 4)
 else:  # no dX phase: stamp 7 is never written, dH1 ends at stamp 8
     allst[:nblk, 7] = allst[:nblk, 8]
     report("head", allst[:nblk], ["idx+stage X", "L1", "L2", "L3", "softmax", "dH2", "dH1"], 8)
@@ -80,6 +84,8 @@ if model == "lenet5":
         nwg = np.array([n for n, _ in cus.values()])
         xccs = sorted({k // 4096 for k in cus})
         per_xcc = " ".join(f"x{x}:{max(m for k, (_, m) in cus.items() if k // 4096 == x):.1f}" for x in xccs)
+        rr = np.mean(((loc >> 32) & 15) == (np.arange(len(loc)) % 8))
+        print(f"{title}: workgroup g on XCD g % 8 for {100 * rr:.1f}% of workgroups")
         print(f"{title} per-CU: {len(cus)} CUs, workgroups/CU min {nwg.min()} max {nwg.max()}; CU finish "
               f"mean {fin.mean():.2f} us  min {fin.min():.2f}  p90 {np.percentile(fin, 90):.2f}  max {fin.max():.2f}; "
               f"per-XCC max {per_xcc}")
