@@ -68,6 +68,14 @@ int xcd_map() {
   static const int on = std::getenv("MNIST_AMD_NO_XCD") == nullptr ? 1 : 0;
   return on;
 }
+// Deferred aux-branch join inside multi-step graphs (default on; MNIST_AMD_DEFER_JOIN=0 joins every step)
+bool defer_join() {
+  static const bool on = [] {
+    const char* e = std::getenv("MNIST_AMD_DEFER_JOIN");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return on;
+}
 // MNIST_AMD_TRACE=1: log every orchestration call of a step to stderr (host-side debugging)
 void trace(const char* what) {
   static const bool on = [] {
@@ -263,7 +271,7 @@ std::vector<Bucket> Trainer::issued_collectives() const {
   return coalesced_buckets();
 }
 
-void Trainer::launch_step(int B, hipStream_t s) {
+void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
   if (B <= 0 || B > batch_) throw std::invalid_argument("train_step: bad batch size");
   const BatchRef br = batch_ref(B);
   const HeadBuffers hb = head_buffers(ptr<float>(p_.metrics));
@@ -272,6 +280,13 @@ void Trainer::launch_step(int B, hipStream_t s) {
   if (model_ == ModelKind::LENET) {
     launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(), s);
     post_launch(s);
+  }
+  if (aux_pending_) {
+    // deferred join of the previous step's aux branch: the head overwrites the activations its FC wgrad
+    // read and reads the FC weights its FC update wrote (conv_fwd touches neither, so it ran without
+    // waiting: the join's cross-queue latency is off the conv_bwd -> conv update -> conv_fwd chain)
+    HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));
+    aux_pending_ = false;
   }
   const int hrows = launch_head(model_, dtype_, true, br, hb, head_rows_per_block(model_, dtype_, batch_), s);
   post_launch(s);
@@ -303,7 +318,10 @@ void Trainer::launch_step(int B, hipStream_t s) {
                       ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, nullptr, aux_stream_);
     post_launch(aux_stream_);
     HIP_CHECK(hipEventRecord(events_[5], aux_stream_));
-    HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));
+    // the conv update touches only conv parameters / operand images and the step counters (which no aux
+    // kernel reads): with defer_join it follows conv_bwd directly, the join moves to the next head
+    if (defer_join) aux_pending_ = true;
+    else HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));
     launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
                       nparam_, splits, cp, 0, cp, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
                       ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, ptr<int32_t>(p_.step), s);
@@ -432,8 +450,12 @@ void Trainer::capture_into(hipStream_t s, int nsteps, hipGraph_t* graph, hipGrap
   trace("capture: begin");
   HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
   try {
-    for (int i = 0; i < nsteps; ++i) launch_step(batch_, s);
+    // steps inside one graph leave their aux branch to the next step's head; the last one joins it
+    aux_pending_ = false;
+    for (int i = 0; i < nsteps; ++i) launch_step(batch_, s, defer_join() && i + 1 < nsteps);
+    if (aux_pending_) throw std::logic_error("capture: aux branch left un-joined");
   } catch (...) {
+    aux_pending_ = false;
     hipGraph_t g = nullptr;
     hipStreamEndCapture(s, &g);
     if (g) hipGraphDestroy(g);

@@ -111,7 +111,9 @@ class Trainer {
   BatchRef batch_ref(int B) const;
   HeadBuffers head_buffers(float* metrics) const;
   LenetConvBuffers conv_buffers() const;
-  void launch_step(int B, hipStream_t s);
+  // defer_join: (single GPU, concurrent schedule, inside a multi-step graph) leave the aux branch (FC
+  // wgrad + FC update) un-joined at the end of the step; the NEXT step's head waits for it instead.
+  void launch_step(int B, hipStream_t s, bool defer_join = false);
   void launch_lenet_comm_tail(int B, int nslab, int splits, hipStream_t s);
   struct GraphSlot {
     hipGraph_t graph = nullptr;
@@ -141,6 +143,7 @@ class Trainer {
   hipStream_t comm_stream_ = nullptr;
   hipStream_t aux_stream_ = nullptr;  // concurrent FC wgrad branch (fork/join inside the step graph)
   std::vector<hipEvent_t> events_;
+  bool aux_pending_ = false;  // the aux branch of the previous step is not joined yet (events_[5])
   std::map<uint64_t, GraphSlot> graphs_;
   int multi_k_ = 0;
   int zero_step_dev_ = 0;
