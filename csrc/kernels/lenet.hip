@@ -825,18 +825,25 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
           const T* a0 = dys + ((y0 + 4) * 18 + x + 4) * 16;
           const T* a1 = dys + ((y1 + 4) * 18 + x + 4) * 16;
           f32x4 acc0 = zero4(), acc1 = zero4();
-          Frag fb = M::load(bq), fa0 = M::load(a0 + doff[0]), fa1 = M::load(a1 + doff[0]);
+          // Row y1 = y0 + 2 sees the SAME dY2 window two kernel rows (kh' + 2 = SH chunks) later:
+          // A(y1, kc) = A(y0, kc - SH).  Tile y0's fragments stay in registers for SH chunks, so tile
+          // y1 loads only its first SH chunks (20 instead of 30 A reads per pair for bf16).
+          constexpr int SH = 160 / KC;  // chunks per two kernel rows (10 taps x 16 channels)
+          static_assert(SH < D2CH, "row-pair A reuse needs more than two kernel rows of K");
+          Frag A0[D2CH];
+          Frag fb = M::load(bq), fa1 = M::load(a1 + doff[0]);
+          A0[0] = M::load(a0 + doff[0]);
 #pragma unroll
           for (int kc = 0; kc < D2CH; ++kc) {  // next chunk's fragments in flight during this one's MFMAs
-            Frag nb = fb, na0 = fa0, na1 = fa1;
+            Frag nb = fb, na1 = fa1;
             if (kc + 1 < D2CH) {
               nb = M::load(bq + (kc + 1) * KC);
-              na0 = M::load(a0 + doff[kc + 1]);
-              na1 = M::load(a1 + doff[kc + 1]);
+              A0[kc + 1] = M::load(a0 + doff[kc + 1]);
+              na1 = kc + 1 < SH ? M::load(a1 + doff[kc + 1]) : A0[kc + 1 - SH];
             }
-            M::mma(acc0, fa0, fb);
+            M::mma(acc0, A0[kc], fb);
             M::mma(acc1, fa1, fb);
-            fb = nb; fa0 = na0; fa1 = na1;
+            fb = nb; fa1 = na1;
           }
           dgrad_tile_epi(y0, acc0);
           dgrad_tile_epi(y1, acc1);
