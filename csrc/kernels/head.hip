@@ -139,7 +139,12 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   const int B = br.B;
   // The device step counters are read where they are needed, not here: a scalar load issued at the top
   // made every later scalar-operand wait (lgkmcnt(0)) -- the first weight loads included -- wait for it.
+  // (Exception: the MLP head gathers and draws dropout masks with them early on, so for it -- the model
+  //  with the dropout / look-ahead paths -- both counters are still read here.)
   auto batch_idx = [&] { return br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride; };
+  constexpr bool EARLY_STEP = H::GATHER || H::DROPOUT;
+  const int step_early = EARLY_STEP ? br.step_ptr[0] : 0;
+  const int gstep_early = EARLY_STEP ? br.step_ptr[1] : 0;
   const T* pack = reinterpret_cast<const T*>(hb.pack);
   const float* prm = hb.params;
   const int ldB = hb.ldB;
@@ -201,7 +206,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   if (look) {
     if (tid < R) sLab[tid] = (r0 + tid < B) ? (int)br.ynext[r0 + tid] : 0;
   } else if (H::GATHER && tid < R) {
-    sIdx[tid] = (r0 + tid < B) ? batch_idx()[r0 + tid] : -1;
+    sIdx[tid] = (r0 + tid < B) ? br.idx_epoch[(size_t)step_early * br.batch_stride + r0 + tid] : -1;
   }
   RowStager<T, NTH, H::N2P, H::N1P, S::PW2> st_w2;
   RowStager<T, NTH, H::N1P, H::N2P, S::PW2T> st_w2t;
@@ -270,7 +275,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   // look-ahead indices: issued after every load the staging barrier waits for (in-order vmcnt)
   if constexpr (LOOK) {
     if (look) {
-      const int nidx = br.step_ptr[2], step = br.step_ptr[0];
+      const int nidx = br.step_ptr[2], step = step_early;
 #pragma unroll
       for (int j = 0; j < GIT2; ++j) {
         const int e = tid + j * NTH, r = e / 49;
@@ -345,7 +350,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   __syncthreads();
   stamp(1);
   // labels: fetched by the LAST threads of the block (idle in L1 when NWV > NT1), used after 3 barriers
-  const int gstep = br.step_ptr[1];  // dropout stream (read after the staging barrier, see batch_idx)
+  const int gstep = EARLY_STEP ? gstep_early : br.step_ptr[1];  // dropout stream (see batch_idx)
   if (!look) {
     const int t = tid - (NTH - R);
     if (t >= 0) {
