@@ -237,7 +237,7 @@ class NativeTrainer:
         if "plan" in cfg or "bwd_blocks" in cfg:
             self.set_plan(cfg.get("plan", self.plan), int(cfg.get("bwd_blocks", 0)))
 
-    def autotune_plan(self, candidates=None, iters: int = 16, warmup: int = 3, reduce_max=None,
+    def autotune_plan(self, candidates=None, iters: int = 48, warmup: int = 8, reduce_max=None,
                       margin: float = 0.015, log=None) -> dict:
         """Time each candidate step schedule and keep the fastest (a start-up calibration, like
         cudnn.benchmark).
@@ -257,6 +257,12 @@ class NativeTrainer:
         all-reduce) makes the decision identical on every rank.  Parameters, momentum, counters and
         metrics are restored afterwards, and the chosen schedule's graphs are left ready to replay.
         ``MNIST_AMD_MG_SCHED=join|split`` pins the multi-GPU plan.
+
+        48 timed replays per candidate (after 8 untimed rounds): with RCCL in the step the per-replay
+        times jitter with the collective's latency, and the median of 48 separates plans a few percent
+        apart.  At W = 1 this is ~15 ms of GPU work (~25 ms for the three multi-GPU candidates at W = 8);
+        it also brings the GPU from idle to its sustained clock before the caller's warm-up steps
+        (measured: steps 1-20 after a cold start run ~6 % slower than steps 100+, scripts/step_times.py).
         """
         from ..parallel.ddp import choose_plan, default_plan_candidates, local_plan_candidates
         forced = os.environ.get("MNIST_AMD_MG_SCHED")
