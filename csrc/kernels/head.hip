@@ -512,6 +512,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   };
 
   prefetch_dx();
+  stamp(12);  // dX operand loads issued
 
   // ---------------------------------------------------------------- softmax cross-entropy
   // Every thread takes one (row, class) pair: t -> r = t >> 4, c = t & 15, so a row is one 16-lane
@@ -541,6 +542,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
         sD[r * S::PD + 16 + c] = to_t<T>(0.f);  // K padding of the dH2 product (NCK = 32)
       }
     }
+    stamp(13);  // softmax rows done (before the metric reductions)
     loss = wave_sum(loss);
     corr = wave_sum(corr);
     cnt = wave_sum(cnt);
@@ -564,6 +566,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       atomicAdd(hb.metrics + 2, c);
     }
   };
+  stamp(14);  // metric partials stored (before the barrier)
   __syncthreads();
   stamp(5);
   if constexpr (!TRAIN) {

@@ -54,6 +54,10 @@ if model == "lenet5":
     hs = allst[:nblk][:, [0, 9, 10, 11, 1]]
     if (hs[:, 1:4] > 0).all():
         report("head staging", hs, ["issue loads", "wait+W stores", "X stores", "barrier"], 4)
+    # inside the softmax phase: [4] start -> [12] dX loads issued -> [13] rows done -> [14] partials -> [5] barrier
+    ss = allst[:nblk][:, [4, 12, 13, 14, 5]]
+    if (ss[:, 1:4] > 0).all():
+        report("head softmax", ss, ["dX prefetch", "softmax rows", "metric sums", "barrier"], 4)
 else:  # no dX phase: stamp 7 is never written, dH1 ends at stamp 8
     allst[:nblk, 7] = allst[:nblk, 8]
     report("head", allst[:nblk], ["idx+stage X", "L1", "L2", "L3", "softmax", "dH2", "dH1"], 8)
