@@ -438,7 +438,6 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   }
   __syncthreads();
   stamp(2);
-
   // ---------------------------------------------------------------- L2: H2 = relu(H1 W2^T + b2)
   {
     constexpr int NT = H::N2P / 16, KCH = H::N1P / KC;
@@ -494,7 +493,9 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   stamp(4);
 
   // ---- dX operands (W1^T, [K0 rows][N1P]): the first two n-tiles of this wave, fetched now so the
-  //      L2/MALL latency hides behind softmax, dH2 and dH1
+  //      L2/MALL latency hides behind softmax, dH2 and dH1.  (Their issue -- 128 wave-loads per CU --
+  //      occupies the CU's memory pipeline for ~1.5 us wherever it is placed: issued at the start of layer 2
+  //      the softmax phase drops 2.5 -> 1.0 us and layer 2 grows 1.0 -> 2.8 us.)
   constexpr int NTX = rup(H::K0, 16) / 16, KCHX = H::N1P / KC, PXT = KCHX <= 4 ? 2 : 1;  // <= 32 VGPRs
   Frag bx[H::DX && TRAIN ? PXT : 1][KCHX];
   auto prefetch_dx = [&] {
@@ -543,9 +544,14 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       }
     }
     stamp(13);  // softmax rows done (before the metric reductions)
-    loss = wave_sum(loss);
-    corr = wave_sum(corr);
-    cnt = wave_sum(cnt);
+    // only the class-0 lane of each 16-lane row accumulates (lanes 0, 16, 32, 48: c = lane & 15 in every
+    // iteration), so the wave total is those four lanes -- bitwise what wave_sum gives (its row sums add
+    // zeros), without its three dependent DPP chains
+    static_assert(NTH % 16 == 0, "class index = lane & 15 in every softmax iteration");
+    auto rows4 = [](float v) { return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48)); };
+    loss = rows4(loss);
+    corr = rows4(corr);
+    cnt = rows4(cnt);
     if (lane == 0) {
       sPart[w * 4 + 0] = loss;
       sPart[w * 4 + 1] = corr;
@@ -567,6 +573,8 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
     }
   };
   stamp(14);  // metric partials stored (before the barrier)
+  // per-wave arrival at the softmax barrier (profiling stamps, rows 512 + block, one slot per wave)
+  if (hb.stamps && lane == 0 && w < 16 && blockIdx.x < 512) hb.stamps[(512 + blockIdx.x) * 16 + w] = wall_clock64();
   __syncthreads();
   stamp(5);
   if constexpr (!TRAIN) {

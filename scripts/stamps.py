@@ -58,6 +58,11 @@ if model == "lenet5":
     ss = allst[:nblk][:, [4, 12, 13, 14, 5]]
     if (ss[:, 1:4] > 0).all():
         report("head softmax", ss, ["dX prefetch", "softmax rows", "metric sums", "barrier"], 4)
+        pw = allst[512:512 + nblk, :16]
+        if (pw > 0).all():
+            rel = (pw - allst[:nblk, 4][:, None]) * 10 / 1000.0
+            print("  per-wave arrival at the softmax barrier (us after phase start): " +
+                  " ".join(f"w{i}:{rel[:, i].mean():.2f}" for i in range(16)))
 else:  # no dX phase: stamp 7 is never written, dH1 ends at stamp 8
     allst[:nblk, 7] = allst[:nblk, 8]
     report("head", allst[:nblk], ["idx+stage X", "L1", "L2", "L3", "softmax", "dH2", "dH1"], 8)
