@@ -9,12 +9,21 @@ Each timed step is a COMPLETE data-parallel training step through the native pat
 normalise of the step's samples from the HBM-resident uint8 dataset, LeNet-5 forward and
 backward (hand-written CDNA4 MFMA kernels, bf16 inputs / fp32 accumulate / fp32 master
 weights), at N > 1 the gradient all-reduce over the native RCCL communicator (the step plan --
-one coalesced all-reduce after the backward join, or the FC bucket sent beside conv_bwd -- is
-chosen at start-up by timing both on the real communicator and is reported in the JSON), and
-the SGD-momentum update, replayed as one hipGraph per step.
+one coalesced all-reduce after the backward join, or the FC bucket + FC update sent beside
+conv_bwd -- is chosen at start-up by timing both on the real communicator and is reported in the
+JSON), and the SGD-momentum update, replayed as hipGraphs.  The reference MLP (``--model mlp``)
+runs with the reference's Dropout(0.2) in the timed step.
 The DistributedSampler(seed=42) order of every epoch the run touches is computed
 before timing and kept in HBM (the step counter crosses epoch boundaries on the device).
 Data: synthetic 28x28 uint8 images of the MNIST shape (no network), random init.
+
+Timing: W untimed warm-up steps; then every rank passes a barrier, synchronises its device and
+times exactly K steps ending with its own device synchronisation; the reported time is the MAX of
+the per-rank times (one gloo max-reduction AFTER the clock stops -- no collective or barrier inside
+the timed region other than the step's own gradient all-reduces).
+With a communicator the JSON carries ``comm_profile``: the RCCL world, the latency of each bucket's
+standalone all-reduce, and the exposed communication (step with the plan's collectives minus the
+local schedule without any, interleaved replays).
 
 Launch:
   ``python bench.py`` (1 GPU);
@@ -22,6 +31,8 @@ Launch:
   before this parent touches a GPU) and relays rank 0's JSON line;
   ``python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
   --master-port P bench.py --gpus N --steps K --warmup W`` runs the ranks under torchrun.
+  ``--comm gloo`` exchanges gradients over c10d gloo through host memory instead of RCCL; ranks may
+  then share one GPU (test path: the multi-process chain on a one-GPU box).
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -49,7 +60,10 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=8192, help="per-GPU batch")
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--momentum", type=float, default=0.9)
-    ap.add_argument("--comm", default="rccl", choices=["rccl", "torch"])
+    ap.add_argument("--dropout", type=float, default=None,
+                    help="dropout after layer 1 (default: the reference's 0.2 for --model mlp; LeNet-5 has none)")
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "torch", "gloo"],
+                    help="gradient data plane: native RCCL (default), c10d nccl, or c10d gloo via host memory")
     ap.add_argument("--plan", default="auto", choices=["auto", "join", "split", "fixed"],
                     help="step plan: auto = time the candidates at start-up and keep the fastest "
                          "(multi-GPU plans, or the single-GPU schedules); join/split = that multi-GPU plan; "
@@ -57,11 +71,15 @@ def parse(argv=None):
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--comm-world1", action="store_true",
                     help="attach a world-1 RCCL communicator (runs the multi-GPU step schedule on one GPU)")
+    ap.add_argument("--synthetic-mode", default="easy", choices=["easy", "hard"],
+                    help="synthetic data generator (hard: stronger noise / affine jitter, top-1 below 1.0)")
     ap.add_argument("--eval", action="store_true", default=True)
     ap.add_argument("--no-eval", dest="eval", action="store_false")
     ap.add_argument("--json-out", default=None)
     ap.add_argument("--digest", action="store_true",
                     help="every rank prints a sha256 of its final parameters to stderr (replica consistency check)")
+    ap.add_argument("--dump-params", default=None,
+                    help="every rank saves its final parameter slab to PATH.rank<r>.pt (tests)")
     ap.add_argument("--dry-run", action="store_true",
                     help="check the launch wiring only: every rank validates its env, rank 0 prints a JSON line, no GPU")
     return ap.parse_args(argv)
@@ -104,6 +122,49 @@ def dry_run(a) -> int:
     return 0
 
 
+def bench_data(world: int, rank: int, batch: int, total_steps: int, mode: str = "easy"):
+    """The run's data: the MNIST-shaped synthetic train split (repeated so every rank has >= 8 full
+    batches per epoch), the test split, and this rank's DistributedSampler(seed=42) order of every epoch
+    the run touches, each cut to its full batches and laid end to end (the device step counter walks
+    from one epoch straight into the next, so no index upload or counter reset sits between timed
+    steps).  Deterministic: tests rebuild it to emulate the ranks in one process."""
+    import numpy as np
+    import torch
+
+    from pytorch_ddp_mnist_amd.data.sampler import epoch_indices, num_samples
+    from pytorch_ddp_mnist_amd.data.synthetic import make_split
+    base_x, base_y = make_split(60000, seed=1, mode=mode)
+    reps = max(1, -(-(world * batch * 8) // 60000))
+    n = 60000 * reps
+    images = np.tile(base_x.reshape(-1, 784), (reps, 1))
+    labels = np.tile(base_y, reps)
+    ns = num_samples(n, world)
+    steps_per_epoch = ns // batch
+    n_epochs = -(-total_steps // steps_per_epoch)
+    idx_all = torch.cat([epoch_indices(n, world, rank, e, seed=42)[: steps_per_epoch * batch]
+                         for e in range(n_epochs)]).to(torch.int32)
+    test_x, test_y = make_split(10000, seed=2, mode=mode)
+    return torch.from_numpy(images), torch.from_numpy(labels), idx_all, test_x, test_y
+
+
+def timed_region(ctx, tr, run, steps: int, cuda_sync, clock=time.perf_counter) -> float:
+    """Time exactly ``steps`` steps on every rank; returns the max over ranks (seconds).
+
+    A barrier + device sync puts every rank at the start line; each rank's clock stops after its own
+    stream drained (the trainer's synchronize() is the collective watchdog with a communicator).  The
+    rank-max reduction runs after both clock reads: nothing but the steps themselves (and their
+    gradient all-reduces) is inside the timed region."""
+    tr.synchronize()
+    ctx.barrier()
+    cuda_sync()
+    t0 = clock()
+    run(steps)
+    tr.synchronize()
+    cuda_sync()
+    t1 = clock()
+    return ctx.all_reduce_max(t1 - t0)
+
+
 def main(argv=None) -> int:
     a = parse(argv)
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -113,93 +174,74 @@ def main(argv=None) -> int:
 
     import torch
 
-    from pytorch_ddp_mnist_amd.data.sampler import epoch_indices, num_samples
-    from pytorch_ddp_mnist_amd.data.synthetic import make_split
-    from pytorch_ddp_mnist_amd.engine.native import NativeTrainer
+    from pytorch_ddp_mnist_amd.engine.native import NativeTrainer, resolve_plan
     from pytorch_ddp_mnist_amd.models import build_model
     from pytorch_ddp_mnist_amd.parallel.comm import init_distributed
     from pytorch_ddp_mnist_amd.parallel.ddp import model_phases, plan_buckets
 
+    pinned = resolve_plan(a.plan)   # validates --plan before any device work
+    dropout = a.dropout if a.dropout is not None else (0.2 if a.model == "mlp" else 0.0)
+    if a.model == "lenet5" and dropout:
+        raise SystemExit("LeNet-5 has no dropout layer")
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    ctx = init_distributed(None, parallel=world_env > 1, device="cuda", comm=a.comm)
+    ctx = init_distributed(None, parallel=world_env > 1, device="cuda", comm=a.comm,
+                           share_device=a.comm == "gloo")
     if ctx.world != a.gpus and ctx.rank == 0:
         print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={ctx.world}; using {ctx.world}", file=sys.stderr)
     W, rank, dev = ctx.world, ctx.rank, ctx.device
 
-    # ---- data: MNIST-shaped synthetic set; repeated so every rank has >= 8 full batches per epoch
-    base_x, base_y = make_split(60000, seed=1)
-    reps = max(1, -(-(W * a.batch * 8) // 60000))
-    N = 60000 * reps
-    images = torch.from_numpy(base_x.reshape(-1, 784)).to(dev).repeat(reps, 1)
-    labels = torch.from_numpy(base_y).to(dev).repeat(reps)
-    test_x, test_y = make_split(10000, seed=2)
-
-    ns = num_samples(N, W)
-    steps_per_epoch = ns // a.batch
-    total = a.warmup + a.steps
-    n_epochs = -(-total // steps_per_epoch)
-    # DistributedSampler(seed=42) order of every epoch the run touches, each cut to its full batches and
-    # laid end to end in HBM before timing: the device step counter walks from one epoch straight into
-    # the next, so no index upload or counter reset sits between timed steps
-    idx_all = torch.cat([epoch_indices(N, W, rank, e, seed=42)[: steps_per_epoch * a.batch]
-                         for e in range(n_epochs)]).to(torch.int32)
+    images, labels, idx_all, test_x, test_y = bench_data(W, rank, a.batch, a.warmup + a.steps, a.synthetic_mode)
 
     torch.manual_seed(0)
-    tr = NativeTrainer(a.model, a.dtype, a.batch, images, labels, device=dev, lr=a.lr, momentum=a.momentum,
-                       dropout=0.0, init=build_model(a.model), max_indices=idx_all.numel())
+    tr = NativeTrainer(a.model, a.dtype, a.batch, images.to(dev), labels.to(dev), device=dev, lr=a.lr,
+                       momentum=a.momentum, dropout=dropout, init=build_model(a.model), max_indices=idx_all.numel())
     tr.set_buckets(plan_buckets(model_phases(a.model)))
     tr.set_epoch_indices(idx_all)
-    comm, rccl_version, tune = None, None, None
-    if W > 1 or a.comm_world1:
-        if a.comm == "rccl":
-            from pytorch_ddp_mnist_amd.ops.native import load_c
-            C = load_c()
-            comm = ctx.rccl
-            if comm is None:  # --comm-world1: a world-1 RCCL communicator, no rendezvous needed
-                from pytorch_ddp_mnist_amd.utils.logging import native_stdout_to_stderr
-                with native_stdout_to_stderr():  # RCCL's init banner must not reach the JSON stdout
-                    comm = C.RcclComm(bytes(C.RcclComm.make_unique_id()), 0, 1, ctx.local_rank)
-            rccl_version = C.rccl_version()
-            tr.attach_comm(comm, W)
-            tr.broadcast_params(0)
-            if a.plan != "auto":
-                tr.set_plan(a.plan)
+    comm, rccl_version, tune, prof = None, None, None, None
+    external = a.comm in ("torch", "gloo") and W > 1
+    if external:
+        import torch.distributed as dist
+        if a.comm == "gloo":
+            p = tr.params.cpu()
+            dist.broadcast(p, 0)
+            tr.load_flat(p)
         else:
-            import torch.distributed as dist
             dist.broadcast(tr.params, 0)
             tr.load_flat(tr.params.clone())
+        tr.attach_external_allreduce(lambda t: dist.all_reduce(t), W, host=a.comm == "gloo")
+    elif W > 1 or a.comm_world1:
+        if a.comm != "rccl":
+            raise SystemExit("--comm-world1 needs --comm rccl")
+        from pytorch_ddp_mnist_amd.ops.native import load_c
+        C = load_c()
+        comm = ctx.rccl
+        if comm is None:  # --comm-world1: a world-1 RCCL communicator, no rendezvous needed
+            from pytorch_ddp_mnist_amd.utils.logging import native_stdout_to_stderr
+            with native_stdout_to_stderr():  # RCCL's init banner must not reach the JSON stdout
+                comm = C.RcclComm(bytes(C.RcclComm.make_unique_id()), 0, 1, ctx.local_rank)
+        rccl_version = C.rccl_version()
+        tr.attach_comm(comm, W)
+        tr.broadcast_params(0)
+        if pinned is not None:
+            tr.set_plan(pinned)
 
-    use_graph = not a.no_graph and a.comm == "rccl"
+    use_graph = not a.no_graph and not external
     # start-up schedule calibration (multi-GPU plan on the communicator, or the single-GPU
-    # schedule): a few captured-step replays per candidate, state restored, choice in the JSON
-    if use_graph and a.plan == "auto" and (comm is not None or W == 1):
+    # schedule): interleaved captured-step replays per candidate, state restored, choice in the JSON.
+    # With an external data plane the step is not a graph: the local schedules are still timed (rank-max)
+    if a.plan == "auto" and (use_graph or external):
         tune = tr.autotune_plan(reduce_max=ctx.all_reduce_max)
+    if comm is not None and use_graph:
+        prof = tr.comm_profile(reduce_max=ctx.all_reduce_max, tune=tune)
 
     def run(n):
-        if a.comm == "rccl" or W == 1:
-            tr.run_steps(n, use_graph=use_graph)  # k-step graphs (MNIST_AMD_GRAPH_STEPS), then single steps
-            return
-        import torch.distributed as dist
-        for _ in range(n):
-            tr.forward_backward(a.batch)
-            with torch.cuda.stream(tr.stream):
-                dist.all_reduce(tr.grad)
-            tr.optimizer_step(1.0 / W)
+        tr.run_steps(n, use_graph=use_graph)  # k-step graphs (MNIST_AMD_GRAPH_STEPS), then single steps
 
-    if use_graph and (a.comm == "rccl" or W == 1):
+    if use_graph:
         tr.prepare_graphs()   # capture + instantiate the 1-step and k-step graphs before the clock
     tr.reset_metrics()
     run(a.warmup)
-    tr.synchronize()
-    ctx.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    run(a.steps)
-    tr.synchronize()
-    torch.cuda.synchronize(dev)
-    ctx.barrier()
-    t1 = time.perf_counter()
-    elapsed = ctx.all_reduce_max(t1 - t0)
+    elapsed = timed_region(ctx, tr, run, a.steps, lambda: torch.cuda.synchronize(dev))
     train = tr.read_metrics()
     tr.check_comm()
 
@@ -214,8 +256,9 @@ def main(argv=None) -> int:
     if comm is not None:
         colls = " + ".join(f"{c['bytes'] // 1024} KiB" for c in info["collectives"])
         comm_desc = f"native RCCL {rccl_version}, plan={info['plan']}: all-reduce {colls} per step"
-    elif a.comm == "torch" and W > 1:
-        comm_desc = "c10d nccl (RCCL) all_reduce of the whole grad slab"
+    elif external:
+        comm_desc = ("c10d gloo all_reduce of the grad slab via pinned host memory" if a.comm == "gloo"
+                     else "c10d nccl (RCCL) all_reduce of the whole grad slab")
     else:
         comm_desc = "none (single process, no gradient exchange)"
     ms = elapsed / a.steps * 1e3
@@ -232,7 +275,8 @@ def main(argv=None) -> int:
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": a.dtype,
-        "data": "synthetic (MNIST-shaped 28x28 uint8, class-template + noise; random-init weights)",
+        "data": f"synthetic (MNIST-shaped 28x28 uint8, class-template + noise, mode={a.synthetic_mode}; "
+                "random-init weights)",
         "config": {
             "model": "LeNet-5" if a.model == "lenet5" else "MLP-784-128-128-10",
             "global_batch": n_gpus * a.batch,
@@ -241,19 +285,25 @@ def main(argv=None) -> int:
             "image_shape": [1, 28, 28],
             "parallelism": f"dp{n_gpus}",
             "optimizer": f"SGD(lr={a.lr}, momentum={a.momentum})",
+            "dropout": dropout,
             "comm": comm_desc,
             "plan": info,
             "plan_autotune": tune,
             "hipgraph": use_graph,
         },
+        "rccl_world": comm.world if comm is not None else None,
+        "comm_profile": prof,
         "top1": None if top1 is None else round(top1, 4),
         "train_loss_mean": round(train.mean_loss, 4),
     }
-    if a.digest:
-        import hashlib
+    if a.digest or a.dump_params:
         tr.synchronize()
-        print(f"digest rank={rank} {hashlib.sha256(tr.params.cpu().numpy().tobytes()).hexdigest()}",
-              file=sys.stderr, flush=True)
+        p = tr.params.detach().cpu()
+        if a.digest:
+            import hashlib
+            print(f"digest rank={rank} {hashlib.sha256(p.numpy().tobytes()).hexdigest()}", file=sys.stderr, flush=True)
+        if a.dump_params:
+            torch.save(p, f"{a.dump_params}.rank{rank}.pt")
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

@@ -37,6 +37,7 @@ PYBIND11_MODULE(_C, m) {
 
   m.def("model_nparam", [](int model) { return model_nparam(static_cast<ModelKind>(model)); });
   m.def("model_conv_params", [](int model) { return model_conv_params(static_cast<ModelKind>(model)); });
+  m.def("model_phase_split", [](int model) { return model_phase_split(static_cast<ModelKind>(model)); });
   m.def("model_pack_size", [](int model) { return model_pack_size(static_cast<ModelKind>(model)); });
   m.def("conv_bwd_blocks", &lenet_conv_bwd_blocks, py::arg("B"), py::arg("target_blocks") = 0);
   m.def("conv_bwd_max_blocks", &lenet_conv_bwd_max_blocks, py::arg("B"), py::arg("target_blocks") = 0);
@@ -101,6 +102,13 @@ PYBIND11_MODULE(_C, m) {
            [](RcclComm& c, uintptr_t buf, size_t n, uintptr_t s) {
              c.all_reduce_max_f64(reinterpret_cast<double*>(buf), n, reinterpret_cast<hipStream_t>(s));
            })
+      .def("time_all_reduce",
+           [](RcclComm& c, uintptr_t buf, size_t n, int warmup, int iters, uintptr_t s, double timeout) {
+             return c.time_all_reduce(reinterpret_cast<float*>(buf), n, warmup, iters,
+                                      reinterpret_cast<hipStream_t>(s), timeout);
+           },
+           py::arg("buf"), py::arg("count"), py::arg("warmup"), py::arg("iters"), py::arg("stream"),
+           py::arg("timeout") = 600.0, py::call_guard<py::gil_scoped_release>())
       .def("async_error", &RcclComm::async_error)
       .def("wait_stream",
            [](RcclComm& c, uintptr_t s, double timeout) { return c.wait_stream(reinterpret_cast<hipStream_t>(s), timeout); },
@@ -118,6 +126,8 @@ PYBIND11_MODULE(_C, m) {
       .def("set_optimizer", &Trainer::set_optimizer)
       .def("set_dropout", &Trainer::set_dropout)
       .def("set_buckets", &Trainer::set_buckets)
+      .def_property("comm_enabled", &Trainer::comm_enabled, &Trainer::set_comm_enabled)
+      .def_property_readonly("phase_split", &Trainer::phase_split)
       .def("buckets", &Trainer::buckets)
       .def("set_plan", &Trainer::set_plan)
       .def_property_readonly("plan", &Trainer::plan)

@@ -573,8 +573,9 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
     }
   };
   stamp(14);  // metric partials stored (before the barrier)
-  // per-wave arrival at the softmax barrier (profiling stamps, rows 512 + block, one slot per wave)
-  if (hb.stamps && lane == 0 && w < 16 && blockIdx.x < 512) hb.stamps[(512 + blockIdx.x) * 16 + w] = wall_clock64();
+  // per-wave arrival at the softmax barrier (profiling stamps, own row range, one slot per wave)
+  if (hb.stamps && lane == 0 && w < 16 && blockIdx.x < 512)
+    hb.stamps[(STAMP_HEAD_ARRIVE + blockIdx.x) * 16 + w] = wall_clock64();
   __syncthreads();
   stamp(5);
   if constexpr (!TRAIN) {
@@ -726,7 +727,7 @@ __global__ __launch_bounds__(256) void l1_split_kernel(BatchRef br, HeadBuffers 
   const int r0 = blockIdx.x * 16, ng = blockIdx.y, q = blockIdx.z;
   const int lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
   auto stamp = [&](int k) {
-    if (hb.stamps && tid == 0 && lin < 512) hb.stamps[(3584 + lin) * 16 + k] = wall_clock64();
+    if (hb.stamps && tid == 0 && lin < 512) hb.stamps[(STAMP_L1 + lin) * 16 + k] = wall_clock64();
   };
   stamp(0);
   const int c0 = q * QCH, c1 = min(KCH, c0 + QCH);
@@ -838,7 +839,7 @@ struct WgArgs {
   float* slab;
   SgdFuse sgd;          // used when fuse != 0 (then splits == 1)
   int fuse;
-  unsigned long long* stamps;  // optional phase stamps (MNIST_AMD_STAMPS): slots [3072 + block][16]
+  unsigned long long* stamps;  // optional phase stamps (MNIST_AMD_STAMPS): slots [STAMP_WGRAD + block][16]
 };
 
 template <typename T>
@@ -961,7 +962,7 @@ __global__ __launch_bounds__(256) void wgrad_sgd_kernel(WgArgs<T> a) {
   constexpr int KV = M::KV, KC = M::KC, FPS = 8;
   const int lane = threadIdx.x & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
   auto stamp = [&](int k) {
-    if (a.stamps && threadIdx.x == 0 && blockIdx.x < 512) a.stamps[(3072 + blockIdx.x) * 16 + k] = wall_clock64();
+    if (a.stamps && threadIdx.x == 0 && blockIdx.x < 512) a.stamps[(STAMP_WGRAD + blockIdx.x) * 16 + k] = wall_clock64();
   };
   stamp(0);
   const int tile = blockIdx.x;
@@ -1036,11 +1037,13 @@ __global__ __launch_bounds__(256) void wgrad_sgd_kernel(WgArgs<T> a) {
 
 template <typename T, class H, class Model>
 int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab_ld, int xcd_ch, hipStream_t s,
-                 const SgdFuse* fuse) {
+                 const SgdFuse* fuse, int job_mask) {
   WgArgs<T> a{};
   const int BT = fuse ? 32 : 64;  // output tile per block (wgrad_sgd_kernel: 32, wgrad_kernel: 64)
-  auto mk = [&](int i, const void* dy, const void* x, int N, int K, int NP, bool bias, int off, int& blk) {
-    WgJob<T>& J = a.job[i];
+  int nj = 0;
+  auto mk = [&](int layer, const void* dy, const void* x, int N, int K, int NP, bool bias, int off, int& blk) {
+    if (!(job_mask >> layer & 1)) return;
+    WgJob<T>& J = a.job[nj++];
     J.dyT = reinterpret_cast<const T*>(dy);
     J.xT = reinterpret_cast<const T*>(x);
     J.N = N; J.K = K; J.NP = NP; J.bias = bias ? 1 : 0; J.out_off = off;
@@ -1052,7 +1055,8 @@ int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab
   mk(0, hb.dy1T, hb.xT, H::N1, H::K0, H::N1P, true, H::W1, blk);
   mk(1, hb.dy2T, hb.h1T, H::N2, H::N1, H::N2P, true, H::W2, blk);
   mk(2, hb.dy3T, hb.h2T, H::NC, H::N2, H::NCP, H::BIAS3, H::W3, blk);
-  a.njobs = 3;
+  if (nj == 0) throw std::invalid_argument("wgrad: empty job mask");
+  a.njobs = nj;
   a.ldB = hb.ldB;
   constexpr int KC = Mma<T>::KC;
   a.Bp = rup(B, KC);
@@ -1205,14 +1209,14 @@ int launch_head(ModelKind m, DType t, bool train, const BatchRef& br, const Head
 }
 
 int launch_head_wgrad(ModelKind m, DType t, const HeadBuffers& hb, int B, int splits, float* slab,
-                      int slab_ld, hipStream_t s, int head_rows, const SgdFuse* fuse) {
+                      int slab_ld, hipStream_t s, int head_rows, const SgdFuse* fuse, int job_mask) {
   // head_rows: batch rows per head workgroup for this B (0 = unknown: contiguous split mapping)
   if (m == ModelKind::MLP) {
     if (t == DType::F32)
-      return wgrad_launch<float, MlpModel::Head, MlpModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse);
-    return wgrad_launch<bf16, MlpModel::Head, MlpModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse);
+      return wgrad_launch<float, MlpModel::Head, MlpModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse, job_mask);
+    return wgrad_launch<bf16, MlpModel::Head, MlpModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse, job_mask);
   }
   if (t == DType::F32)
-    return wgrad_launch<float, LenetModel::Head, LenetModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse);
-  return wgrad_launch<bf16, LenetModel::Head, LenetModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse);
+    return wgrad_launch<float, LenetModel::Head, LenetModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse, job_mask);
+  return wgrad_launch<bf16, LenetModel::Head, LenetModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse, job_mask);
 }

@@ -65,6 +65,17 @@ struct LenetConvBuffers {
   unsigned long long* stamps = nullptr;  // optional phase timestamps (profiling): fwd [block][16], bwd [block][16]
 };
 
+// MNIST_AMD_STAMPS profiling buffer: [STAMP_ROWS][16] uint64 wall-clock stamps, one row per workgroup,
+// each kernel in its own row range (scripts/stamps.py reads the same layout)
+constexpr int STAMP_HEAD = 0;          // head workgroups            [0, 1024)
+constexpr int STAMP_CONV_BWD = 1024;   // conv_bwd MODE 0/1 blocks   [1024, 1536), MODE 2 blocks [1536, 2048)
+constexpr int STAMP_CONV_FWD = 2048;   // conv_fwd                   [2048, 3072)
+constexpr int STAMP_WGRAD = 3072;      // grouped FC wgrad           [3072, 3584)
+constexpr int STAMP_L1 = 3584;         // layer-1 K-split GEMM       [3584, 4096)
+constexpr int STAMP_HEAD_ARRIVE = 4096;  // head: per-wave softmax-barrier arrival, slot = wave [4096, 4608)
+constexpr int STAMP_BWD_HWLOC = 4608;  // conv_bwd MODE 0: workgroup hardware location, slot 0 [4608, 5120)
+constexpr int STAMP_ROWS = 5120;
+
 int head_rows_per_block(ModelKind m, DType t, int B);
 // Small batches (B <= L1_SPLIT_MAX_B) run layer 1 as a separate many-workgroup GEMM split L1_KSPLIT
 // ways over K (the head kernel alone would put the whole 784-deep GEMM on B/16 CUs).
@@ -89,8 +100,11 @@ struct SgdFuse {
   int32_t* step_ptr;
 };
 
+// job_mask: which layers' weight gradients to compute (bit l = layer l+1; 7 = all three).  A subset
+// writes only those layers' slab columns (the MLP's SPLIT plan sends layers 2+3 while layer 1 computes).
 int launch_head_wgrad(ModelKind m, DType t, const HeadBuffers& hb, int B, int splits, float* slab,
-                       int slab_ld, hipStream_t s, int head_rows = 0, const SgdFuse* fuse = nullptr);
+                       int slab_ld, hipStream_t s, int head_rows = 0, const SgdFuse* fuse = nullptr,
+                       int job_mask = 7);
 
 void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetConvBuffers& cb,
                            hipStream_t s);
@@ -126,4 +140,7 @@ void launch_gather_normalize(DType t, const BatchRef& br, void* out, int ld, hip
 // model geometry queried by the host runtime
 int model_nparam(ModelKind m);
 int model_conv_params(ModelKind m);
+// first parameter of backward phase 0 (the late layers, whose gradients backward produces first):
+// LeNet: conv_params (phase 0 = FC head); MLP: the layer-2 weight (phase 0 = layers 2+3)
+int model_phase_split(ModelKind m);
 int model_pack_size(ModelKind m);

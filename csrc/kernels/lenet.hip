@@ -125,7 +125,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   const float* prm = cb.params;
   // optional wall-clock stamps (profiling): [0] start, [1] setup, 3 per image for images 0..3, [14] loop end
   auto stamp = [&](int k) {
-    if (cb.stamps && tid == 0 && blockIdx.x < 1024) cb.stamps[(1024 + blockIdx.x) * 16 + k] = wall_clock64();
+    if (cb.stamps && tid == 0 && blockIdx.x < 1024) cb.stamps[(STAMP_CONV_FWD - STAMP_CONV_BWD + blockIdx.x) * 16 + k] = wall_clock64();
   };
   stamp(0);
 
@@ -398,7 +398,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
     if (t < 4) stamp(4 + 3 * t);
   }
   stamp(14);
-  if (cb.stamps && tid == 0 && blockIdx.x < 1024) cb.stamps[(1024 + blockIdx.x) * 16 + 15] = hw_location();
+  if (cb.stamps && tid == 0 && blockIdx.x < 1024) cb.stamps[(STAMP_CONV_FWD - STAMP_CONV_BWD + blockIdx.x) * 16 + 15] = hw_location();
   flush_p2(unit * ipb + ipb - 1);
 }
 
@@ -930,8 +930,9 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     }
   }
   stamp(15);
-  // (MODE 0 only: the MODE-2 stamp rows hold this block's hardware location)
-  if (MODE == 0 && cb.stamps && tid == 0 && blockIdx.x < 512) cb.stamps[(512 + blockIdx.x) * 16] = hw_location();
+  // (MODE 0 only: this block's hardware location, in its own row range; cb.stamps starts at STAMP_CONV_BWD)
+  if (MODE == 0 && cb.stamps && tid == 0 && blockIdx.x < 512)
+    cb.stamps[(STAMP_BWD_HWLOC - STAMP_CONV_BWD + blockIdx.x) * 16] = hw_location();
 }
 
 }  // namespace

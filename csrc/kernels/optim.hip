@@ -301,6 +301,7 @@ void launch_gather_normalize(DType t, const BatchRef& br, void* out, int ld, hip
 
 int model_nparam(ModelKind m) { return m == ModelKind::MLP ? MlpModel::NPARAM : LenetModel::NPARAM; }
 int model_conv_params(ModelKind m) { return m == ModelKind::MLP ? 0 : LenetModel::CONV_PARAMS; }
+int model_phase_split(ModelKind m) { return m == ModelKind::MLP ? MlpModel::Head::W2 : LenetModel::CONV_PARAMS; }
 int model_pack_size(ModelKind m) { return m == ModelKind::MLP ? MlpModel::PACK_SIZE : LenetModel::PACK_SIZE; }
 
 void launch_reduce_sgd(ModelKind m, DType t, const float* slab_a, int lda, int na, const float* slab_b, int ldb,

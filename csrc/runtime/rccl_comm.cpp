@@ -54,6 +54,42 @@ void RcclComm::all_reduce_max_f64(double* buf, size_t count, hipStream_t s) {
   NCCL_CHECK(ncclAllReduce(buf, buf, count, ncclFloat64, ncclMax, comm_, s));
 }
 
+std::vector<float> RcclComm::time_all_reduce(float* buf, size_t count, int warmup, int iters, hipStream_t s,
+                                             double timeout_s) {
+  if (count == 0 || iters <= 0) return {};
+  hipGraph_t g = nullptr;
+  hipGraphExec_t ge = nullptr;
+  HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+  ncclResult_t r = ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm_, s);
+  HIP_CHECK(hipStreamEndCapture(s, &g));
+  if (r != ncclSuccess && r != ncclInProgress) {
+    hipGraphDestroy(g);
+    NCCL_CHECK(r);
+  }
+  HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+  std::vector<hipEvent_t> ev(iters + 1);
+  for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+  for (int i = 0; i < warmup; ++i) HIP_CHECK(hipGraphLaunch(ge, s));
+  HIP_CHECK(hipEventRecord(ev[0], s));
+  for (int i = 0; i < iters; ++i) {
+    HIP_CHECK(hipGraphLaunch(ge, s));
+    HIP_CHECK(hipEventRecord(ev[i + 1], s));
+  }
+  const std::string err = wait_stream(s, timeout_s);
+  std::vector<float> out;
+  if (err.empty()) {
+    out.resize(iters);
+    for (int i = 0; i < iters; ++i) HIP_CHECK(hipEventElapsedTime(&out[i], ev[i], ev[i + 1]));
+  }
+  if (err.empty()) {
+    for (auto& e : ev) hipEventDestroy(e);
+    hipGraphExecDestroy(ge);
+    hipGraphDestroy(g);
+  }  // else: the replays may still be in flight -- leak rather than destroy under them; the caller aborts
+  if (!err.empty()) throw std::runtime_error("time_all_reduce: " + err);
+  return out;
+}
+
 std::string RcclComm::async_error() {
   if (!comm_) return "communicator not initialised";
   ncclResult_t e = ncclSuccess;

@@ -11,6 +11,7 @@
 #include <rccl/rccl.h>
 
 #include <string>
+#include <vector>
 
 class RcclComm {
  public:
@@ -23,6 +24,12 @@ class RcclComm {
   void all_reduce_sum_f32(float* buf, size_t count, hipStream_t s);
   void broadcast_f32(float* buf, size_t count, int root, hipStream_t s);
   void all_reduce_max_f64(double* buf, size_t count, hipStream_t s);
+  // Latency of ONE sum all-reduce of `count` floats at `buf`, as the step graph issues it: the call is
+  // captured into its own hipGraph and replayed `warmup` + `iters` times back to back on `s`; returns the
+  // `iters` per-replay times in ms (events between replays).  Collective: every rank must call it with
+  // the same count, in the same order.  Waits through wait_stream (throws on an RCCL error / timeout).
+  std::vector<float> time_all_reduce(float* buf, size_t count, int warmup, int iters, hipStream_t s,
+                                     double timeout_s);
   // Returns "" if healthy, else the error string.  Non-blocking.
   std::string async_error();
   // Wait for `s` with async-error polling: "" once it drains, else the RCCL error or "timeout after …".

@@ -6,8 +6,12 @@
 //   LeNet, comm    : conv_fwd -> head -> { conv_bwd -> reduce(conv)  ||  wgrad(FC) -> reduce(FC) on aux }
 //                    then Plan::JOIN  : ONE all-reduce of the coalesced slab -> sgd_pack
 //                      or Plan::SPLIT : comm stream: AR(FC buckets) as soon as reduce(FC) is done (beside
-//                                       conv_bwd), then AR(conv buckets) after reduce(conv) -> sgd_pack
-//   MLP            : head -> wgrad -> reduce -> [RCCL buckets] -> sgd_pack
+//                                       conv_bwd) -> update(FC range); then AR(conv buckets) after
+//                                       reduce(conv) -> update(conv range) + step bump
+//   MLP, no comm   : head -> wgrad(+SGD epilogue) or wgrad -> reduce_sgd
+//   MLP, comm      : JOIN : head -> wgrad -> reduce -> ONE all-reduce -> sgd_pack
+//                    SPLIT: head -> wgrad(layers 2+3) -> reduce -> [comm: AR -> update(layers 2+3)]
+//                                -> wgrad(layer 1) -> reduce -> [comm: AR -> update(layer 1) + bump]
 // conv_bwd's one-round grid (2 blocks/CU) is LDS-bound and leaves VGPR room on every SIMD, which the
 // FC wgrad (no LDS) fills: running the two concurrently hides most of the wgrad (-6% step time on
 // one MI355X).  MNIST_AMD_CONCURRENT=0 restores the serial single-GPU schedule.  Which multi-GPU plan
@@ -98,13 +102,9 @@ Trainer::Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const
   nparam_ = model_nparam(model_);
   max_conv_slabs_ = model_ == ModelKind::LENET ? lenet_conv_bwd_max_blocks(batch_, 0) : 0;
   concurrent_ = concurrent_mode() != 0;
-  const int cp = model_conv_params(model_);
-  if (cp > 0) {
-    buckets_.push_back({cp, nparam_, 0});
-    buckets_.push_back({0, cp, 1});
-  } else {
-    buckets_.push_back({0, nparam_, 0});
-  }
+  const int ps = model_phase_split(model_);  // default buckets: one per backward phase (see Plan)
+  buckets_.push_back({ps, nparam_, 0});
+  buckets_.push_back({0, ps, 1});
   HIP_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
   HIP_CHECK(hipStreamCreateWithFlags(&aux_stream_, hipStreamNonBlocking));
   events_.resize(6);
@@ -122,14 +122,24 @@ Trainer::~Trainer() {
 }
 
 int Trainer::pack_size() const { return model_pack_size(model_); }
+int Trainer::phase_split() const { return model_phase_split(model_); }
 int Trainer::conv_params() const { return model_conv_params(model_); }
 int Trainer::conv_slabs() const { return model_ == ModelKind::LENET ? lenet_conv_bwd_blocks(batch_, bwd_blocks_) : 0; }
 
+void Trainer::sync_own_streams() {
+  // a replay of a cached graph may still be running on the stream it was launched on and on its forked
+  // aux / comm branches: drain those (not the whole device, which would also wait on other trainers'
+  // and other libraries' work).  After an abort a collective may never complete: nothing is waited for.
+  if (comm_ && comm_->aborted()) return;
+  if (last_stream_) (void)hipStreamSynchronize(last_stream_);
+  (void)hipStreamSynchronize(aux_stream_);
+  (void)hipStreamSynchronize(comm_stream_);
+}
+
 void Trainer::invalidate() {
   if (graphs_.empty()) return;
-  // a replay of one of these graphs may still be running: let it drain before its exec is destroyed
-  // (configuration changes only, never in the step loop)
-  (void)hipDeviceSynchronize();
+  // configuration changes only, never in the step loop
+  sync_own_streams();
   for (auto& kv : graphs_) drop(kv.second);
   graphs_.clear();
 }
@@ -191,8 +201,8 @@ LenetConvBuffers Trainer::conv_buffers() const {
     return e ? std::atoi(e) : 0;
   }();
   cb.ablate = ablate;
-  // stamps layout (16 slots per workgroup): head blocks [0, 1024), conv_bwd [1024, 2048), conv_fwd [2048, 4096)
-  cb.stamps = p_.stamps ? ptr<unsigned long long>(p_.stamps) + 1024 * 16 : nullptr;
+  // stamps layout: launch.h STAMP_* (the conv kernels address their rows relative to STAMP_CONV_BWD)
+  cb.stamps = p_.stamps ? ptr<unsigned long long>(p_.stamps) + STAMP_CONV_BWD * 16 : nullptr;
   return cb;
 }
 
@@ -262,8 +272,8 @@ void Trainer::all_reduce(const std::vector<Bucket>& bs, int phase, hipStream_t s
 
 std::vector<Bucket> Trainer::issued_collectives() const {
   std::vector<Bucket> out;
-  if (!comm_) return out;
-  if (model_ == ModelKind::LENET && plan_ == Plan::SPLIT) {
+  if (!use_comm()) return out;
+  if (plan_ == Plan::SPLIT) {
     for (const Bucket& b : buckets_) if (b.phase == 0) out.push_back(b);
     for (const Bucket& b : buckets_) if (b.phase != 0) out.push_back(b);
     return out;
@@ -277,6 +287,8 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
   const HeadBuffers hb = head_buffers(ptr<float>(p_.metrics));
   const float scale = 1.0f / float(B);
   const int cp = model_conv_params(model_);
+  const bool comm = use_comm();
+  last_stream_ = s;
   if (model_ == ModelKind::LENET) {
     launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(), s);
     post_launch(s);
@@ -291,7 +303,7 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
   const int hrows = launch_head(model_, dtype_, true, br, hb, head_rows_per_block(model_, dtype_, batch_), s);
   post_launch(s);
 
-  if (model_ == ModelKind::LENET && (comm_ || concurrent_)) {
+  if (model_ == ModelKind::LENET && (comm || concurrent_)) {
     // fork: conv_bwd on the main stream (enqueued first, so its one-round grid is dispatched whole:
     // measured wgrad-first 0.1692 ms/step, conv_bwd-first 0.1565, serial 0.1671), the FC wgrad (no LDS,
     // 320 small blocks) on the aux stream beside it
@@ -303,11 +315,14 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     if (split_bwd()) {
       launch_lenet_conv_bwd(dtype_, br, conv_buffers(), nullptr, aux_stream_, 2, bwd_blocks_);
       post_launch(aux_stream_);
+      // the conv update (main) reads the conv2-wgrad columns this half writes, and the next conv_fwd
+      // overwrites the activations it reads: the main stream waits for it before either (events_[3])
+      HIP_CHECK(hipEventRecord(events_[3], aux_stream_));
     }
     const int splits =
         launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, aux_stream_, hrows);
     post_launch(aux_stream_);
-    if (comm_) {
+    if (comm) {
       launch_lenet_comm_tail(B, nslab, splits, s);
       return;
     }
@@ -322,6 +337,7 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     // kernel reads): with defer_join it follows conv_bwd directly, the join moves to the next head
     if (defer_join) aux_pending_ = true;
     else HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));
+    if (defer_join && split_bwd()) HIP_CHECK(hipStreamWaitEvent(s, events_[3], 0));
     launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
                       nparam_, splits, cp, 0, cp, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
                       ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, ptr<int32_t>(p_.step), s);
@@ -329,7 +345,11 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     return;
   }
 
-  if (model_ == ModelKind::MLP && !comm_ && fc_splits_ == 1 && fuse_wgrad_sgd_) {
+  if (model_ == ModelKind::MLP && comm) {
+    launch_mlp_comm_tail(B, s, hb, hrows);
+    return;
+  }
+  if (model_ == ModelKind::MLP && fc_splits_ == 1 && fuse_wgrad_sgd_) {
     // one GPU, one batch split: the SGD update is the wgrad kernel's epilogue (no reduce_sgd kernel)
     const SgdFuse f{scale, lr_, momentum_, ptr<float>(p_.params), ptr<float>(p_.grad),
                     momentum_ != 0.f ? ptr<float>(p_.mom) : nullptr,  // as launch_reduce_sgd
@@ -345,21 +365,60 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s, 0, bwd_blocks_);
     post_launch(s);
   }
-  if (!comm_) {
-    // ONE fused reduce + SGD + pack kernel (2 boundaries fewer than reduce -> sgd)
-    launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
-                      nparam_, splits, cp, 0, nparam_, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
-                      ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, ptr<int32_t>(p_.step), s);
+  // no communicator: ONE fused reduce + SGD + pack kernel (2 boundaries fewer than reduce -> sgd)
+  launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
+                    nparam_, splits, cp, 0, nparam_, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
+                    ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, ptr<int32_t>(p_.step), s);
+  post_launch(s);
+}
+
+// Comm stream: wait for phase `phase`'s reduced gradients, all-reduce its buckets, then update that
+// phase's parameter range (and operand images) with the 1/W average folded in.  Everything stays on the
+// comm stream, so no other stream waits on an event recorded behind a captured RCCL call mid-step.
+void Trainer::comm_phase(int phase, hipEvent_t ready, bool bump) {
+  HIP_CHECK(hipStreamWaitEvent(comm_stream_, ready, 0));
+  all_reduce(buckets_, phase, comm_stream_);
+  const int ps = model_phase_split(model_);
+  const int p0 = phase == 0 ? ps : 0, p1 = phase == 0 ? nparam_ : ps;
+  launch_sgd_pack_range(model_, dtype_, ptr<float>(p_.params), ptr<const float>(p_.grad), ptr<float>(p_.mom),
+                        ptr<void>(p_.pack), p0, p1, lr_, momentum_, 1.0f / float(world_),
+                        bump ? ptr<int32_t>(p_.step) : nullptr, comm_stream_);
+  post_launch(comm_stream_);
+}
+
+// MLP with a communicator (after the head).  JOIN: the whole weight gradient, one all-reduce, one update.
+// SPLIT: layers 2+3 first (their buckets and update go out on the comm stream), then layer 1's 784-deep
+// weight gradient -- the largest GEMM of the step -- runs beside that all-reduce.
+void Trainer::launch_mlp_comm_tail(int B, hipStream_t s, const HeadBuffers& hb, int hrows) {
+  const float scale = 1.0f / float(B);
+  const int ps = model_phase_split(model_);
+  float* g = ptr<float>(p_.grad);
+  float* slab = ptr<float>(p_.slab_fc);
+  if (plan_ == Plan::JOIN) {
+    const int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, slab, nparam_, s, hrows);
+    post_launch(s);
+    launch_reduce(slab, nparam_, splits, 0, nparam_, scale, g, s);
+    post_launch(s);
+    all_reduce(coalesced_buckets(), -1, s);
+    launch_sgd_pack(model_, dtype_, ptr<float>(p_.params), g, ptr<float>(p_.mom), ptr<void>(p_.pack), nparam_, lr_,
+                    momentum_, 1.0f / float(world_), ptr<int32_t>(p_.step), s);
     post_launch(s);
     return;
   }
-  // MLP with a communicator: the whole backward is done here, nothing is left to overlap with
-  launch_reduce(ptr<const float>(p_.slab_fc), nparam_, splits, cp, nparam_, scale, ptr<float>(p_.grad), s);
+  int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, slab, nparam_, s, hrows, nullptr, 6);
   post_launch(s);
-  all_reduce(coalesced_buckets(), -1, s);
-  launch_sgd_pack(model_, dtype_, ptr<float>(p_.params), ptr<const float>(p_.grad), ptr<float>(p_.mom),
-                  ptr<void>(p_.pack), nparam_, lr_, momentum_, 1.0f / float(world_), ptr<int32_t>(p_.step), s);
+  launch_reduce(slab, nparam_, splits, ps, nparam_, scale, g, s);
   post_launch(s);
+  HIP_CHECK(hipEventRecord(events_[1], s));
+  comm_phase(0, events_[1], false);
+  splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, slab, nparam_, s, hrows, nullptr, 1);
+  post_launch(s);
+  launch_reduce(slab, nparam_, splits, 0, ps, scale, g, s);
+  post_launch(s);
+  HIP_CHECK(hipEventRecord(events_[2], s));
+  comm_phase(1, events_[2], true);
+  HIP_CHECK(hipEventRecord(events_[0], comm_stream_));
+  HIP_CHECK(hipStreamWaitEvent(s, events_[0], 0));
 }
 
 // LeNet with a communicator, after the fork (conv_bwd on `s`, FC wgrad on the aux stream).
@@ -372,7 +431,7 @@ void Trainer::launch_lenet_comm_tail(int B, int nslab, int splits, hipStream_t s
   launch_reduce(ptr<const float>(p_.slab_fc), nparam_, splits, cp, nparam_, scale, g, aux_stream_);
   post_launch(aux_stream_);
   HIP_CHECK(hipEventRecord(events_[5], aux_stream_));
-  if (split_bwd()) HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));  // conv2 columns come from the aux half
+  if (split_bwd()) HIP_CHECK(hipStreamWaitEvent(s, events_[3], 0));  // conv2 columns come from the aux half
   if (plan_ == Plan::JOIN) {
     launch_reduce(ptr<const float>(p_.slab_conv), cp, nslab, 0, cp, scale, g, s);
     post_launch(s);
@@ -383,27 +442,21 @@ void Trainer::launch_lenet_comm_tail(int B, int nslab, int splits, hipStream_t s
     post_launch(s);
     return;
   }
-  // SPLIT: the comm stream sends the FC buckets as soon as reduce(FC) is done (beside conv_bwd), then
-  // the conv buckets after reduce(conv); one update after both.  (A graph where another stream waits
-  // on an event recorded behind a captured RCCL call made hipStreamEndCapture segfault on ROCm 7.0's
-  // runtime, so only the main stream consumes the comm stream's completion.)
-  trace("split: comm waits reduce(FC)");
-  HIP_CHECK(hipStreamWaitEvent(comm_stream_, events_[5], 0));
-  trace("split: AR(FC)");
-  all_reduce(buckets_, 0, comm_stream_);
+  // SPLIT: the comm stream sends the FC buckets as soon as reduce(FC) is done (beside conv_bwd) and
+  // updates the FC range right behind them; the conv buckets follow reduce(conv), then the conv update
+  // (+ step bump).  (A graph where another stream waits on an event recorded behind a captured RCCL call
+  // made hipStreamEndCapture segfault on ROCm 7.0's runtime, so only the main stream consumes the comm
+  // stream's completion, once, at the end of the step.)
+  trace("split: comm AR(FC) + update(FC)");
+  comm_phase(0, events_[5], false);
   trace("split: reduce(conv)");
   launch_reduce(ptr<const float>(p_.slab_conv), cp, nslab, 0, cp, scale, g, s);
   post_launch(s);
   HIP_CHECK(hipEventRecord(events_[1], s));
-  HIP_CHECK(hipStreamWaitEvent(comm_stream_, events_[1], 0));
-  trace("split: AR(conv)");
-  all_reduce(buckets_, 1, comm_stream_);
+  trace("split: comm AR(conv) + update(conv)");
+  comm_phase(1, events_[1], true);
   HIP_CHECK(hipEventRecord(events_[0], comm_stream_));
   HIP_CHECK(hipStreamWaitEvent(s, events_[0], 0));
-  trace("split: update");
-  launch_sgd_pack(model_, dtype_, ptr<float>(p_.params), g, ptr<float>(p_.mom), ptr<void>(p_.pack), nparam_, lr_,
-                  momentum_, gs, ptr<int32_t>(p_.step), s);
-  post_launch(s);
   trace("split: done");
 }
 
@@ -480,8 +533,9 @@ void Trainer::drop(GraphSlot& g) {
 // different cached graph instead of re-capturing, so a calibration can interleave the candidates'
 // replays back to back; anything that changes the kernels' arguments clears the cache (invalidate).
 uint64_t Trainer::schedule_key(int nsteps) const {
-  return (static_cast<uint64_t>(nsteps) << 32) | (static_cast<uint64_t>(bwd_blocks_) << 3) |
-         (static_cast<uint64_t>(concurrent_) << 2) | static_cast<uint64_t>(plan_);
+  return (static_cast<uint64_t>(nsteps) << 40) | (static_cast<uint64_t>(bwd_blocks_) << 8) |
+         (static_cast<uint64_t>(comm_enabled_) << 3) | (static_cast<uint64_t>(concurrent_) << 2) |
+         static_cast<uint64_t>(plan_);
 }
 
 const Trainer::GraphSlot* Trainer::find_graph(int nsteps) const {
@@ -515,6 +569,7 @@ bool Trainer::captured() const { return find_graph(1) != nullptr; }
 void Trainer::replay(uintptr_t stream) {
   const GraphSlot* g = find_graph(1);
   if (!g) throw std::runtime_error("replay: no captured graph for the current schedule");
+  last_stream_ = S(stream);
   HIP_CHECK(hipGraphLaunch(g->exec, S(stream)));
   if (sync_debug()) HIP_CHECK(hipStreamSynchronize(S(stream)));
 }
@@ -522,6 +577,7 @@ void Trainer::replay(uintptr_t stream) {
 void Trainer::replay_multi(uintptr_t stream) {
   const GraphSlot* g = multi_k_ > 1 ? find_graph(multi_k_) : nullptr;
   if (!g) throw std::runtime_error("replay_multi: no captured multi-step graph for the current schedule");
+  last_stream_ = S(stream);
   HIP_CHECK(hipGraphLaunch(g->exec, S(stream)));
   if (sync_debug()) HIP_CHECK(hipStreamSynchronize(S(stream)));
 }

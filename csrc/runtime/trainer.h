@@ -31,12 +31,15 @@ struct Bucket {
   int p0, p1, phase;
 };
 
-// Multi-GPU step plans (LeNet; the MLP's backward is one fused head kernel + one wgrad, so it always
-// joins).  Both keep every collective on ONE comm stream, in the same order on every rank.
-//   JOIN  : FC branch and conv_bwd join, then ONE all-reduce of the coalesced slab, then one SGD.
-//   SPLIT : the FC buckets go out on the comm stream as soon as the FC grads are reduced (beside
-//           conv_bwd, which may be given fewer workgroups so whole CUs stay free for RCCL's kernels);
-//           the conv buckets follow reduce(conv) on the same stream, then one update.
+// Multi-GPU step plans.  Both models' backward produces its gradients in two phases: phase 0 = the late
+// layers (LeNet: the FC head [conv_params, n); MLP: layers 2+3 [W2, n)), phase 1 = the early ones (LeNet:
+// conv [0, conv_params); MLP: layer 1 [0, W2)).  Every collective is issued on ONE comm stream, in the
+// same order on every rank.
+//   JOIN  : both phases' gradients are reduced, then ONE all-reduce of the coalesced slab, then one SGD.
+//   SPLIT : phase 0's buckets go out on the comm stream as soon as they are reduced (LeNet: beside conv_bwd,
+//           whose grid can be capped to leave whole CUs free for RCCL's kernels; MLP: beside the layer-1
+//           weight gradient) and phase 0's parameters are updated right after them on the same stream;
+//           phase 1's buckets follow its reduce, then its update (which also bumps the step counters).
 enum class Plan : int { JOIN = 0, SPLIT = 1 };
 
 class Trainer {
@@ -44,7 +47,11 @@ class Trainer {
   Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const TrainerPtrs& p);
   ~Trainer();
 
-  void set_comm(std::shared_ptr<RcclComm> c) { comm_ = std::move(c); invalidate(); }
+  void set_comm(std::shared_ptr<RcclComm> c) { invalidate(); comm_ = std::move(c); }
+  // Timing only (exposed-communication measurement): with a communicator attached, run the local
+  // single-GPU schedule without any collective.  Cached graphs are keyed by it.
+  void set_comm_enabled(bool on) { comm_enabled_ = on; }
+  bool comm_enabled() const { return comm_enabled_; }
   void set_world(int w) { world_ = w; invalidate(); }
   void set_optimizer(float lr, float momentum) { lr_ = lr; momentum_ = momentum; invalidate(); }
   void set_dropout(float p, uint32_t seed) { drop_p_ = p; seed_ = seed; invalidate(); }
@@ -74,6 +81,8 @@ class Trainer {
   std::vector<Bucket> issued_collectives() const;
   bool has_comm() const { return comm_ != nullptr; }
   int world() const { return world_; }
+  // first parameter of backward phase 0 (see Plan): LeNet conv_params, MLP the layer-2 weight offset
+  int phase_split() const;
   // Hold `stream` busy for `seconds` (bounded device spin; watchdog tests).
   void spin(double seconds, uintptr_t stream);
 
@@ -115,6 +124,11 @@ class Trainer {
   // wgrad + FC update) un-joined at the end of the step; the NEXT step's head waits for it instead.
   void launch_step(int B, hipStream_t s, bool defer_join = false);
   void launch_lenet_comm_tail(int B, int nslab, int splits, hipStream_t s);
+  void launch_mlp_comm_tail(int B, hipStream_t s, const HeadBuffers& hb, int hrows);
+  // comm stream: wait for `ready`, all-reduce phase `phase`'s buckets, update its parameter range
+  void comm_phase(int phase, hipEvent_t ready, bool bump);
+  bool use_comm() const { return comm_ && comm_enabled_; }
+  void sync_own_streams();
   struct GraphSlot {
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
@@ -136,6 +150,8 @@ class Trainer {
   Plan plan_ = Plan::JOIN;
   bool concurrent_ = true;
   bool fuse_wgrad_sgd_ = true;
+  bool comm_enabled_ = true;
+  hipStream_t last_stream_ = nullptr;  // stream of the last graph launch / capture (drained by invalidate)
   int bwd_blocks_ = 0;
   int max_conv_slabs_ = 0;  // rows of the conv slab (lenet_conv_bwd_max_blocks(batch) at the default target)
   std::shared_ptr<RcclComm> comm_;

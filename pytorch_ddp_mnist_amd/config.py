@@ -98,7 +98,8 @@ def _add_extra_flags(p: argparse.ArgumentParser, defaults: TrainConfig) -> None:
     add("--data_format", type=str, default=None, choices=["auto", "idx", "netcdf", "synthetic"])
     add("--device", type=str, default=None, choices=["auto", "cpu", "cuda"])
     add("--bucket_cap_kb", type=int, default=None, help="DDP gradient bucket cap (KiB)")
-    add("--comm", type=str, default=None, choices=["rccl", "torch"], help="gradient all-reduce path")
+    add("--comm", type=str, default=None, choices=["rccl", "torch", "gloo"],
+        help="gradient all-reduce path: native RCCL, c10d nccl, or c10d gloo via host memory (ranks may share a GPU)")
     add("--no_graph", action="store_true", help="launch the step eagerly instead of replaying a hipGraph")
     add("--profile", action="store_true", help="emit roctx ranges and per-phase timers")
     add("--no_save", action="store_true", help="do not write model.pt")

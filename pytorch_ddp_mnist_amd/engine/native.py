@@ -31,6 +31,31 @@ from ..models import MODEL_IDS, build_model, flatten_state, unflatten_state
 from ..ops.native import require_gpu
 
 PLANS = {"join": 0, "split": 1}
+STAMP_ROWS = 5120  # csrc/kernels/launch.h
+
+
+def resolve_plan(name: Optional[str]) -> Optional[str]:
+    """CLI ``--plan`` value -> the plan to pin, or None for the start-up calibration.
+
+    ``auto`` (or None) = calibrate; ``fixed`` = no calibration, keep the default ``join`` plan; a plan
+    name pins it.  Anything else is rejected here, before any device work."""
+    if name is None or name == "auto":
+        return None
+    if name == "fixed":
+        return "join"
+    if name not in PLANS:
+        raise ValueError(f"unknown step plan {name!r} (choices: auto, fixed, {', '.join(sorted(PLANS))})")
+    return name
+
+
+def forced_plan() -> Optional[str]:
+    """``MNIST_AMD_MG_SCHED`` pins the multi-GPU plan (validated: a typo must not silently calibrate)."""
+    v = os.environ.get("MNIST_AMD_MG_SCHED")
+    if not v:
+        return None
+    if v not in PLANS:
+        raise ValueError(f"MNIST_AMD_MG_SCHED={v!r}: expected one of {sorted(PLANS)}")
+    return v
 PLAN_NAMES = {v: k for k, v in PLANS.items()}
 
 
@@ -141,9 +166,9 @@ class NativeTrainer:
         P.p1, P.m1, P.p2, P.m2, P.dp2 = ptr(self.p1), ptr(self.m1), ptr(self.p2), ptr(self.m2), ptr(self.dp2)
         P.z1p = ptr(self.z1p)
         P.xnext, P.ynext = ptr(self.xnext), ptr(self.ynext)
-        # MNIST_AMD_STAMPS=1: per-workgroup phase timestamps (wall clock, 100 MHz), 16 slots per workgroup:
-        # head blocks [0, 1024), conv_bwd [1024, 2048), conv_fwd [2048, 3072) (later workgroups skip)
-        self.stamps = z(4096 * 16, dt=torch.int64) if os.environ.get("MNIST_AMD_STAMPS") else None
+        # MNIST_AMD_STAMPS=1: per-workgroup phase timestamps (wall clock, 100 MHz), 16 slots per workgroup,
+        # one row range per kernel (csrc/kernels/launch.h STAMP_*; later workgroups skip)
+        self.stamps = z(STAMP_ROWS * 16, dt=torch.int64) if os.environ.get("MNIST_AMD_STAMPS") else None
         P.stamps = ptr(self.stamps)
         self._ptrs = P
         self.rt = C.Trainer(mid, did, self.batch, self.ld_b, fc_splits, P)
@@ -152,6 +177,7 @@ class NativeTrainer:
         self.stream = torch.cuda.Stream(device=dev)
         self.world = 1
         self.comm = None
+        self.ext_allreduce = None   # external data plane (attach_external_allreduce)
         self.module_template = build_model(model)
         if init is not None:
             self.load_module(init)
@@ -194,6 +220,8 @@ class NativeTrainer:
         self.set_plan(plan, bwd_blocks)
 
     def set_plan(self, plan: str, bwd_blocks: int = 0) -> None:
+        if plan not in PLANS:
+            raise ValueError(f"unknown step plan {plan!r} (choices: {sorted(PLANS)})")
         self.rt.set_plan(PLANS[plan])
         if self.model_name == "lenet5":
             self.rt.set_bwd_blocks(int(bwd_blocks))
@@ -221,6 +249,36 @@ class NativeTrainer:
         self.rt.pack(self.stream.cuda_stream)
         self.synchronize()
 
+    def attach_external_allreduce(self, fn, world: int, host: bool = True) -> None:
+        """Exchange gradients through an EXTERNAL collective instead of the native RCCL communicator:
+        ``fn(t)`` must SUM ``t`` in place across the ranks (c10d gloo / c10d nccl all_reduce).
+
+        Every step then runs the phase API: forward/backward + slab reduce on the device, the gradient
+        slab into ``fn`` (staged through pinned host memory when ``host``, else the device tensor on the
+        trainer stream), then the SGD update with the 1/W average folded in.  No graphs: the collective
+        is a host call.  This is the plumbing / test path -- with a host collective several processes
+        can share ONE GPU (RCCL refuses two ranks on one device), so the whole multi-process chain
+        (launch, rendezvous, broadcast, rank-max calibration, sharded training) runs on a one-GPU box."""
+        self.ext_allreduce = (fn, bool(host))
+        self.world = int(world)
+        self.rt.set_world(self.world)
+        self._host_grad = torch.empty(self.nparam, dtype=torch.float32, pin_memory=True) if host else None
+
+    def _external_step(self, B: int) -> None:
+        fn, host = self.ext_allreduce
+        self.forward_backward(B)
+        if host:
+            with torch.cuda.stream(self.stream):
+                self._host_grad.copy_(self.grad, non_blocking=True)
+            self.stream.synchronize()
+            fn(self._host_grad)
+            with torch.cuda.stream(self.stream):
+                self.grad.copy_(self._host_grad, non_blocking=True)
+        else:
+            with torch.cuda.stream(self.stream):
+                fn(self.grad)
+        self.optimizer_step(1.0 / self.world)
+
     def check_comm(self) -> None:
         """Non-blocking health poll (once per epoch): abort + raise on an asynchronous RCCL error."""
         if self.comm is None:
@@ -230,22 +288,25 @@ class NativeTrainer:
             self.comm.abort()
             raise CollectiveError(f"RCCL communicator error on rank {self.comm.rank}: {err}")
 
+    def current_schedule(self) -> dict:
+        """The installed schedule as an :meth:`apply_plan` candidate."""
+        cfg = {"concurrent": bool(self.rt.concurrent)}
+        if self.comm is not None:
+            cfg.update(plan=self.plan, bwd_blocks=int(self.rt.bwd_blocks))
+        return cfg
+
     def apply_plan(self, cfg: dict) -> None:
-        """Install one candidate of :meth:`autotune_plan` ({plan, bwd_blocks, concurrent})."""
+        """Install one candidate of :meth:`autotune_plan` ({plan, bwd_blocks, concurrent, comm}).
+        ``comm: False`` (timing only) runs the local schedule without collectives."""
+        self.rt.comm_enabled = bool(cfg.get("comm", True))
         if "concurrent" in cfg:
             self.rt.set_concurrent(bool(cfg["concurrent"]))
         if "plan" in cfg or "bwd_blocks" in cfg:
             self.set_plan(cfg.get("plan", self.plan), int(cfg.get("bwd_blocks", 0)))
 
-    def autotune_plan(self, candidates=None, iters: int = 48, warmup: int = 8, reduce_max=None,
-                      margin: float = 0.015, log=None) -> dict:
-        """Time each candidate step schedule and keep the fastest (a start-up calibration, like
-        cudnn.benchmark).
-
-        With a communicator the candidates are the multi-GPU plans (JOIN / SPLIT / SPLIT with a
-        capped conv_bwd grid, :func:`~pytorch_ddp_mnist_amd.parallel.ddp.default_plan_candidates`),
-        timed on the real communicator; without one, the single-GPU LeNet schedules
-        (:func:`~pytorch_ddp_mnist_amd.parallel.ddp.local_plan_candidates`).
+    def time_schedules(self, candidates: Dict[str, dict], iters: int = 48, warmup: int = 8,
+                       reduce_max=None) -> Dict[str, float]:
+        """Median step time (ms) of each candidate schedule, state restored afterwards.
 
         Every candidate's step graph (and its k-step graph) is captured first -- graphs are cached
         per schedule -- and then the candidates' replays are INTERLEAVED round-robin (rotating the
@@ -254,32 +315,12 @@ class NativeTrainer:
         faster clock.  Each replay trains on batch 0 of the loaded epoch order (the device step
         counter is rewound), so all ranks issue the same collectives in the same order; per-replay
         GPU times come from events on the step stream and ``reduce_max`` (e.g. a gloo MAX
-        all-reduce) makes the decision identical on every rank.  Parameters, momentum, counters and
-        metrics are restored afterwards, and the chosen schedule's graphs are left ready to replay.
-        ``MNIST_AMD_MG_SCHED=join|split`` pins the multi-GPU plan.
-
-        48 timed replays per candidate (after 8 untimed rounds): with RCCL in the step the per-replay
-        times jitter with the collective's latency, and the median of 48 separates plans a few percent
-        apart.  At W = 1 this is ~15 ms of GPU work (~25 ms for the three multi-GPU candidates at W = 8);
-        it also brings the GPU from idle to its sustained clock before the caller's warm-up steps
-        (measured: steps 1-20 after a cold start run ~6 % slower than steps 100+, scripts/step_times.py).
-        """
-        from ..parallel.ddp import choose_plan, default_plan_candidates, local_plan_candidates
-        forced = os.environ.get("MNIST_AMD_MG_SCHED")
-        if self.comm is not None and forced:
-            self.set_plan(forced, 0)
-            return {"chosen": forced, "timings_ms": {}, "forced": True}
-        if self.model_name != "lenet5":
-            return {"chosen": "join" if self.comm is not None else "local", "timings_ms": {}}
-        if candidates is None:
-            if self.comm is not None:
-                ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
-                candidates = default_plan_candidates(self.C.conv_bwd_blocks(self.batch), ncu)
-            else:
-                candidates = local_plan_candidates()
-        prefer = "join" if self.comm is not None else "concurrent"
+        all-reduce) makes the result identical on every rank.  Parameters, momentum, gradients,
+        counters and metrics are restored afterwards (the operand images are re-packed); the
+        schedule installed before the call is re-installed."""
         if getattr(self, "n_epoch", 0) < max(2, self.host_step + 1) * self.batch:
-            raise RuntimeError("autotune_plan: the loaded epoch order needs >= 2 full batches beyond the current step")
+            raise RuntimeError("time_schedules: the loaded epoch order needs >= 2 full batches beyond the current step")
+        before = self.current_schedule()
         self.synchronize()
         saved = [t.clone() for t in (self.params, self.mom, self.grad, self.step_ctr, self.metrics)]
         self._sync_in()
@@ -313,13 +354,98 @@ class NativeTrainer:
             for dst, src in zip((self.params, self.mom, self.grad, self.step_ctr, self.metrics), saved):
                 dst.copy_(src)
         self.rt.pack(st.cuda_stream)
-        chosen = choose_plan(timings, prefer=prefer, margin=margin)
+        self.apply_plan(before)
+        return timings
+
+    def autotune_plan(self, candidates=None, iters: int = 48, warmup: int = 8, reduce_max=None,
+                      margin: float = 0.015, log=None) -> dict:
+        """Time each candidate step schedule (:meth:`time_schedules`) and keep the fastest (a start-up
+        calibration, like cudnn.benchmark).
+
+        With a communicator the candidates are the multi-GPU plans -- LeNet: JOIN / SPLIT / SPLIT
+        with a capped conv_bwd grid (:func:`~pytorch_ddp_mnist_amd.parallel.ddp.default_plan_candidates`);
+        MLP: JOIN / SPLIT (:func:`~pytorch_ddp_mnist_amd.parallel.ddp.mlp_plan_candidates`) -- timed on
+        the real communicator, plus the timing-only ``nocomm`` schedule (the local single-GPU step, no
+        collective), so ``exposed_comm_ms`` = chosen plan - nocomm is measured in the same interleaved
+        run.  Without a communicator, the single-GPU LeNet schedules
+        (:func:`~pytorch_ddp_mnist_amd.parallel.ddp.local_plan_candidates`).
+        ``MNIST_AMD_MG_SCHED=join|split`` pins the multi-GPU plan.
+
+        48 timed replays per candidate (after 8 untimed rounds): with RCCL in the step the per-replay
+        times jitter with the collective's latency, and the median of 48 separates plans a few percent
+        apart.  At W = 1 this is ~15 ms of GPU work (~25 ms for the multi-GPU candidates at W = 8);
+        it also brings the GPU from idle to its sustained clock before the caller's warm-up steps
+        (measured: steps 1-20 after a cold start run ~6 % slower than steps 100+, scripts/step_times.py).
+        """
+        from ..parallel.ddp import (choose_plan, default_plan_candidates, local_plan_candidates,
+                                    mlp_plan_candidates)
+        forced = forced_plan()
+        if self.comm is not None and forced:
+            self.set_plan(forced, 0)
+            return {"chosen": forced, "timings_ms": {}, "forced": True}
+        if candidates is None:
+            if self.comm is not None:
+                if self.model_name == "lenet5":
+                    ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+                    candidates = default_plan_candidates(self.C.conv_bwd_blocks(self.batch), ncu)
+                else:
+                    candidates = mlp_plan_candidates()
+            elif self.model_name == "lenet5":
+                candidates = local_plan_candidates()
+            else:
+                return {"chosen": "local", "timings_ms": {}}
+        prefer = "join" if self.comm is not None else "concurrent"
+        extra = {"nocomm": {"comm": False, "concurrent": True}} if self.comm is not None else {}
+        timings = self.time_schedules({**candidates, **extra}, iters=iters, warmup=warmup, reduce_max=reduce_max)
+        chosen = choose_plan({k: timings[k] for k in candidates}, prefer=prefer, margin=margin)
         self.apply_plan(candidates[chosen])
         out = {"chosen": chosen, "timings_ms": {k: round(v, 4) for k, v in timings.items()},
                "candidates": candidates, "replays_per_candidate": iters, "interleaved": True}
+        if extra:
+            out["exposed_comm_ms"] = round(timings[chosen] - timings["nocomm"], 4)
         if log is not None:
             log(out)
         return out
+
+    def comm_profile(self, reduce_max=None, iters: int = 48, warmup: int = 8, tune: Optional[dict] = None) -> dict:
+        """Attributable communication figures of the installed plan (bench JSON ``comm_profile``).
+
+        * ``rccl_world`` -- ranks of the RCCL communicator;
+        * per collective the step issues: its size and the latency of ONE standalone all-reduce of that
+          size, captured in its own graph and replayed back to back (median of ``iters``, rank-max);
+        * ``step_plan_ms`` / ``step_local_ms`` / ``exposed_comm_us`` -- the captured step with the plan's
+          collectives vs the local single-GPU schedule without any, interleaved replays (taken from
+          ``tune`` when the calibration already timed both).
+        Collective: every rank calls it at the same point."""
+        if self.comm is None:
+            return {"rccl_world": None}
+        colls = []
+        for c in self.plan_info()["collectives"]:
+            a, b = c["params"]
+            buf = torch.zeros(b - a, dtype=torch.float32, device=self.device)
+            self._sync_in()
+            try:
+                ts = self.comm.time_all_reduce(buf.data_ptr(), b - a, warmup, iters, self.stream.cuda_stream,
+                                               comm_timeout())
+            except RuntimeError as e:
+                self.comm.abort()
+                raise CollectiveError(f"rank {self.comm.rank}: {e} (communicator aborted)") from e
+            ts = sorted(ts)
+            med = ts[len(ts) // 2]
+            med = reduce_max(med) if reduce_max is not None else med
+            colls.append({"params": [a, b], "bytes": 4 * (b - a), "allreduce_us": round(med * 1000.0, 2)})
+        tm = (tune or {}).get("timings_ms", {})
+        chosen = (tune or {}).get("chosen")
+        if chosen in tm and "nocomm" in tm:
+            plan_ms, local_ms = tm[chosen], tm["nocomm"]
+        else:
+            cur = self.current_schedule()
+            t = self.time_schedules({"plan": cur, "nocomm": {"comm": False, "concurrent": True}}, iters=iters,
+                                    warmup=warmup, reduce_max=reduce_max)
+            plan_ms, local_ms = t["plan"], t["nocomm"]
+        return {"rccl_world": int(self.comm.world), "collectives": colls,
+                "step_plan_ms": round(plan_ms, 4), "step_local_ms": round(local_ms, 4),
+                "exposed_comm_us": round((plan_ms - local_ms) * 1000.0, 2)}
 
     # ------------------------------------------------------------------ training
     def set_epoch_indices(self, indices: torch.Tensor) -> None:
@@ -360,6 +486,9 @@ class NativeTrainer:
 
     def step(self, B: Optional[int] = None, use_graph: bool = True) -> None:
         B = self.batch if B is None else B
+        if self.ext_allreduce is not None:
+            self._external_step(B)   # counts the step itself (optimizer_step)
+            return
         self._check_rows(B)
         self.host_step += 1
         if use_graph and B == self.batch:
@@ -386,7 +515,7 @@ class NativeTrainer:
         (``MNIST_AMD_GRAPH_STEPS``, default 8; the graph launch gap is paid once per k steps), the
         remainder single-step graphs.  Same kernels, same order, same results as ``n`` x :meth:`step`."""
         k = self.graph_steps() if k is None else int(k)
-        if not use_graph or k <= 1:
+        if not use_graph or k <= 1 or self.ext_allreduce is not None:
             for _ in range(n):
                 self.step(self.batch, use_graph)
             return

@@ -35,7 +35,7 @@ class NativeEngine:
 
     def __init__(self, cfg: TrainConfig, ctx: DistContext, xtr, ytr, xte, yte, init: torch.nn.Module):
         from ..data.device_loader import upload_arrays
-        from .native import NativeTrainer
+        from .native import NativeTrainer, resolve_plan
         dev = ctx.device
 
         def on_device(x, y):  # numpy arrays are staged (pinned -> async copy); device tensors used as is
@@ -56,12 +56,19 @@ class NativeEngine:
             self.tr.attach_comm(ctx.rccl, ctx.world)
             self.tr.broadcast_params(0)
         elif self.torch_comm:
+            # c10d data plane: the all-reduce is enqueued behind the backward on the trainer stream and the
+            # SGD kernel that follows on the same stream waits for it (c10d makes the current stream wait);
+            # a gloo-only group stages the slab through pinned host memory
             import torch.distributed as dist
-            dist.broadcast(self.tr.params, 0)
-            self.tr.load_flat(self.tr.params.clone())
+            host = dist.get_backend() == "gloo"
+            p = self.tr.params.cpu() if host else self.tr.params
+            dist.broadcast(p, 0)
+            self.tr.load_flat(p.clone())
+            self.tr.attach_external_allreduce(lambda t: dist.all_reduce(t), ctx.world, host=host)
         self.use_graph = cfg.graph and not self.torch_comm
         self.fault = FaultInjector(ctx.rank)
-        self.plan_forced = None if cfg.plan == "auto" else cfg.plan
+        self.plan_pinned = cfg.plan != "auto"
+        self.plan_forced = resolve_plan(cfg.plan)  # 'fixed' = no calibration, default join plan
         self.tuned = not self.use_graph  # the calibration times captured steps
         self.tune = None
 
@@ -97,16 +104,7 @@ class NativeEngine:
 
     def _step(self, b: int) -> None:
         self.fault.tick()
-        if self.torch_comm:
-            import torch.distributed as dist
-            self.tr.forward_backward(b)
-            # the collective is enqueued behind the backward on the trainer stream, and the SGD kernel
-            # that follows on the same stream waits for it (c10d makes the current stream wait)
-            with torch.cuda.stream(self.tr.stream):
-                dist.all_reduce(self.tr.grad)
-            self.tr.optimizer_step(1.0 / self.ctx.world)
-        else:
-            self.tr.step(b, use_graph=self.use_graph)
+        self.tr.step(b, use_graph=self.use_graph)
 
     def _maybe_tune(self, nfull: int) -> None:
         """First epoch: pick the step schedule by timing the candidates (multi-GPU plans on the
@@ -114,7 +112,7 @@ class NativeEngine:
         if self.tuned or nfull < 2:
             return
         self.tuned = True
-        if self.plan_forced:
+        if self.plan_pinned:
             if self.tr.comm is not None:
                 self.tr.set_plan(self.plan_forced)
             return
@@ -241,7 +239,8 @@ def run(cfg: TrainConfig, entry: str = "ddp_tutorial_cpu", show_banner: bool = F
         # The method only decides how rank/world/master are derived from the launcher env; the
         # backend follows the device: no GPU -> gloo (the reference forces "gloo" here, which
         # also drops the SLURM/PMI variables: mnist_cpu_mp.py:247-249 -- we keep them).
-        ctx = init_distributed(method, parallel=parallel, device=cfg.device, comm=cfg.comm)
+        ctx = init_distributed(method, parallel=parallel, device=cfg.device, comm=cfg.comm,
+                               share_device=cfg.comm == "gloo")
     fmt = _data_format(cfg, entry)
     root = cfg.data_path if cfg.data_path else ("." if fmt == "netcdf" else "./mnist_data")
     if cfg.io_mode == "per_sample" and fmt != "netcdf":

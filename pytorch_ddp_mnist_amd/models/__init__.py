@@ -21,6 +21,9 @@ MODEL_IDS = {"mlp": 0, "lenet5": 1}
 FACTORIES = {"mlp": create_model, "lenet5": create_lenet5}
 NPARAM = {"mlp": 118272, "lenet5": 61706}
 CONV_PARAMS = {"mlp": 0, "lenet5": 2572}
+# first parameter of backward phase 0 = the late layers, whose gradients backward produces first
+# (LeNet: the FC head after the convs; MLP: layers 3.* and 5.* after 0.*) -- csrc model_phase_split
+PHASE_SPLIT = {"mlp": 100480, "lenet5": 2572}
 
 
 def build_model(name: str) -> nn.Module:
@@ -59,4 +62,5 @@ def flatten_grads(module: nn.Module) -> torch.Tensor:
 
 
 __all__ = ["create_model", "create_lenet5", "build_model", "param_layout", "flatten_state",
-           "unflatten_state", "flatten_grads", "MODEL_IDS", "NPARAM", "CONV_PARAMS"]
+           "unflatten_state", "flatten_grads", "MODEL_IDS", "NPARAM", "CONV_PARAMS",
+           "PHASE_SPLIT"]

@@ -81,12 +81,17 @@ def _want_gpu(device: str) -> bool:
 
 
 def init_distributed(method: Optional[str] = None, parallel: bool = True, device: str = "auto",
-                     comm: str = "rccl", timeout_s: float = 600.0) -> DistContext:
+                     comm: str = "rccl", timeout_s: float = 600.0, share_device: bool = False) -> DistContext:
     """Bring up rank/world/device and the communicators.
 
     ``method=None`` uses plain ``env://`` variables (torchrun / torch.distributed.launch); a
     reference wire-up name derives them from the scheduler environment first.
+    ``comm``: ``rccl`` (gloo control plane + native RCCL data plane), ``torch`` (c10d nccl data
+    plane) or ``gloo`` (everything over gloo).  ``share_device`` (only with ``comm="gloo"``) maps local
+    rank r to GPU r % device_count, so several ranks can share one GPU (RCCL refuses that).
     """
+    if share_device and comm != "gloo":
+        raise ValueError("share_device needs comm='gloo' (RCCL refuses two ranks on one device)")
     use_gpu = _want_gpu(device)
     if not parallel:
         lr = int(os.environ.get("LOCAL_RANK", 0)) if use_gpu else 0
@@ -100,8 +105,13 @@ def init_distributed(method: Optional[str] = None, parallel: bool = True, device
     else:
         w = W.resolve("gloo", os.environ)
         w.export(os.environ)
-    local_rank = W.pick_local_rank(w, torch.cuda.device_count() if use_gpu else 1)
-    dev = torch.device("cuda", local_rank) if use_gpu else torch.device("cpu")
+    ndev = torch.cuda.device_count() if use_gpu else 1
+    local_rank = W.pick_local_rank(w, ndev)
+    if use_gpu and local_rank >= ndev:
+        if not share_device:
+            raise RuntimeError(f"local rank {local_rank} but only {ndev} GPU(s) visible (one rank per GPU; "
+                               f"--comm gloo lets ranks share a GPU)")
+    dev = torch.device("cuda", local_rank % ndev) if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(dev)
     backend = "cpu:gloo,cuda:nccl" if (use_gpu and comm == "torch") else "gloo"

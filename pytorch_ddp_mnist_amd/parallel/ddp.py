@@ -9,16 +9,18 @@ first bucket, so the reference does ONE 473,088-byte (MLP) all-reduce per step w
 
 MI355X design (GPU path, csrc/runtime/trainer.cpp): gradients are written by the kernels into
 ONE flat fp32 slab; a bucket is a contiguous range of it.  :func:`plan_buckets` decides the ranges
-(one per backward phase by default: LeNet-5 FC head 236.5 KB | conv 10 KB, the MLP one 473 KB;
-``bucket_cap_kb`` forces further splits).  For messages this small the all-reduce is latency-bound
+(one per backward phase by default: LeNet-5 FC head 236.5 KB | conv 10 KB, MLP layers 2+3 71 KB |
+layer 1 402 KB; ``bucket_cap_kb`` forces further splits).  For messages this small the all-reduce is latency-bound
 on xGMI (7 point-to-point links, ~153 GB/s each: a 247 KB ring step is ~2 us of wire time), so
 WHEN the buckets go out matters more than how many there are.  Two step plans exist (trainer.h):
 
   * ``join``  -- the FC and conv backward branches join, then ONE all-reduce of the coalesced
     slab (one ring latency per step, fully exposed);
-  * ``split`` -- the FC buckets go out on the comm stream as soon as the FC grads are reduced,
-    beside conv_bwd (whose grid can be capped to leave whole CUs free for RCCL's kernels), and the
-    FC update runs on the aux stream; only the 10 KB conv bucket is exposed.
+  * ``split`` -- phase 0's buckets go out on the comm stream as soon as its grads are reduced
+    (LeNet: the FC buckets beside conv_bwd, whose grid can be capped to leave whole CUs free for
+    RCCL's kernels; MLP: layers 2+3 beside the layer-1 weight gradient) and phase 0's parameters are
+    updated right behind them on the same stream; phase 1's buckets and update follow its reduce
+    (LeNet: only the 10 KB conv bucket and its 2,572-parameter update are exposed).
 
 Which one is faster depends on the xGMI latency at the actual world size and on whether RCCL's
 kernels find CU room beside conv_bwd, so it is not hard-coded: at start-up every candidate of
@@ -73,6 +75,12 @@ def default_plan_candidates(default_grid: int, n_cu: int, reserve_cus=(16,)) -> 
     return out
 
 
+def mlp_plan_candidates() -> Dict[str, dict]:
+    """MLP multi-GPU candidates: one coalesced all-reduce after the whole weight gradient, or layers 2+3
+    sent beside the layer-1 weight gradient."""
+    return {"join": dict(plan="join"), "split": dict(plan="split")}
+
+
 def local_plan_candidates() -> Dict[str, dict]:
     """Single-GPU LeNet schedules: the FC weight gradient + FC update on an aux stream beside
     conv_bwd (``concurrent``, the default) or after it (``serial``)."""
@@ -91,9 +99,12 @@ def choose_plan(timings_ms: Dict[str, float], prefer: str = "join", margin: floa
 
 
 def model_phases(model: str) -> List[Tuple[int, int]]:
-    from ..models import CONV_PARAMS, NPARAM
-    n, c = NPARAM[model], CONV_PARAMS[model]
-    return [(c, n), (0, c)] if c else [(0, n)]
+    """The two backward phases of a model, in the order backward produces them: phase 0 = the late
+    layers (LeNet-5 FC head ``7.*,9.*,11.*``; MLP ``3.*,5.*``), phase 1 = the early ones (LeNet-5 convs;
+    MLP ``0.*``).  Reference gradient-ready order: survey §2.7."""
+    from ..models import NPARAM, PHASE_SPLIT
+    n, c = NPARAM[model], PHASE_SPLIT[model]
+    return [(c, n), (0, c)]
 
 
 class GlooReducer:

@@ -7,8 +7,10 @@ SPLIT multi-GPU plans, with the default or a capped conv_bwd grid.  ``w2`` varia
 1/W arithmetic of a 2-rank job on one GPU (world set to 2 on a world-1 communicator, so every
 rank's "all-reduced" gradient is its own): they must equal a local run at half the learning rate
 (x0.5 is exact in binary floating point).
-Usage: python scripts/sched_equiv.py VARIANT [VARIANT ...]
-  VARIANT = local | local_halflr | {join,split}[_b<blocks>][_w2]
+``_k<k>`` variants run the steps as ONE k-step graph (run_steps), whose steps may leave the aux
+branch join to the next step's head; they must equal the same number of single-step graphs.
+Usage: python scripts/sched_equiv.py [--model mlp|lenet5] VARIANT [VARIANT ...]
+  VARIANT = {local,local_halflr,join,split}[_b<blocks>][_w2][_k<k>]
 """
 import argparse
 import hashlib
@@ -29,27 +31,32 @@ ap = argparse.ArgumentParser()
 ap.add_argument("variants", nargs="+")
 ap.add_argument("--batch", type=int, default=512)
 ap.add_argument("--steps", type=int, default=4)
+ap.add_argument("--model", default="lenet5", choices=["lenet5", "mlp"])
 a = ap.parse_args()
 x, y = make_split(4096, seed=7)
 C = load_c()
 order = torch.randperm(4096, generator=torch.Generator().manual_seed(1)).to(torch.int32)
 
 for v in a.variants:
-    lr = 0.025 if v == "local_halflr" else 0.05
-    torch.manual_seed(0)
-    tr = NativeTrainer("lenet5", "bf16", a.batch, torch.from_numpy(x.reshape(-1, 784)), torch.from_numpy(y),
-                       lr=lr, momentum=0.9, dropout=0.0, init=build_model("lenet5"))
-    m = re.fullmatch(r"(join|split)(?:_b(\d+))?(_w2)?", v)
-    if m:
-        tr.attach_comm(C.RcclComm(C.RcclComm.make_unique_id(), 0, 1, 0), 2 if m.group(3) else 1,
-                       plan=m.group(1), bwd_blocks=int(m.group(2) or 0))
-        tr.broadcast_params(0)
-    elif v.startswith("local_b"):
-        tr.rt.set_bwd_blocks(int(v[7:]))
-    elif v not in ("local", "local_halflr"):
+    m = re.fullmatch(r"(local_halflr|local|join|split)(?:_b(\d+))?(_w2)?(?:_k(\d+))?", v)
+    if not m:
         raise SystemExit(f"unknown variant {v}")
+    kind, blocks, w2, k = m.group(1), int(m.group(2) or 0), bool(m.group(3)), int(m.group(4) or 0)
+    lr = 0.025 if kind == "local_halflr" else 0.05
+    torch.manual_seed(0)
+    tr = NativeTrainer(a.model, "bf16", a.batch, torch.from_numpy(x.reshape(-1, 784)), torch.from_numpy(y),
+                       lr=lr, momentum=0.9, dropout=0.0, init=build_model(a.model))
+    if kind in ("join", "split"):
+        tr.attach_comm(C.RcclComm(C.RcclComm.make_unique_id(), 0, 1, 0), 2 if w2 else 1, plan=kind,
+                       bwd_blocks=blocks)
+        tr.broadcast_params(0)
+    elif blocks:
+        tr.rt.set_bwd_blocks(blocks)
     tr.set_epoch_indices(order)
-    for _ in range(a.steps):
-        tr.step(a.batch, use_graph=True)
+    if k:
+        tr.run_steps(a.steps, use_graph=True, k=k)
+    else:
+        for _ in range(a.steps):
+            tr.step(a.batch, use_graph=True)
     tr.synchronize()
     print("digest", v, hashlib.sha256(tr.params.cpu().numpy().tobytes()).hexdigest(), flush=True)

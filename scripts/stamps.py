@@ -58,7 +58,7 @@ if model == "lenet5":
     ss = allst[:nblk][:, [4, 12, 13, 14, 5]]
     if (ss[:, 1:4] > 0).all():
         report("head softmax", ss, ["dX prefetch", "softmax rows", "metric sums", "barrier"], 4)
-        pw = allst[512:512 + nblk, :16]
+        pw = allst[4096:4096 + nblk, :16]  # STAMP_HEAD_ARRIVE
         if (pw > 0).all():
             rel = (pw - allst[:nblk, 4][:, None]) * 10 / 1000.0
             print("  per-wave arrival at the softmax barrier (us after phase start): " +
@@ -105,7 +105,7 @@ if model == "lenet5":
           f"head last end -> conv_bwd first start {(bw[:, 0].min() - hd[:, 8].max()) * 10 / 1000:.2f} us; "
           f"conv_fwd first start -> conv_bwd last end {(bw[:, 15].max() - fw[:, 0].min()) * 10 / 1000:.2f} us")
     per_cu("conv_fwd", allst[2048:2048 + min(nf, 1024)], allst[2048:2048 + min(nf, 1024), 15], 14)
-    per_cu("conv_bwd", allst[1024:1024 + nb], allst[1536:1536 + nb, 0], 15)
+    per_cu("conv_bwd", allst[1024:1024 + nb], allst[4608:4608 + nb, 0], 15)  # hw location: STAMP_BWD_HWLOC
     per_cu("head", allst[:nblk], allst[:nblk, 15], 8)
 
 if model == "mlp":

@@ -20,7 +20,7 @@ def _port():
 
 
 def test_bucket_plans():
-    assert plan_buckets(model_phases("mlp")) == [(0, 118272, 0)]
+    assert plan_buckets(model_phases("mlp")) == [(100480, 118272, 0), (0, 100480, 1)]
     assert plan_buckets(model_phases("lenet5")) == [(2572, 61706, 0), (0, 2572, 1)]
     b = plan_buckets(model_phases("lenet5"), cap_bytes=64 * 1024)
     assert b[0] == (61706 - 16384, 61706, 0)  # backward produces the last layers first

@@ -3,10 +3,12 @@
 The FC weight gradient runs on an aux stream beside conv_bwd (default) or after it
 (MNIST_AMD_CONCURRENT=0); conv_bwd can run as two concurrent halves (MNIST_AMD_SPLIT_BWD=1); with a
 communicator the gradient exchange follows the JOIN plan (one coalesced all-reduce after the backward
-join) or the SPLIT plan (FC buckets on the comm stream beside conv_bwd, per-range updates).  All of
-them reduce in the same fixed order, so the trained parameters must be bitwise identical; a capped
-conv_bwd grid changes the summation order, so capped variants are compared among themselves.  The
-``_w2`` variants check the 1/W averaging of both plans against a local run at half the learning rate.
+join) or the SPLIT plan (phase-0 buckets + their update on the comm stream beside the rest of the
+backward, then phase 1's).  All of them reduce in the same fixed order, so the trained parameters must
+be bitwise identical; a capped conv_bwd grid changes the summation order, so capped variants are
+compared among themselves.  The ``_w2`` variants check the 1/W averaging of both plans against a local
+run at half the learning rate; ``_k4`` variants run the steps as one 4-step graph (deferred aux join).
+The MLP has the same plans (layers 2+3 sent beside the layer-1 weight gradient).
 """
 import os
 import re
@@ -19,9 +21,10 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _digests(env_extra, variants):
+def _digests(env_extra, variants, model="lenet5"):
     env = dict(os.environ, PYTHONPATH=ROOT, **env_extra)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "sched_equiv.py")] + variants, env=env,
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "sched_equiv.py"), "--model", model] + variants,
+                       env=env,
                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:]
     return dict(re.findall(r"digest (\S+) (\w+)", r.stdout))
@@ -31,11 +34,20 @@ def _digests(env_extra, variants):
 def test_schedules_bitwise_equal(native):
     serial = _digests({"MNIST_AMD_CONCURRENT": "0"}, ["local", "local_halflr"])
     d = _digests({"MNIST_AMD_CONCURRENT": "1"},
-                 ["local", "join", "split", "join_w2", "split_w2", "local_b480", "join_b480", "split_b480"])
-    halves = _digests({"MNIST_AMD_CONCURRENT": "1", "MNIST_AMD_SPLIT_BWD": "1"}, ["local", "split"])
+                 ["local", "join", "split", "join_w2", "split_w2", "local_b480", "join_b480", "split_b480",
+                  "local_k4", "join_k4", "split_k4"])
+    halves = _digests({"MNIST_AMD_CONCURRENT": "1", "MNIST_AMD_SPLIT_BWD": "1"}, ["local", "split", "local_k4"])
     ref = serial["local"]
-    for k in ("local", "join", "split"):
+    for k in ("local", "join", "split", "local_k4", "join_k4", "split_k4"):
         assert d[k] == ref, k
-    assert halves["local"] == ref and halves["split"] == ref
+    assert halves["local"] == ref and halves["split"] == ref and halves["local_k4"] == ref
     assert d["join_w2"] == serial["local_halflr"] and d["split_w2"] == serial["local_halflr"]
     assert d["join_b480"] == d["local_b480"] and d["split_b480"] == d["local_b480"]
+
+
+@pytest.mark.timeout(300)
+def test_mlp_schedules_bitwise_equal(native):
+    d = _digests({}, ["local", "local_halflr", "join", "split", "join_w2", "split_w2", "split_k4"], model="mlp")
+    for k in ("join", "split", "split_k4"):
+        assert d[k] == d["local"], k
+    assert d["join_w2"] == d["local_halflr"] and d["split_w2"] == d["local_halflr"]
