@@ -289,20 +289,18 @@ class NativeTrainer:
             raise CollectiveError(f"RCCL communicator error on rank {self.comm.rank}: {err}")
 
     def current_schedule(self) -> dict:
-        """The installed schedule as an :meth:`apply_plan` candidate."""
-        cfg = {"concurrent": bool(self.rt.concurrent)}
-        if self.comm is not None:
-            cfg.update(plan=self.plan, bwd_blocks=int(self.rt.bwd_blocks))
-        return cfg
+        """The installed schedule as a complete :meth:`apply_plan` candidate."""
+        return {"plan": self.plan, "bwd_blocks": int(self.rt.bwd_blocks) if self.model_name == "lenet5" else 0,
+                "concurrent": bool(self.rt.concurrent)}
 
     def apply_plan(self, cfg: dict) -> None:
-        """Install one candidate of :meth:`autotune_plan` ({plan, bwd_blocks, concurrent, comm}).
-        ``comm: False`` (timing only) runs the local schedule without collectives."""
+        """Install one candidate of :meth:`autotune_plan` ({plan, bwd_blocks, concurrent, comm}).  Keys a
+        candidate leaves out take their defaults (join, default conv_bwd grid, concurrent, comm on), so
+        a candidate names ONE cached graph whatever was installed before it.  ``comm: False`` (timing
+        only) runs the local schedule without collectives."""
         self.rt.comm_enabled = bool(cfg.get("comm", True))
-        if "concurrent" in cfg:
-            self.rt.set_concurrent(bool(cfg["concurrent"]))
-        if "plan" in cfg or "bwd_blocks" in cfg:
-            self.set_plan(cfg.get("plan", self.plan), int(cfg.get("bwd_blocks", 0)))
+        self.rt.set_concurrent(bool(cfg.get("concurrent", True)))
+        self.set_plan(cfg.get("plan", "join"), int(cfg.get("bwd_blocks", 0)))
 
     def time_schedules(self, candidates: Dict[str, dict], iters: int = 48, warmup: int = 8,
                        reduce_max=None) -> Dict[str, float]:
