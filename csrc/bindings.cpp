@@ -42,6 +42,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_bwd_blocks", &lenet_conv_bwd_blocks, py::arg("B"), py::arg("target_blocks") = 0);
   m.def("conv_bwd_max_blocks", &lenet_conv_bwd_max_blocks, py::arg("B"), py::arg("target_blocks") = 0);
   m.attr("L1_KSPLIT") = L1_KSPLIT;
+  m.def("metric_rows", [](int B) { return metric_rows(B); });
   m.attr("L1_SPLIT_MAX_B") = L1_SPLIT_MAX_B;
   m.def("device_count", [] {
     int n = 0;

@@ -176,15 +176,24 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
     }
   }
 
-  // ---- L1 operands of this wave's first n-tile: issued first, in flight during the staging
+  // ---- L1 operands of this wave's first n-tile: issued first, in flight during the staging.
+  //      KS1: with at least two waves per layer-1 n-tile, the 784/400-deep K is split in two halves
+  //      (wave w: n-tile w % NT1, half w / NT1); the second half's accumulators are added through LDS.
+  //      Halves each wave's chain of B-fragment fetches (the MLP's 25-chunk layer 1 ran on 8 of the 16
+  //      waves, 10.4 us of a 23 us head).
   constexpr int NT1 = H::N1P / 16, KCH1 = H::K0P / KC;
-  constexpr bool PF1 = !PRE && KCH1 <= 16;  // <= 64 VGPRs of prefetched fragments (LeNet bf16: 13 chunks)
-  Frag b1pre[PF1 ? KCH1 : 1];
+  constexpr bool KS1 = !PRE && NWV >= 2 * NT1 && NT1 * MT * 64 * 16 <= R * S::PX * (int)sizeof(T);
+  constexpr int KH1 = KS1 ? (KCH1 + 1) / 2 : KCH1;  // chunks of the first half (per-wave chunk count bound)
+  constexpr bool PF1 = !PRE && KH1 <= 16;  // <= 64 VGPRs of prefetched fragments
+  const int l1_nt = KS1 ? w % NT1 : w, l1_half = KS1 ? w / NT1 : 0;
+  const int l1_k0 = l1_half * KH1, l1_k1 = KS1 ? (l1_half ? KCH1 : KH1) : KCH1;
+  const bool l1_live = KS1 ? w < 2 * NT1 : w < NT1;
+  Frag b1pre[PF1 ? KH1 : 1];
   if constexpr (PF1) {
-    if (w < NT1) {
-      const T* bp = pack + H::F1 + (w * 16 + row) * H::K0P + grp * KV;
+    if (l1_live) {
+      const T* bp = pack + H::F1 + (l1_nt * 16 + row) * H::K0P + grp * KV;
 #pragma unroll
-      for (int kc = 0; kc < KCH1; ++kc) b1pre[kc] = M::load(bp + kc * KC);
+      for (int kc = 0; kc < KH1; ++kc) b1pre[kc] = M::load(bp + min(l1_k0 + kc, KCH1 - 1) * KC);
     }
   }
 
@@ -290,28 +299,69 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   // (PRE: layer 1 already ran in l1_split_kernel, which also wrote xT; X itself is not needed)
   if constexpr (PRE) {
   } else if constexpr (H::GATHER) {
-    constexpr int CH = H::K0P / 8;
+    // one work item = one 16-pixel chunk of 4 consecutive rows: four 16-byte image loads (all items'
+    // loads issued before any conversion), 16-byte LDS stores, and 4-row-wide xT stores (one per pixel)
+    static_assert(H::K0 % 16 == 0 && H::K0P % 16 == 0 && R % 4 == 0, "gather chunking");
+    constexpr int GC = H::K0P / 16, NGI = (R / 4) * GC, ITG = (NGI + NTH - 1) / NTH;
     T* xT = reinterpret_cast<T*>(hb.xT);
-    for (int e = tid; e < R * CH; e += NTH) {
-      const int r = e % R, k = (e / R) * 8;
-      const int s = sIdx[r];
-      float v[8];
-      if (s >= 0 && k < H::K0) {
-        const uint2 u = *reinterpret_cast<const uint2*>(br.images + (size_t)s * 784 + k);
+    u32x4 px[ITG][4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          v[j] = mnist_norm((u.x >> (8 * j)) & 255u);
-          v[j + 4] = mnist_norm((u.y >> (8 * j)) & 255u);
+    for (int i = 0; i < ITG; ++i) {
+      const int e = min(tid + i * NTH, NGI - 1), r = (e % (R / 4)) * 4, c = e / (R / 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {  // branch-free: padding chunks / rows past the batch read row 0, zeroed at use
+        const int sidx = sIdx[r + q];
+        px[i][q] = *reinterpret_cast<const u32x4*>(br.images + (size_t)max(sidx, 0) * 784 + min(c, H::K0 / 16 - 1) * 16);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < ITG; ++i) {
+      const int e = tid + i * NTH, r = (e % (R / 4)) * 4, c = e / (R / 4);
+      if (e >= NGI) break;
+      if constexpr (sizeof(T) == 2) {
+        // each row's 16 pixels -> 16 bf16 packed in 8 registers (two 16-byte LDS stores); the xT store of
+        // pixel j takes halfword j of the four rows (as the pool2-row path below)
+        u32x4 pk[4][2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const bool live = sIdx[r + q] >= 0 && c < H::K0 / 16;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            bf16x8 f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              f[j] = (bf16)(live ? mnist_norm((px[i][q][2 * h + (j >> 2)] >> (8 * (j & 3))) & 255u) : 0.f);
+            pk[q][h] = __builtin_bit_cast(u32x4, f);
+            *reinterpret_cast<u32x4*>(sX + (r + q) * S::PX + c * 16 + h * 8) = pk[q][h];
+          }
+        }
+        if constexpr (TRAIN) {
+#pragma unroll
+          for (int j = 0; j < 16; ++j) {
+            const int h = j >> 3, wd = (j & 7) >> 1, sh = 16 * (j & 1);
+            const uint32_t lo = ((pk[0][h][wd] >> sh) & 0xFFFFu) | (((pk[1][h][wd] >> sh) & 0xFFFFu) << 16);
+            const uint32_t hi = ((pk[2][h][wd] >> sh) & 0xFFFFu) | (((pk[3][h][wd] >> sh) & 0xFFFFu) << 16);
+            *reinterpret_cast<u32x2*>(xT + (size_t)(c * 16 + j) * ldB + r0 + r) = u32x2{lo, hi};
+          }
         }
       } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[j] = 0.f;
-      }
+        for (int j0 = 0; j0 < 16; j0 += 4) {  // fp32: 4 pixels at a time (one 16-byte LDS store per row)
+          float v[4][4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sX[r * S::PX + k + j] = to_t<T>(v[j]);
-      if constexpr (TRAIN) {
+          for (int q = 0; q < 4; ++q) {
+            const bool live = sIdx[r + q] >= 0 && c < H::K0 / 16;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) xT[(size_t)(k + j) * ldB + r0 + r] = to_t<T>(v[j]);
+            for (int j = 0; j < 4; ++j)
+              v[q][j] = live ? mnist_norm((px[i][q][(j0 + j) >> 2] >> (8 * ((j0 + j) & 3))) & 255u) : 0.f;
+            *reinterpret_cast<f32x4*>(sX + (r + q) * S::PX + c * 16 + j0) = f32x4{v[q][0], v[q][1], v[q][2], v[q][3]};
+          }
+          if constexpr (TRAIN) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              store_col4<T>(xT + (size_t)(c * 16 + j0 + j) * ldB + r0 + r, v[0][j], v[1][j], v[2][j], v[3][j]);
+          }
+        }
       }
     }
   } else {
@@ -400,19 +450,39 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   } else {
     T* h1T = reinterpret_cast<T*>(hb.h1T);
     const T* ap = sX + row * S::PX + grp * KV;
+    constexpr int NJ1 = KS1 ? 1 : (NT1 + NWV - 1) / NWV;
 #pragma unroll
-    for (int j = 0; j < (NT1 + NWV - 1) / NWV; ++j) {
-      const int nt = w + j * NWV;
-      if (nt >= NT1) break;
+    for (int j = 0; j < NJ1; ++j) {
+      const int nt = KS1 ? l1_nt : w + j * NWV;
+      const bool live = KS1 ? l1_live : nt < NT1;
+      if (!KS1 && !live) break;
       f32x4 acc[MT];
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = zero4();
-      const T* bp = pack + H::F1 + (nt * 16 + row) * H::K0P + grp * KV;
+      if (live) {
+        const T* bp = pack + H::F1 + (nt * 16 + row) * H::K0P + grp * KV;
 #pragma unroll
-      for (int kc = 0; kc < KCH1; ++kc) {
-        const Frag b = (PF1 && j == 0) ? b1pre[PF1 ? kc : 0] : M::load(bp + kc * KC);
+        for (int kk = 0; kk < KH1; ++kk) {
+          const int kc = l1_k0 + kk;
+          if (kc >= l1_k1) break;  // wave-uniform (second half of an odd chunk count)
+          const Frag b = (PF1 && j == 0) ? b1pre[PF1 ? kk : 0] : M::load(bp + kc * KC);
 #pragma unroll
-        for (int m = 0; m < MT; ++m) M::mma(acc[m], M::load(ap + m * 16 * S::PX + kc * KC), b);
+          for (int m = 0; m < MT; ++m) M::mma(acc[m], M::load(ap + m * 16 * S::PX + kc * KC), b);
+        }
+      }
+      if constexpr (KS1) {
+        // second-half waves hand their partial sums to the first-half wave of the same n-tile through the
+        // X region (every wave has finished reading X at the first barrier; every wave passes both)
+        f32x4* red = reinterpret_cast<f32x4*>(smem + S::OFF_X);
+        __syncthreads();
+        if (live && l1_half == 1) {
+#pragma unroll
+          for (int m = 0; m < MT; ++m) red[(nt * MT + m) * 64 + lane] = acc[m];
+        }
+        __syncthreads();
+        if (!live || l1_half == 1) continue;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[m] += red[(nt * MT + m) * 64 + lane];
       }
       const int n = nt * 16 + row;
       const float bias = sB1[n];
@@ -558,7 +628,10 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       sPart[w * 4 + 2] = cnt;
     }
   }
-  // tile totals -> hb.metrics at the very end (contended float atomics kept off the phases)
+  // tile totals -> this workgroup's own row of hb.metrics ([grid][4], summed on the host when read):
+  // a plain read-modify-write, no atomics.  (Three float atomics per workgroup on the same three words
+  // were serialised at the memory side behind the kernel's last stores and held the kernel's end --
+  // and the next kernel's start -- back by several us; a fixed row per workgroup is also deterministic.)
   auto flush_metrics = [&] {
     if (tid == 0) {
       float a = 0.f, b = 0.f, c = 0.f;
@@ -567,9 +640,9 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
         b += sPart[i * 4 + 1];
         c += sPart[i * 4 + 2];
       }
-      atomicAdd(hb.metrics + 0, a);
-      atomicAdd(hb.metrics + 1, b);
-      atomicAdd(hb.metrics + 2, c);
+      float* m = hb.metrics + (size_t)blockIdx.x * 4;
+      const f32x4 old = *reinterpret_cast<const f32x4*>(m);
+      *reinterpret_cast<f32x4*>(m) = f32x4{old[0] + a, old[1] + b, old[2] + c, 0.f};
     }
   };
   stamp(14);  // metric partials stored (before the barrier)
@@ -842,12 +915,14 @@ struct WgArgs {
   unsigned long long* stamps;  // optional phase stamps (MNIST_AMD_STAMPS): slots [STAMP_WGRAD + block][16]
 };
 
-template <typename T>
+template <typename T, int WD>
 __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
   using M = Mma<T>;
   using Frag = typename M::Frag;
   constexpr int KV = M::KV, KC = M::KC;
   const int lane = threadIdx.x & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
+  const int lin = blockIdx.y * gridDim.x + blockIdx.x;  // profiling stamps: [0] start, [1] end
+  if (a.stamps && threadIdx.x == 0 && lin < 512) a.stamps[(STAMP_WGRAD + lin) * 16] = wall_clock64();
   int tile, split, nsteps, x = 0, m0 = 0, spc = 1, rs = 0;
   if (a.xcd_ch == 0) {
     tile = blockIdx.x;
@@ -900,28 +975,35 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
   const int sel0 = kk0 < J.K ? 0 : (kk0 == J.K && J.bias ? 1 : 2);
   const int sel1 = kk1 < J.K ? 0 : (kk1 == J.K && J.bias ? 1 : 2);
 
-  // software pipeline: the next K-chunk's four fragments are in flight while this one computes
-  Frag na0, na1, nb0, nb1;
-  auto fetch = [&](int rc) {
-    na0 = M::load(ap0 + rc);
-    na1 = nv1 ? M::load(ap1 + rc) : zf;
-    nb0 = M::load(bp0 + rc);
-    nb1 = M::load(bp1 + rc);
+  // software pipeline: a ring of WD K-steps' fragments (four per step) is in flight while the oldest one
+  // computes (one step of look-ahead left every wave waiting a full L2 round trip per 32-row step)
+  Frag ra0[WD], ra1[WD], rb0[WD], rb1[WD];
+  auto fetch = [&](int d, int rc) {
+    ra0[d] = M::load(ap0 + rc);
+    ra1[d] = nv1 ? M::load(ap1 + rc) : zf;
+    rb0[d] = M::load(bp0 + rc);
+    rb1[d] = M::load(bp1 + rc);
   };
-  int rc = nsteps > 0 ? step_row(0) : a.Bp;
-  if (rc < a.Bp) fetch(rc);
-  for (int st = 0; st < nsteps; ++st) {
-    if (rc >= a.Bp) break;  // rows past the (padded) batch: nothing left in this sequence
-    const Frag a0 = na0, a1 = na1;
-    const Frag b0 = sel0 == 0 ? nb0 : (sel0 == 1 ? ones : zf);
-    const Frag b1 = sel1 == 0 ? nb1 : (sel1 == 1 ? ones : zf);
-    const int rn = st + 1 < nsteps ? step_row(st + 1) : a.Bp;
-    if (rn < a.Bp) fetch(rn);
-    M::mma(acc[0][0], a0, b0);
-    M::mma(acc[0][1], a0, b1);
-    M::mma(acc[1][0], a1, b0);
-    M::mma(acc[1][1], a1, b1);
-    rc = rn;
+#pragma unroll
+  for (int d = 0; d < WD; ++d) {
+    const int rc = d < nsteps ? step_row(d) : a.Bp;
+    if (rc < a.Bp) fetch(d, rc);
+  }
+  for (int st0 = 0; st0 < nsteps; st0 += WD) {
+#pragma unroll
+    for (int d = 0; d < WD; ++d) {
+      const int st = st0 + d;
+      if (st >= nsteps || step_row(st) >= a.Bp) break;  // rows past the (padded) batch: nothing left
+      const Frag a0 = ra0[d], a1 = ra1[d];
+      const Frag b0 = sel0 == 0 ? rb0[d] : (sel0 == 1 ? ones : zf);
+      const Frag b1 = sel1 == 0 ? rb1[d] : (sel1 == 1 ? ones : zf);
+      const int rn = st + WD < nsteps ? step_row(st + WD) : a.Bp;
+      if (rn < a.Bp) fetch(d, rn);
+      M::mma(acc[0][0], a0, b0);
+      M::mma(acc[0][1], a0, b1);
+      M::mma(acc[1][0], a1, b0);
+      M::mma(acc[1][1], a1, b1);
+    }
   }
 
   float* out = a.slab + (size_t)split * a.slab_ld + J.out_off;
@@ -946,6 +1028,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         if (qi[mi][ni][i] >= 0) out[qi[mi][ni][i]] = acc[mi][ni][i];
+  if (a.stamps && threadIdx.x == 0 && lin < 512) a.stamps[(STAMP_WGRAD + lin) * 16 + 1] = wall_clock64();
 }
 
 // Weight-gradient GEMM + SGD update for one GPU and ONE batch split (small batches): every output
@@ -1035,6 +1118,15 @@ __global__ __launch_bounds__(256) void wgrad_sgd_kernel(WgArgs<T> a) {
   stamp(2);
 }
 
+// K-steps of fragments in flight per wave in wgrad_kernel (MNIST_AMD_WGRAD_DEPTH=2: one step of look-ahead)
+inline int wgrad_depth() {
+  static const int d = [] {
+    const char* e = std::getenv("MNIST_AMD_WGRAD_DEPTH");
+    return e ? std::atoi(e) : 4;
+  }();
+  return d;
+}
+
 template <typename T, class H, class Model>
 int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab_ld, int xcd_ch, hipStream_t s,
                  const SgdFuse* fuse, int job_mask) {
@@ -1080,11 +1172,13 @@ int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab
     a.sx = splits / 8;
     const int head_grid = (rup(B, 32) + xcd_ch - 1) / xcd_ch;  // head_launch_mtw's grid
     a.contig = hb.xcd && head_grid % 8 == 0 && a.nch == head_grid;
-    hipLaunchKernelGGL(wgrad_kernel<T>, dim3(blk * splits), dim3(256), 0, s, a);
+    if (wgrad_depth() == 2) hipLaunchKernelGGL((wgrad_kernel<T, 2>), dim3(blk * splits), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_kernel<T, 4>), dim3(blk * splits), dim3(256), 0, s, a);
   } else if (a.fuse) {
     hipLaunchKernelGGL((wgrad_sgd_kernel<T, Model>), dim3(blk), dim3(256), 0, s, a);
   } else {
-    hipLaunchKernelGGL(wgrad_kernel<T>, dim3(blk, splits), dim3(256), 0, s, a);
+    if (wgrad_depth() == 2) hipLaunchKernelGGL((wgrad_kernel<T, 2>), dim3(blk, splits), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_kernel<T, 4>), dim3(blk, splits), dim3(256), 0, s, a);
   }
   return splits;
 }

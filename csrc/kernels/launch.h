@@ -43,7 +43,7 @@ struct HeadBuffers {
   void* dy2T;            // [N2P][ldB]
   void* dy3T;            // [16][ldB]
   void* dx;              // LeNet: dp2 [B][K0P]
-  float* metrics;        // [loss_sum, correct, count]
+  float* metrics;        // [head grid][4]: per-workgroup [loss_sum, correct, count, 0] (metric_rows(batch) rows)
   float* z1p;            // [L1_KSPLIT][N1P][ldB] fp32 layer-1 partial sums (small-batch split path) or null
   unsigned long long* stamps;  // optional phase timestamps [block][16] (MNIST_AMD_STAMPS profiling) or null
   int32_t ldB;
@@ -77,6 +77,8 @@ constexpr int STAMP_BWD_HWLOC = 4608;  // conv_bwd MODE 0: workgroup hardware lo
 constexpr int STAMP_ROWS = 5120;
 
 int head_rows_per_block(ModelKind m, DType t, int B);
+// rows of a metrics buffer: one per head workgroup of any batch <= B (16-row tiles at the smallest)
+constexpr int metric_rows(int B) { return (B + 31) / 32 * 2; }
 // Small batches (B <= L1_SPLIT_MAX_B) run layer 1 as a separate many-workgroup GEMM split L1_KSPLIT
 // ways over K (the head kernel alone would put the whole 784-deep GEMM on B/16 CUs).
 constexpr int L1_KSPLIT = 4;

@@ -319,19 +319,31 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
       // overwrites the activations it reads: the main stream waits for it before either (events_[3])
       HIP_CHECK(hipEventRecord(events_[3], aux_stream_));
     }
-    const int splits =
-        launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, aux_stream_, hrows);
-    post_launch(aux_stream_);
     if (comm) {
+      const int splits =
+          launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, aux_stream_, hrows);
+      post_launch(aux_stream_);
       launch_lenet_comm_tail(B, nslab, splits, s);
       return;
     }
     // single GPU: the FC update follows the FC wgrad on the aux stream (it touches only FC parameters
-    // and FC operand images); the conv update + step bump follows the join
-    launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
-                      nparam_, splits, cp, cp, nparam_, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
-                      ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, nullptr, aux_stream_);
-    post_launch(aux_stream_);
+    // and FC operand images); the conv update + step bump follows the join.  With ONE batch split the
+    // update is the wgrad kernel's epilogue (small batches: one kernel and one boundary less on the aux
+    // branch; bitwise equal to wgrad -> reduce_sgd)
+    int splits = 1;
+    if (fc_splits_ == 1 && fuse_wgrad_sgd_) {
+      const SgdFuse f{scale, lr_, momentum_, ptr<float>(p_.params), ptr<float>(p_.grad),
+                      momentum_ != 0.f ? ptr<float>(p_.mom) : nullptr, ptr<void>(p_.pack), nullptr};
+      launch_head_wgrad(model_, dtype_, hb, B, 1, ptr<float>(p_.slab_fc), nparam_, aux_stream_, hrows, &f);
+      post_launch(aux_stream_);
+    } else {
+      splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, aux_stream_, hrows);
+      post_launch(aux_stream_);
+      launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
+                        nparam_, splits, cp, cp, nparam_, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
+                        ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, nullptr, aux_stream_);
+      post_launch(aux_stream_);
+    }
     HIP_CHECK(hipEventRecord(events_[5], aux_stream_));
     // the conv update touches only conv parameters / operand images and the step counters (which no aux
     // kernel reads): with defer_join it follows conv_bwd directly, the join moves to the next head

@@ -59,7 +59,8 @@ class TrainConfig:
     shard_eval: bool = False
     progress_every: int = 0     # --tqdm update period in batches (0 = ~20 updates per epoch)
     plan: str = "auto"          # multi-GPU step plan: "auto" (timed at start-up) | "join" | "split"
-    io_mode: str = "bulk"       # netCDF: "bulk" (one pread per variable) | "per_sample" (reference __getitem__ reads)
+    io_mode: str = "bulk"       # netCDF: "bulk" (one pread per variable) | "per_sample" (reference __getitem__
+                                # reads, whole epoch first) | "interleaved" (each batch read before its step)
     resume: Optional[str] = None  # params + momentum + epoch file: loaded if present, rewritten each epoch
 
     def to_nested(self) -> dict:
@@ -110,8 +111,9 @@ def _add_extra_flags(p: argparse.ArgumentParser, defaults: TrainConfig) -> None:
     add("--shard_eval", action="store_true", help="shard the test set across ranks (reference: every rank evaluates all)")
     add("--plan", type=str, default=None, choices=["auto", "join", "split", "fixed"],
         help="step plan (auto: time the candidate schedules at start-up; join/split: multi-GPU plan; fixed: defaults)")
-    add("--io_mode", type=str, default=None, choices=["bulk", "per_sample"],
-        help="netCDF input: bulk pread (default) or the reference's per-sample __getitem__ reads, timed (MB/s)")
+    add("--io_mode", type=str, default=None, choices=["bulk", "per_sample", "interleaved"],
+        help="netCDF input: bulk pread (default), or the reference's per-sample __getitem__ reads, timed (MB/s): "
+             "per_sample reads the epoch first, interleaved reads each batch beside the training steps")
     add("--resume", type=str, default=None,
         help="resume file (params + momentum + epoch): loaded when it exists, rewritten after every epoch")
 

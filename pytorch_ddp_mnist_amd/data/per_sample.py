@@ -7,9 +7,14 @@ files" (``mnist_cpu_mp.py:210``) measures.  ``--io_mode per_sample`` reproduces 
 pattern (same ``Dataset`` class, same per-sample calls, sampler order, every epoch) and times it,
 instead of the default bulk ``pread`` of the whole variable.
 
-The samples of an epoch are gathered on the host in sampler order and then handed to the engine
-as that epoch's resident data, so the measured read cost is isolated from the training step (the
-reference's ``num_workers=0`` MP configuration also serialises reading and compute).
+Two schedules:
+  * ``per_sample`` -- the samples of an epoch are gathered on the host in sampler order and then handed
+    to the engine as that epoch's resident data, so the measured read cost is isolated from the step;
+  * ``interleaved`` -- :class:`InterleavedLoader` reads each batch right before the step that consumes
+    it, as the reference's DataLoader with ``num_workers=0`` does (mnist_pnetcdf_cpu_mp.py:39-49 called
+    from the loader of :370-409, inside the training loop).  On the GPU the batch's host read overlaps
+    the previous (asynchronous) step; its rows go through a pinned two-slot ring into the resident
+    buffer.  Same batches, same order: the training is bitwise that of ``per_sample``.
 """
 from __future__ import annotations
 
@@ -40,6 +45,24 @@ class ReadStats:
     def line(self, what: str) -> str:
         return (f"{what}: {self.samples} samples, {self.bytes / 1e6:.2f} MB in {self.seconds:.3f} s "
                 f"= {self.mb_per_s:.2f} MB/s ({self.samples_per_s:,.0f} samples/s, 2 reads per sample)")
+
+
+class InterleavedLoader:
+    """``loader(s, b)``: read the samples at positions [s, s+b) of this epoch's sampler order through
+    ``reader`` (one ``__getitem__`` each) and hand them to ``write_rows(x, y, s)`` -- called by the
+    engine right before the step that trains on rows [s, s+b).  ``stats`` sums the read time."""
+
+    def __init__(self, reader: "PerSampleReader", order, write_rows):
+        self.reader, self.write_rows = reader, write_rows
+        self.order = order.tolist() if isinstance(order, torch.Tensor) else list(order)
+        self.stats = ReadStats()
+
+    def __call__(self, s: int, b: int) -> None:
+        x, y, st = self.reader.read(self.order[s:s + b])
+        self.stats.samples += st.samples
+        self.stats.bytes += st.bytes
+        self.stats.seconds += st.seconds
+        self.write_rows(x, y, s)
 
 
 class PerSampleReader:

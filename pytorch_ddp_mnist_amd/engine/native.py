@@ -131,8 +131,9 @@ class NativeTrainer:
         # device counters: [0] step within the epoch (batch addressing), [1] global step (dropout stream),
         # [2] loaded indices of the epoch (look-ahead gather bound)
         self.step_ctr = torch.zeros(4, dtype=torch.int32, device=dev)
-        self.metrics = z(3, dt=torch.float32)
-        self.eval_metrics = z(3, dt=torch.float32)
+        # per-head-workgroup metric rows [loss_sum, correct, count, 0], summed when read (no atomics)
+        self.metrics = z(C.metric_rows(self.batch), 4, dt=torch.float32)
+        self.eval_metrics = z(C.metric_rows(self.batch), 4, dt=torch.float32)
         self.xT, self.h1T, self.h2T = z(K0P, self.ld_b), z(N1P, self.ld_b), z(N2P, self.ld_b)
         self.dy1T, self.dy2T, self.dy3T = z(N1P, self.ld_b), z(N2P, self.ld_b), z(16, self.ld_b)
         self.slab_fc = z(fc_splits, self.nparam, dt=torch.float32)
@@ -476,8 +477,8 @@ class NativeTrainer:
 
     def read_metrics(self, which: str = "train") -> EpochStats:
         self.synchronize()
-        m = (self.metrics if which == "train" else self.eval_metrics).tolist()
-        return EpochStats(*m)
+        m = (self.metrics if which == "train" else self.eval_metrics).double().sum(0).tolist()
+        return EpochStats(*m[:3])
 
     def capture(self) -> None:
         self.rt.capture(self.stream.cuda_stream)

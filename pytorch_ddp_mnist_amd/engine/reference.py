@@ -75,16 +75,24 @@ class TorchCPUEngine:
         self.x = normalize_batch(torch.from_numpy(np.ascontiguousarray(x))).reshape(self.shape)
         self.y = torch.from_numpy(y.astype(np.int64))
 
+    def write_train_rows(self, x: np.ndarray, y: np.ndarray, row0: int) -> None:
+        """Interleaved I/O: one batch's rows become resident rows [row0, row0+b)."""
+        b = len(y)
+        self.x[row0:row0 + b] = normalize_batch(torch.from_numpy(np.ascontiguousarray(x))).reshape(self.shape)
+        self.y[row0:row0 + b] = torch.from_numpy(y.astype(np.int64))
+
     def load_test_arrays(self, x: np.ndarray, y: np.ndarray) -> None:
         self.xt = normalize_batch(torch.from_numpy(np.ascontiguousarray(x))).reshape(self.shape)
         self.yt = torch.from_numpy(y.astype(np.int64))
 
-    def train_epoch(self, indices: torch.Tensor, progress=None, prefetch=None) -> EpochResult:
+    def train_epoch(self, indices: torch.Tensor, progress=None, prefetch=None, batch_loader=None) -> EpochResult:
         r = EpochResult()
         self.module.train()
         t0 = time.perf_counter()
         slices = batch_slices(indices.numel(), self.batch)
         for s, b in slices:
+            if batch_loader is not None:  # interleaved I/O: this batch's rows are read now
+                batch_loader(s, b)
             idx = indices[s:s + b]
             x, y = self.x[idx], self.y[idx]
             self.fault.tick()  # before the step, as NativeEngine._step: FAIL_AT_STEP=k -> k completed steps

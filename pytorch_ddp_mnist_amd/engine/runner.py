@@ -17,7 +17,7 @@ import torch
 from ..config import TrainConfig
 from ..data.datasets import find_netcdf, load_arrays, synthesize_netcdf
 from ..data.device_loader import upload_netcdf
-from ..data.per_sample import PerSampleReader
+from ..data.per_sample import InterleavedLoader, PerSampleReader
 from ..data.sampler import epoch_indices
 from ..models import build_model
 from ..parallel.comm import DistContext, init_distributed
@@ -86,6 +86,25 @@ class NativeEngine:
     def load_train_arrays(self, x: np.ndarray, y: np.ndarray) -> None:
         self._load_rows(self.tr.images, self.tr.labels, x, y)
 
+    def write_train_rows(self, x: np.ndarray, y: np.ndarray, row0: int) -> None:
+        """Interleaved I/O: one batch's rows -> resident rows [row0, row0+b), through a two-slot pinned ring
+        (a slot is refilled only after its previous copy ran: the host read of batch j+1 overlaps step j)."""
+        b = len(y)
+        if not hasattr(self, "_ring"):
+            self._ring = [(torch.empty(self.batch, 784, dtype=torch.uint8, pin_memory=True),
+                           torch.empty(self.batch, dtype=torch.uint8, pin_memory=True), torch.cuda.Event())
+                          for _ in range(2)]
+            self._slot = 0
+        hx, hy, ev = self._ring[self._slot]
+        self._slot ^= 1
+        ev.synchronize()
+        hx[:b].copy_(torch.from_numpy(np.ascontiguousarray(x).reshape(b, 784)))
+        hy[:b].copy_(torch.from_numpy(np.ascontiguousarray(y).reshape(b)))
+        with torch.cuda.stream(self.tr.stream):
+            self.tr.images[row0:row0 + b].copy_(hx[:b], non_blocking=True)
+            self.tr.labels[row0:row0 + b].copy_(hy[:b], non_blocking=True)
+            ev.record(self.tr.stream)
+
     def load_test_arrays(self, x: np.ndarray, y: np.ndarray) -> None:
         self._load_rows(self.test_images, self.test_labels, x, y)
 
@@ -124,23 +143,33 @@ class NativeEngine:
         cur = self.tr.read_metrics().loss_sum
         return cur, (cur - prev) / max(1, steps * B)
 
-    def train_epoch(self, indices: torch.Tensor, progress=None, prefetch=None) -> EpochResult:
+    def train_epoch(self, indices: torch.Tensor, progress=None, prefetch=None, batch_loader=None) -> EpochResult:
         """``prefetch`` (optional) runs on the host while the epoch's steps execute on the GPU: the
         next epoch's sampler order is ready when this one ends (no host gap between epochs).
         ``progress`` (optional, --tqdm) gets the mean batch loss of the last ``progress.every``
-        batches; reading it is a device sync, so it happens only every ``every`` steps."""
+        batches; reading it is a device sync, so it happens only every ``every`` steps.
+        ``batch_loader(s, b)`` (optional, interleaved I/O) is called before the step on rows [s, s+b)."""
         tr, B = self.tr, self.batch
         r = EpochResult()
         t0 = time.perf_counter()
         tr.set_epoch_indices(indices)
         n = indices.numel()
         nfull, last = divmod(n, B)
+        nsteps = nfull + (1 if last else 0)
+
+        def load(j):  # interleaved I/O, one batch AHEAD of the step that trains on it: the small-batch MLP
+            if batch_loader is not None and j < nsteps:  # head gathers the next step's rows during this one
+                batch_loader(j * B, min(B, n - j * B))
+        if batch_loader is not None:
+            load(0)
+            load(1)
+            tr.rt.prime_next(tr.stream.cuda_stream)  # look-ahead rows of step 0, now that they are resident
         self._maybe_tune(nfull)
         tr.reset_metrics()
         every = getattr(progress, "every", 0) if progress is not None else 0
         prev = 0.0
         with range_("train_full_batches"):
-            if not every and not self.torch_comm and not self.fault.active:
+            if not every and not self.torch_comm and not self.fault.active and batch_loader is None:
                 if self.use_graph:
                     tr.prepare_graphs()
                 tr.run_steps(nfull, use_graph=self.use_graph)   # k-step graph launches
@@ -150,6 +179,7 @@ class NativeEngine:
                 nfull_loop = nfull
             for i in range(nfull_loop):
                 self._step(B)
+                load(i + 2)
                 if every and ((i + 1) % every == 0 or i + 1 == nfull):
                     k = (i % every) + 1
                     prev, bl = self._window_loss(prev, k, B)
@@ -243,18 +273,19 @@ def run(cfg: TrainConfig, entry: str = "ddp_tutorial_cpu", show_banner: bool = F
                                share_device=cfg.comm == "gloo")
     fmt = _data_format(cfg, entry)
     root = cfg.data_path if cfg.data_path else ("." if fmt == "netcdf" else "./mnist_data")
-    if cfg.io_mode == "per_sample" and fmt != "netcdf":
-        raise ValueError("--io_mode per_sample is the netCDF read-cost experiment: use it with the netCDF format")
+    per_sample = cfg.io_mode in ("per_sample", "interleaved")
+    if per_sample and fmt != "netcdf":
+        raise ValueError(f"--io_mode {cfg.io_mode} is the netCDF read-cost experiment: use it with the netCDF format")
     if fmt == "netcdf" and ctx.rank == 0:
         print("=> Reading NetCDF File...")
     # rank 0 creates missing files first, the others wait, then every rank reads
     direct_nc = fmt == "netcdf" and ctx.device.type == "cuda" and cfg.io_mode == "bulk"
-    if fmt == "netcdf" and (direct_nc or cfg.io_mode == "per_sample"):
+    if fmt == "netcdf" and (direct_nc or per_sample):
         if ctx.rank == 0 and find_netcdf(root) is None:
             synthesize_netcdf(root, verbose=True)
         ctx.barrier()
         paths = find_netcdf(root)
-        if cfg.io_mode == "per_sample":
+        if per_sample:
             readers = (PerSampleReader(root, True), PerSampleReader(root, False))
             n_tr = len(readers[0]) if cfg.data_limit is None else min(len(readers[0]), int(cfg.data_limit))
             xtr, ytr = np.zeros((n_tr, 28, 28), np.uint8), np.zeros(n_tr, np.uint8)
@@ -304,9 +335,15 @@ def run(cfg: TrainConfig, entry: str = "ddp_tutorial_cpu", show_banner: bool = F
             engine.load_train_arrays(x_ep, y_ep)
             order = torch.arange(len(y_ep))
             io["train"] = st
+        loader = None
+        if cfg.io_mode == "interleaved":  # each batch read right before its step (reference num_workers=0 loop)
+            loader = InterleavedLoader(readers[0], idx, engine.write_train_rows)
+            order = torch.arange(len(idx))
         bar = ProgressBar.make(cfg, ctx.rank, len(order), "training")
         with range_(f"epoch{i}.train"), timer("train"):
-            tr = engine.train_epoch(order, progress=bar, prefetch=nxt)
+            tr = engine.train_epoch(order, progress=bar, prefetch=nxt, batch_loader=loader)
+        if loader is not None:
+            io["train"] = loader.stats
         if bar is not None:
             bar.close()
         idx = tr.next_indices
@@ -314,7 +351,7 @@ def run(cfg: TrainConfig, entry: str = "ddp_tutorial_cpu", show_banner: bool = F
             tidx = torch.arange(ctx.rank, ntest, ctx.world)
         else:
             tidx = torch.arange(ntest)
-        if cfg.io_mode == "per_sample":
+        if cfg.io_mode in ("per_sample", "interleaved"):
             x_te, y_te, st = readers[1].read(tidx)
             engine.load_test_arrays(x_te, y_te)
             tidx = torch.arange(len(y_te))

@@ -27,6 +27,10 @@ FLOP_PER_IMG = {
     "wgrad": 2 * (400 * 120 + 120 * 84 + 84 * 10),
     "conv_bwd": 2 * (16 * 100 * 150 * 2 + 6 * 784 * 25),
 }
+FLOP_PER_IMG_MLP = {  # reference MLP: head = forward + dgrad of layers 3, 2 (no input grad); wgrad = all three layers
+    "head": 2 * (784 * 128 + 128 * 128 + 128 * 10) + 2 * (10 * 128 + 128 * 128),
+    "wgrad": 2 * (784 * 128 + 128 * 128 + 128 * 10),
+}
 
 
 def short(name: str) -> str:
@@ -69,6 +73,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("prefix", help="e.g. gpurun_out/pmcf (expects _a.._d run dirs)")
     ap.add_argument("--batch", type=int, default=8192)
+    ap.add_argument("--model", default="lenet5", choices=["lenet5", "mlp"])
     a = ap.parse_args()
     P = {s: load(os.path.join(f"{a.prefix}_{s}", "run_counter_collection.csv")) for s in "abcd"}
     print("| kernel | calls | us | VGPR/AGPR | LDS B/WG | waves/SIMD (res.) | MFMA busy % | LDS bank-conflict % "
@@ -84,7 +89,7 @@ def main():
         lds_act = 100.0 * cb.get("SQ_LDS_IDX_ACTIVE", 0.0) / max(1.0, cyc * N_CU) if cyc else float("nan")
         lds_c = 100.0 * cb.get("SQ_LDS_BANK_CONFLICT", 0.0) / max(1.0, cb.get("SQ_LDS_IDX_ACTIVE", 0.0))
         wait = 100.0 * ca.get("SQ_WAIT_ANY", 0.0) / max(1.0, ca.get("SQ_WAVE_CYCLES", 0.0))
-        fl = FLOP_PER_IMG.get(k)
+        fl = (FLOP_PER_IMG_MLP if a.model == "mlp" else FLOP_PER_IMG).get(k)
         tf = fl * a.batch / t / 1e12 if fl else float("nan")
         rd = 2 * cc.get("FETCH_SIZE", 0.0) * 1024 / tc / 1e9 if tc else float("nan")
         wr = cd.get("WRITE_SIZE", 0.0) * 1024 / td / 1e9 if td else float("nan")

@@ -107,14 +107,24 @@ if model == "lenet5":
     per_cu("conv_fwd", allst[2048:2048 + min(nf, 1024)], allst[2048:2048 + min(nf, 1024), 15], 14)
     per_cu("conv_bwd", allst[1024:1024 + nb], allst[4608:4608 + nb, 0], 15)  # hw location: STAMP_BWD_HWLOC
     per_cu("head", allst[:nblk], allst[:nblk, 15], 8)
+    wg = allst[3072:3584]
+    wg = wg[wg[:, 0] > 0]
+    if len(wg):  # FC weight gradient (aux stream beside conv_bwd, or between head and conv_bwd when serial)
+        print(f"wgrad: {len(wg)} workgroups; head last end -> wgrad first start {(wg[:, 0].min() - hd[:, 8].max()) * 10 / 1000:.2f} us; "
+              f"wgrad span {(wg[:, 1].max() - wg[:, 0].min()) * 10 / 1000:.2f} us; wgrad last end -> conv_bwd first start "
+              f"{(bw[:, 0].min() - wg[:, 1].max()) * 10 / 1000:.2f} us")
 
 if model == "mlp":
     def live(st):
         return st[st[:, 0] > 0]
-    report("wgrad", live(allst[3072:3584]), ["GEMM", "epilogue"], 2)
-    report("l1_split", live(allst[3584:4096]), ["stage X", "GEMM"], 2)
     l1s, hs, wgs = live(allst[3584:4096]), allst[:nblk], live(allst[3072:3584])
-    T0 = l1s[:, 0].min()
-    for name, st, last in (("l1_split", l1s, 2), ("head", hs, 8), ("wgrad", wgs, 2)):
+    wlast = 2 if (wgs[:, 2] > 0).all() else 1   # wgrad_sgd stamps 0..2, the split wgrad 0..1
+    report("wgrad", wgs, ["GEMM", "epilogue"][:wlast], wlast)
+    if len(l1s):
+        report("l1_split", l1s, ["stage X", "GEMM"], 2)
+    T0 = (l1s if len(l1s) else hs)[:, 0].min()
+    for name, st, last in (("l1_split", l1s, 2), ("head", hs, 8), ("wgrad", wgs, wlast)):
+        if not len(st):
+            continue
         print(f"{name:9s} first start {(st[:, 0].min() - T0) * 10 / 1000:6.2f} us  last start "
               f"{(st[:, 0].max() - T0) * 10 / 1000:6.2f}  last end {(st[:, last].max() - T0) * 10 / 1000:6.2f}")

@@ -90,3 +90,8 @@ def test_pnetcdf_per_sample_io_mode(tmp_path):
     assert "per-sample netCDF test: 10000 samples" in per
     assert LINE.search(per).group(0) == LINE.search(bulk).group(0)
     assert per.count("=> Dataset created, image nc file is") >= 2   # reference MNISTNetCDF prints, train + test
+    # interleaved: each batch read right before its step (reference num_workers=0 loop) -- same training
+    inter = _run(args + ["--io_mode", "interleaved"], tmp_path)
+    m = re.search(r"per-sample netCDF train: (\d+) samples", inter)
+    assert m and int(m.group(1)) == 1024, inter
+    assert LINE.search(inter).group(0) == LINE.search(bulk).group(0)
