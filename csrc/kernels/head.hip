@@ -155,13 +155,18 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   };
   stamp(0);
 
-  // B operands of each phase: LDS images when they fit (WLDS), else the packed global copies
-  const T* bW2 = S::WLDS ? reinterpret_cast<const T*>(smem + S::OFF_W2) : pack + H::F2;
-  const T* bW2T = S::WLDS ? reinterpret_cast<const T*>(smem + S::OFF_W2T) : pack + H::F2T;
-  const T* bW3 = S::WLDS ? reinterpret_cast<const T*>(smem + S::OFF_W3) : pack + H::F3;
-  const T* bW3T = S::WLDS ? reinterpret_cast<const T*>(smem + S::OFF_W3T) : pack + H::F3T;
-  constexpr int LW2 = S::WLDS ? S::PW2 : H::N1P, LW2T = S::WLDS ? S::PW2T : H::N2P;
-  constexpr int LW3 = S::WLDS ? S::PW3 : H::N2P, LW3T = S::WLDS ? S::PW3T : H::NCK;
+  // B operands of each phase: LDS images when they fit (WLDS), else -- WX: a model without an input
+  // gradient (the MLP), whose X tile is dead after layer 1 -- the same images staged into the X region
+  // after layer 1 (loads issued before it), else the packed global copies
+  constexpr bool WX = !S::WLDS && !PRE && !H::DX && S::W_END - S::OFF_W2 <= S::OFF_H1 - S::OFF_X;
+  constexpr bool WIN = S::WLDS || WX;            // B operands of layers 2/3 and their dgrads from LDS
+  constexpr int WOFF = WX ? S::OFF_X - S::OFF_W2 : 0;  // where the weight images live
+  const T* bW2 = WIN ? reinterpret_cast<const T*>(smem + WOFF + S::OFF_W2) : pack + H::F2;
+  const T* bW2T = WIN ? reinterpret_cast<const T*>(smem + WOFF + S::OFF_W2T) : pack + H::F2T;
+  const T* bW3 = WIN ? reinterpret_cast<const T*>(smem + WOFF + S::OFF_W3) : pack + H::F3;
+  const T* bW3T = WIN ? reinterpret_cast<const T*>(smem + WOFF + S::OFF_W3T) : pack + H::F3T;
+  constexpr int LW2 = WIN ? S::PW2 : H::N1P, LW2T = WIN ? S::PW2T : H::N2P;
+  constexpr int LW3 = WIN ? S::PW3 : H::N2P, LW3T = WIN ? S::PW3T : H::NCK;
 
   // ---- PRE: this thread's layer-1 partial sums (written by l1_split_kernel), issued first: their
   //      latency overlaps the weight staging instead of following it
@@ -187,15 +192,20 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   constexpr bool PF1 = !PRE && KH1 <= 16;  // <= 64 VGPRs of prefetched fragments
   const int l1_nt = KS1 ? w % NT1 : w, l1_half = KS1 ? w / NT1 : 0;
   const int l1_k0 = l1_half * KH1, l1_k1 = KS1 ? (l1_half ? KCH1 : KH1) : KCH1;
-  const bool l1_live = KS1 ? w < 2 * NT1 : w < NT1;
+  const bool l1_live = KS1 ? (NWV == 2 * NT1 || w < 2 * NT1) : w < NT1;  // constant true when every wave works
   Frag b1pre[PF1 ? KH1 : 1];
-  if constexpr (PF1) {
-    if (l1_live) {
-      const T* bp = pack + H::F1 + (l1_nt * 16 + row) * H::K0P + grp * KV;
+  auto prefetch_b1 = [&] {
+    if constexpr (PF1) {
+      if (l1_live) {
+        const T* bp = pack + H::F1 + (l1_nt * 16 + row) * H::K0P + grp * KV;
 #pragma unroll
-      for (int kc = 0; kc < KH1; ++kc) b1pre[kc] = M::load(bp + min(l1_k0 + kc, KCH1 - 1) * KC);
+        for (int kc = 0; kc < KH1; ++kc) b1pre[kc] = M::load(bp + min(l1_k0 + kc, KCH1 - 1) * KC);
+      }
     }
-  }
+  };
+  // (the gathering head issues them after its pixel loads: vmcnt counts in order, so prefetched W1
+  //  fragments issued first would make the gather's conversion wait for all of W1)
+  if constexpr (!H::GATHER) prefetch_b1();
 
   // ---- look-ahead (small-batch MLP training): this step's labels come from ynext (gathered by the
   //      previous step), and this kernel gathers the NEXT step's rows of its tile into xnext / ynext
@@ -314,10 +324,18 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
         px[i][q] = *reinterpret_cast<const u32x4*>(br.images + (size_t)max(sidx, 0) * 784 + min(c, H::K0 / 16 - 1) * 16);
       }
     }
+    // pinned order: pixel loads, then the W1 prefetch, then the conversion (which then waits for the
+    // pixels only -- the scheduler otherwise hoisted the prefetch above them and sank the pixel loads into
+    // the conversion, one wait per row)
+    __builtin_amdgcn_sched_barrier(0);
+    prefetch_b1();
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < ITG; ++i) {
-      const int e = tid + i * NTH, r = (e % (R / 4)) * 4, c = e / (R / 4);
-      if (e >= NGI) break;
+      // threads past the last item convert the (clamped) last item again and skip the stores: no branch
+      // around the loads' consumers
+      const int eu = tid + i * NTH, e = min(eu, NGI - 1), r = (e % (R / 4)) * 4, c = e / (R / 4);
+      const bool item = eu < NGI;
       if constexpr (sizeof(T) == 2) {
         // each row's 16 pixels -> 16 bf16 packed in 8 registers (two 16-byte LDS stores); the xT store of
         // pixel j takes halfword j of the four rows (as the pool2-row path below)
@@ -329,13 +347,15 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
           for (int h = 0; h < 2; ++h) {
             bf16x8 f;
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-              f[j] = (bf16)(live ? mnist_norm((px[i][q][2 * h + (j >> 2)] >> (8 * (j & 3))) & 255u) : 0.f);
+            for (int j = 0; j < 8; ++j) {  // computed unconditionally, then selected: no per-pixel branch
+              const float nv = mnist_norm((px[i][q][2 * h + (j >> 2)] >> (8 * (j & 3))) & 255u);
+              f[j] = (bf16)(live ? nv : 0.f);
+            }
             pk[q][h] = __builtin_bit_cast(u32x4, f);
-            *reinterpret_cast<u32x4*>(sX + (r + q) * S::PX + c * 16 + h * 8) = pk[q][h];
+            if (item) *reinterpret_cast<u32x4*>(sX + (r + q) * S::PX + c * 16 + h * 8) = pk[q][h];
           }
         }
-        if constexpr (TRAIN) {
+        if (TRAIN && item) {
 #pragma unroll
           for (int j = 0; j < 16; ++j) {
             const int h = j >> 3, wd = (j & 7) >> 1, sh = 16 * (j & 1);
@@ -352,11 +372,13 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
           for (int q = 0; q < 4; ++q) {
             const bool live = sIdx[r + q] >= 0 && c < H::K0 / 16;
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-              v[q][j] = live ? mnist_norm((px[i][q][(j0 + j) >> 2] >> (8 * ((j0 + j) & 3))) & 255u) : 0.f;
-            *reinterpret_cast<f32x4*>(sX + (r + q) * S::PX + c * 16 + j0) = f32x4{v[q][0], v[q][1], v[q][2], v[q][3]};
+            for (int j = 0; j < 4; ++j) {
+              const float nv = mnist_norm((px[i][q][(j0 + j) >> 2] >> (8 * ((j0 + j) & 3))) & 255u);
+              v[q][j] = live ? nv : 0.f;
+            }
+            if (item) *reinterpret_cast<f32x4*>(sX + (r + q) * S::PX + c * 16 + j0) = f32x4{v[q][0], v[q][1], v[q][2], v[q][3]};
           }
-          if constexpr (TRAIN) {
+          if (TRAIN && item) {
 #pragma unroll
             for (int j = 0; j < 4; ++j)
               store_col4<T>(xT + (size_t)(c * 16 + j0 + j) * ldB + r0 + r, v[0][j], v[1][j], v[2][j], v[3][j]);
@@ -426,6 +448,14 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   const float keep_scale = H::DROPOUT ? 1.0f / (1.0f - hb.drop_p) : 1.0f;
   const uint32_t drop_thr = H::DROPOUT ? (uint32_t)(hb.drop_p * 4294967295.0f) : 0u;
 
+  if constexpr (WX) {  // weight images for after layer 1 (issued after the label loads: in-order vmcnt)
+    st_w2.load(pack + H::F2, tid);
+    if constexpr (STW_T) {
+      st_w2t.load(pack + H::F2T, tid);
+      st_w3t.load(pack + H::F3T, tid);
+    }
+    st_w3.load(pack + H::F3, tid);
+  }
   // ---------------------------------------------------------------- L1: H1 = relu(X W1^T + b1)
   if constexpr (PRE) {
     // sum the L1_KSPLIT partial products in a fixed order, then the same bias/ReLU/dropout epilogue
@@ -507,6 +537,16 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
     }
   }
   __syncthreads();
+  if constexpr (WX) {  // the X tile is dead: the weight images land in its place (loads issued before L1)
+    T* wb = reinterpret_cast<T*>(smem + WOFF + S::OFF_W2);
+    st_w2.store(wb, tid);
+    if constexpr (STW_T) {
+      st_w2t.store(reinterpret_cast<T*>(smem + WOFF + S::OFF_W2T), tid);
+      st_w3t.store(reinterpret_cast<T*>(smem + WOFF + S::OFF_W3T), tid);
+    }
+    st_w3.store(reinterpret_cast<T*>(smem + WOFF + S::OFF_W3), tid);
+    __syncthreads();
+  }
   stamp(2);
   // ---------------------------------------------------------------- L2: H2 = relu(H1 W2^T + b2)
   {
@@ -660,7 +700,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   {
     // (FT: B[k = c][n] = W3[c][n] read k-strided from the W3 image; the zero dZ columns c >= 16
     //  contribute nothing, so only the 16 staged rows are read)
-    constexpr bool TW3 = S::FT && S::WLDS;
+    constexpr bool TW3 = S::FT && WIN;
     constexpr int NT = H::N2P / 16, KCH = (TW3 ? H::NCP : H::NCK) / KC;
     T* dy2T = reinterpret_cast<T*>(hb.dy2T);
     for (int nt = w; nt < NT; nt += NWV) {
@@ -702,7 +742,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
 
   // ---------------------------------------------------------------- dH1 = (dH2 W2) * [H1 > 0] / keep
   {
-    constexpr bool TW2 = S::FT && S::WLDS;  // B[k = n2][n = n1] = W2[n2][n1], k-strided from the W2 image
+    constexpr bool TW2 = S::FT && WIN;  // B[k = n2][n = n1] = W2[n2][n1], k-strided from the W2 image
     constexpr int NT = H::N1P / 16, KCH = H::N2P / KC;
     T* dy1T = reinterpret_cast<T*>(hb.dy1T);
     for (int nt = w; nt < NT; nt += NWV) {
@@ -1031,6 +1071,129 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
   if (a.stamps && threadIdx.x == 0 && lin < 512) a.stamps[(STAMP_WGRAD + lin) * 16 + 1] = wall_clock64();
 }
 
+// LDS-staged variant of wgrad_kernel (same tiles, splits, step order and slab layout; every output element
+// is the same MFMA chain, so the results are bitwise those of wgrad_kernel): per 32-row K-step the
+// workgroup stages the 64-row dY^T tile and the 64-row X^T tile ONCE (one 16-byte chunk of each per
+// thread, loaded a step ahead into registers), and each wave reads its 32x32 operands from LDS.  In
+// wgrad_kernel every fragment is fetched by two waves straight from L2 -- twice the L2 -> CU traffic,
+// which bounds that kernel (~37 GB/s per CU measured on the MLP at B=8192).  96-byte rows (64 data + 32
+// pad) make the fragment reads conflict-free for ds_read_b128's lane groups.  Needs 24 KB of LDS, so it
+// is for the schedules where nothing LDS-heavy runs beside it (the MLP; LeNet's FC wgrad shares the CUs
+// with conv_bwd and keeps the LDS-free kernel).
+template <typename T>
+__global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
+  using M = Mma<T>;
+  using Frag = typename M::Frag;
+  constexpr int KV = M::KV, KC = M::KC;
+  constexpr int PE = 96 / (int)sizeof(T);    // row pitch (elements): 64 B of data + 32 B of padding
+  constexpr int TILE = 64 * PE;              // one [64 rows][KC] tile
+  __shared__ __attribute__((aligned(16))) T lds[2][2][TILE];  // [buffer][A = dY^T, B = X^T]
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
+  const int lin = blockIdx.y * gridDim.x + blockIdx.x;
+  if (a.stamps && threadIdx.x == 0 && lin < 512) a.stamps[(STAMP_WGRAD + lin) * 16] = wall_clock64();
+  int tile, split, nsteps, x = 0, m0 = 0, spc = 1, rs = 0;
+  if (a.xcd_ch == 0) {
+    tile = blockIdx.x;
+    split = blockIdx.y;
+    rs = split * a.rlen;
+    nsteps = (min(rs + a.rlen, a.Bp) - rs + KC - 1) / KC;
+  } else {
+    const int L = blockIdx.x, q = L >> 3;
+    x = L & 7;
+    tile = q / a.sx;
+    const int sub = q % a.sx;
+    split = x * a.sx + sub;
+    const int mx = a.contig ? a.nch / 8 : (x < a.nch ? (a.nch - x + 7) / 8 : 0);
+    m0 = sub * mx / a.sx;
+    const int m1 = (sub + 1) * mx / a.sx;
+    spc = a.xcd_ch / KC;
+    nsteps = (m1 - m0) * spc;
+  }
+  auto step_row = [&](int st) -> int {  // first batch row of step st (monotonic in st)
+    if (a.xcd_ch == 0) return rs + st * KC;
+    const int m = m0 + st / spc;
+    return (a.contig ? x * (a.nch / 8) + m : x + 8 * m) * a.xcd_ch + (st % spc) * KC;
+  };
+  while (nsteps > 0 && step_row(nsteps - 1) >= a.Bp) --nsteps;  // steps past the (padded) batch
+  int j = 0;
+  while (j + 1 < a.njobs && tile >= a.job[j + 1].blk_begin) ++j;
+  const WgJob<T>& J = a.job[j];
+  const int lb = tile - J.blk_begin;
+  const int bn = lb / J.nblk_k, bk = lb % J.nblk_k;
+  const int nb0 = bn * 64, kb0 = bk * 64;              // block origin (block-uniform)
+  const int n0 = nb0 + (w >> 1) * 32, k0 = kb0 + (w & 1) * 32;
+  const int Kb = J.K + (J.bias ? 1 : 0);
+  const bool wave_live = n0 < J.N && k0 < Kb;         // waves without outputs still stage and sync
+
+  // staging role: tile row r = tid / 4, 16-byte chunk c = tid % 4 of the step's KC elements
+  const int sr = tid >> 2, sc = tid & 3;
+  const bool a_ok = nb0 + sr < J.NP, b_ok = kb0 + sr < J.K;
+  const T* asrc = J.dyT + (size_t)min(nb0 + sr, J.NP - 1) * a.ldB + sc * KV;
+  const T* bsrc = J.xT + (size_t)min(kb0 + sr, J.K > 0 ? J.K - 1 : 0) * a.ldB + sc * KV;
+  const u32x4 z4 = u32x4{0u, 0u, 0u, 0u};
+  u32x4 ra, rb;
+  auto fetch = [&](int st) {
+    const int rc = step_row(st);
+    ra = *reinterpret_cast<const u32x4*>(asrc + rc);
+    rb = *reinterpret_cast<const u32x4*>(bsrc + rc);
+  };
+  auto stage = [&](int buf) {
+    *reinterpret_cast<u32x4*>(&lds[buf][0][sr * PE + sc * KV]) = a_ok ? ra : z4;
+    *reinterpret_cast<u32x4*>(&lds[buf][1][sr * PE + sc * KV]) = b_ok ? rb : z4;
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = zero4();
+  Frag ones;
+#pragma unroll
+  for (int q = 0; q < KV; ++q) M::set(ones, q, 1.f);
+  const Frag zf = M::zero();
+  const int kk0 = k0 + row, kk1 = k0 + 16 + row;
+  const int sel0 = kk0 < J.K ? 0 : (kk0 == J.K && J.bias ? 1 : 2);
+  const int sel1 = kk1 < J.K ? 0 : (kk1 == J.K && J.bias ? 1 : 2);
+  const int ao0 = (n0 - nb0 + row) * PE + grp * KV, ao1 = ao0 + 16 * PE;
+  const int bo0 = (k0 - kb0 + row) * PE + grp * KV, bo1 = bo0 + 16 * PE;
+
+  if (nsteps > 0) {
+    fetch(0);
+    stage(0);
+  }
+  __syncthreads();
+  for (int st = 0; st < nsteps; ++st) {
+    const int buf = st & 1;
+    if (st + 1 < nsteps) fetch(st + 1);  // next step's chunks in flight during this step's MFMAs
+    const Frag a0 = M::load(&lds[buf][0][ao0]), a1 = M::load(&lds[buf][0][ao1]);
+    const Frag f0 = M::load(&lds[buf][1][bo0]), f1 = M::load(&lds[buf][1][bo1]);
+    const Frag b0 = sel0 == 0 ? f0 : (sel0 == 1 ? ones : zf);
+    const Frag b1 = sel1 == 0 ? f1 : (sel1 == 1 ? ones : zf);
+    M::mma(acc[0][0], a0, b0);
+    M::mma(acc[0][1], a0, b1);
+    M::mma(acc[1][0], a1, b0);
+    M::mma(acc[1][1], a1, b1);
+    if (st + 1 < nsteps) stage(buf ^ 1);  // that buffer was last read in step st - 1, before the barrier
+    __syncthreads();
+  }
+  if (!wave_live) return;
+
+  float* out = a.slab + (size_t)split * a.slab_ld + J.out_off;
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) {
+      const int k = k0 + ni * 16 + row;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int n = n0 + mi * 16 + grp * 4 + i;
+        const int q = n >= J.N ? -1 : (k < J.K ? n * J.K + k : (k == J.K && J.bias ? J.N * J.K + n : -1));
+        if (q >= 0) out[q] = acc[mi][ni][i];
+      }
+    }
+  if (a.stamps && threadIdx.x == 0 && lin < 512) a.stamps[(STAMP_WGRAD + lin) * 16 + 1] = wall_clock64();
+}
+
 // Weight-gradient GEMM + SGD update for one GPU and ONE batch split (small batches): every output
 // element is the whole gradient, so the update is the epilogue -- g = scale * dW, momentum, parameter,
 // packed operand images, device step counters -- and the separate reduce + SGD kernel disappears
@@ -1118,13 +1281,24 @@ __global__ __launch_bounds__(256) void wgrad_sgd_kernel(WgArgs<T> a) {
   stamp(2);
 }
 
-// K-steps of fragments in flight per wave in wgrad_kernel (MNIST_AMD_WGRAD_DEPTH=2: one step of look-ahead)
+// Ring slots of K-step fragments per wave in wgrad_kernel (MNIST_AMD_WGRAD_DEPTH A/B knob): 1 = the next
+// step's fragments fetched while this one computes (default), 2 / 4 = two / four steps ahead (LeNet:
+// 1 and 2 within noise; 4 measured 0.3-1.6 % slower than 2 on both models)
 inline int wgrad_depth() {
   static const int d = [] {
     const char* e = std::getenv("MNIST_AMD_WGRAD_DEPTH");
-    return e ? std::atoi(e) : 4;
+    return e ? std::atoi(e) : 1;
   }();
   return d;
+}
+// LDS-staged weight gradient (wgrad_lds_kernel): default for the MLP, whose wgrad runs alone on the chip;
+// MNIST_AMD_WGRAD_LDS=0/1 overrides (A/B knob)
+inline bool wgrad_lds(bool mlp) {
+  static const int e = [] {
+    const char* v = std::getenv("MNIST_AMD_WGRAD_LDS");
+    return v ? std::atoi(v) : -1;
+  }();
+  return e < 0 ? mlp : e != 0;
 }
 
 template <typename T, class H, class Model>
@@ -1164,6 +1338,7 @@ int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab
   a.slab_ld = slab_ld;
   a.stamps = hb.stamps;
   a.xcd_ch = 0;
+  const bool lds_stage = wgrad_lds(std::is_same<Model, MlpModel>::value);
   static const bool xcd_off = std::getenv("MNIST_AMD_NO_XCD") != nullptr;  // A/B knob
   // XCD-aware mapping when the head's row tiling is known and the split count divides over 8 XCDs
   if (!fuse && !xcd_off && xcd_ch > 0 && xcd_ch % KC == 0 && splits % 8 == 0) {
@@ -1172,13 +1347,17 @@ int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab
     a.sx = splits / 8;
     const int head_grid = (rup(B, 32) + xcd_ch - 1) / xcd_ch;  // head_launch_mtw's grid
     a.contig = hb.xcd && head_grid % 8 == 0 && a.nch == head_grid;
-    if (wgrad_depth() == 2) hipLaunchKernelGGL((wgrad_kernel<T, 2>), dim3(blk * splits), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((wgrad_kernel<T, 4>), dim3(blk * splits), dim3(256), 0, s, a);
+    if (lds_stage) hipLaunchKernelGGL(wgrad_lds_kernel<T>, dim3(blk * splits), dim3(256), 0, s, a);
+    else if (wgrad_depth() == 4) hipLaunchKernelGGL((wgrad_kernel<T, 4>), dim3(blk * splits), dim3(256), 0, s, a);
+    else if (wgrad_depth() == 1) hipLaunchKernelGGL((wgrad_kernel<T, 1>), dim3(blk * splits), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_kernel<T, 2>), dim3(blk * splits), dim3(256), 0, s, a);
   } else if (a.fuse) {
     hipLaunchKernelGGL((wgrad_sgd_kernel<T, Model>), dim3(blk), dim3(256), 0, s, a);
   } else {
-    if (wgrad_depth() == 2) hipLaunchKernelGGL((wgrad_kernel<T, 2>), dim3(blk, splits), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((wgrad_kernel<T, 4>), dim3(blk, splits), dim3(256), 0, s, a);
+    if (lds_stage) hipLaunchKernelGGL(wgrad_lds_kernel<T>, dim3(blk, splits), dim3(256), 0, s, a);
+    else if (wgrad_depth() == 4) hipLaunchKernelGGL((wgrad_kernel<T, 4>), dim3(blk, splits), dim3(256), 0, s, a);
+    else if (wgrad_depth() == 1) hipLaunchKernelGGL((wgrad_kernel<T, 1>), dim3(blk, splits), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_kernel<T, 2>), dim3(blk, splits), dim3(256), 0, s, a);
   }
   return splits;
 }
@@ -1237,7 +1416,14 @@ void head_launch_split(bool train, const BatchRef& br, const HeadBuffers& hb, hi
 // returns the batch rows per workgroup actually used (the wgrad kernel's XCD-aware mapping needs it)
 template <typename T, class H>
 int head_launch_t(bool train, const BatchRef& br, const HeadBuffers& hb, int rows, hipStream_t s) {
-  if (hb.z1p && br.B <= L1_SPLIT_MAX_B && !std::getenv("MNIST_AMD_NO_L1_SPLIT")) {
+  // the split layer 1 pays for its extra launch only on the 784-deep MLP layer; LeNet's 400-deep layer 1
+  // runs inside the head (B=128: 38.2 vs 39.9 us per step with the split).  MNIST_AMD_L1_SPLIT=0/1 overrides.
+  static const int l1s = [] {
+    const char* e = std::getenv("MNIST_AMD_L1_SPLIT");
+    return e ? std::atoi(e) : (std::getenv("MNIST_AMD_NO_L1_SPLIT") ? 0 : -1);
+  }();
+  const bool split_l1 = l1s < 0 ? H::K0 >= 512 : l1s != 0;
+  if (hb.z1p && br.B <= L1_SPLIT_MAX_B && split_l1) {
     head_launch_split<T, H>(train, br, hb, s);
     return 16;
   }
@@ -1287,9 +1473,10 @@ int head_rows_per_block(ModelKind m, DType t, int B) {
   if (B <= 256) return 16;
   if (t == DType::F32) return 32;
   if (m == ModelKind::MLP) return B >= 4096 ? 64 : 32;
-  // LeNet bf16, 16-wave workgroups: 64-row tiles (128 workgroups at B=8192) measured best
-  // (step 0.2004 ms vs 0.2023 at 32 rows, 0.215 at 16 rows)
-  return B >= 4096 ? 64 : 32;
+  // LeNet bf16, 16-wave workgroups: 32-row tiles = 256 workgroups at B=8192, every CU (0.1143-0.1150 ms
+  // per step vs 0.1184-0.1186 with 64-row tiles on 128 CUs, same box; before the head's end-of-kernel
+  // atomics were removed the 64-row tiles had measured 0.5 % faster)
+  return 32;
 }
 
 int launch_head(ModelKind m, DType t, bool train, const BatchRef& br, const HeadBuffers& hb, int rows,
