@@ -40,6 +40,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("model_phase_split", [](int model) { return model_phase_split(static_cast<ModelKind>(model)); });
   m.def("model_pack_size", [](int model) { return model_pack_size(static_cast<ModelKind>(model)); });
   m.def("conv_bwd_blocks", &lenet_conv_bwd_blocks, py::arg("B"), py::arg("target_blocks") = 0);
+  m.def("fwd_head_applies", [](int dtype, int B) { return lenet_fwd_head_applies(static_cast<DType>(dtype), B); },
+        py::arg("dtype"), py::arg("B"));
   m.def("conv_bwd_max_blocks", &lenet_conv_bwd_max_blocks, py::arg("B"), py::arg("target_blocks") = 0);
   m.attr("L1_KSPLIT") = L1_KSPLIT;
   m.def("metric_rows", [](int B) { return metric_rows(B); });
@@ -133,6 +135,8 @@ PYBIND11_MODULE(_C, m) {
       .def("set_plan", &Trainer::set_plan)
       .def_property_readonly("plan", &Trainer::plan)
       .def("set_concurrent", &Trainer::set_concurrent)
+      .def("set_fwd_head", &Trainer::set_fwd_head)
+      .def_property_readonly("fwd_head", &Trainer::fwd_head)
       .def_property_readonly("concurrent", &Trainer::concurrent)
       .def("set_bwd_blocks", &Trainer::set_bwd_blocks)
       .def_property_readonly("bwd_blocks", &Trainer::bwd_blocks)

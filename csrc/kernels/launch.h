@@ -110,6 +110,14 @@ int launch_head_wgrad(ModelKind m, DType t, const HeadBuffers& hb, int B, int sp
 
 void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetConvBuffers& cb,
                            hipStream_t s);
+// LeNet training forward + FC head (fwd, softmax-CE, dgrad) in one kernel (lenet.hip fwd_head_kernel):
+// replaces launch_lenet_conv_fwd + launch_head for bf16 batches B >= 4096, B % 16 == 0 (MNIST_AMD_FWD_HEAD=0
+// disables it).  Returns the head-rows value for launch_head_wgrad's XCD-aware mapping (32: the fused
+// kernel's 16-row units give each XCD the same contiguous eighth of the batch as 32-row head tiles), or 0
+// when it does not apply (the caller launches the two kernels).
+int launch_lenet_fwd_head(DType t, const BatchRef& br, const LenetConvBuffers& cb, const HeadBuffers& hb,
+                          hipStream_t s);
+bool lenet_fwd_head_applies(DType t, int B);
 // mode 0: full backward; 1: conv2 dgrad + conv1 wgrad half; 2: conv2 wgrad half (lenet.hip MODE)
 // target_blocks: workgroup count to aim for (0 = default, one full round of 2 blocks per CU); each
 // block walks ceil(B / target) images, so a smaller target leaves whole CUs free (for RCCL kernels).

@@ -38,11 +38,13 @@ constexpr int P1IMG = 6 * P1CP;      // elements per image in cb.p1
 constexpr int M1CP = 240;            // pool1 code channel pitch (bytes), multiple of 16
 constexpr int M1IMG = 6 * M1CP;      // bytes per image in cb.m1
 
+// p 16-byte aligned; 16-byte stores, scalar tail; by threads tid of nth (default: the whole workgroup)
 template <typename T>
-DEV void zero_lds(T* p, int n) {  // p 16-byte aligned; 16-byte stores, scalar tail
+DEV void zero_lds(T* p, int n, int tid = -1, int nth = 0) {
+  if (tid < 0) { tid = threadIdx.x; nth = blockDim.x; }
   const int nv = n * (int)sizeof(T) / 16;
-  for (int e = threadIdx.x; e < nv; e += blockDim.x) reinterpret_cast<uint4*>(p)[e] = make_uint4(0, 0, 0, 0);
-  for (int e = nv * 16 / (int)sizeof(T) + threadIdx.x; e < n; e += blockDim.x) p[e] = to_t<T>(0.f);
+  for (int e = tid; e < nv; e += nth) reinterpret_cast<uint4*>(p)[e] = make_uint4(0, 0, 0, 0);
+  for (int e = nv * 16 / (int)sizeof(T) + tid; e < n; e += nth) p[e] = to_t<T>(0.f);
 }
 
 // The sample indices of a workgroup's images, loaded ONCE at kernel start: lane l of every wave holds
@@ -97,35 +99,39 @@ struct FwdSmem {
 // output is read only after another kernel has run (pool1 -> conv_bwd), so it is stored non-temporally
 // and is not left dirty in L2 for the kernel-end write-back; pool2 (read by the very next kernel) is not.
 template <bool STREAM = false>
-DEV void copy_out16(void* dst, const void* src, int bytes) {
-  for (int e = threadIdx.x; e < bytes / 16; e += blockDim.x) {
+DEV void copy_out16(void* dst, const void* src, int bytes, int tid, int nth) {
+  for (int e = tid; e < bytes / 16; e += nth) {
     const uint4 v = reinterpret_cast<const uint4*>(src)[e];
     if constexpr (STREAM) st_stream16(reinterpret_cast<uint4*>(dst) + e, v);
     else reinterpret_cast<uint4*>(dst)[e] = v;
   }
 }
 
-template <typename T, bool TRAIN>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void conv_fwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
+// The image loop of the forward pass, run by 4 waves (local thread ids 0..255) over the images
+// [first, first + ipb) in the LDS region `smem` (FwdSmem layout).  conv_fwd_kernel runs one such stream
+// per workgroup; fwd_head_kernel runs two (one per 4-wave half) and then the FC head on their rows.
+// XROWS (fwd_head_kernel): pool2 of image t goes to row xrow0 + t of the head's LDS input tile `xrows`
+// (row pitch XPITCH, zero for images past the batch) instead of global memory.
+template <typename T, bool TRAIN, bool XROWS = false, int XPITCH = 0>
+DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int first, int ipb, char* smem, int tid,
+                         int w, bool stamper, T* xrows) {
   using M = Mma<T>;
   using Frag = typename M::Frag;
   using S = FwdSmem<T>;
   constexpr int KV = M::KV, KC = M::KC;
-  __shared__ __attribute__((aligned(16))) char smem[S::TOTAL];
   T* xs = reinterpret_cast<T*>(smem + S::OFF_XS);
   T* p1s = reinterpret_cast<T*>(smem + S::OFF_P1);
   T* p1c = reinterpret_cast<T*>(smem + S::OFF_P1C);
   uint8_t* m1s = reinterpret_cast<uint8_t*>(smem + S::OFF_M1);
   T* p2s = reinterpret_cast<T*>(smem + S::OFF_P2);
   uint8_t* m2s = reinterpret_cast<uint8_t*>(smem + S::OFF_M2);
-  const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
-  const int unit = xcd_unit(blockIdx.x, gridDim.x, br.xcd);  // this workgroup's images: [unit * ipb, +ipb)
-  const BlockIdx bidx(br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride, unit * ipb, ipb, br.B);
+  const int lane = tid & 63, row = lane & 15, grp = lane >> 4;
+  const BlockIdx bidx(br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride, first, ipb, br.B);
   const T* pack = reinterpret_cast<const T*>(cb.pack);
   const float* prm = cb.params;
   // optional wall-clock stamps (profiling): [0] start, [1] setup, 3 per image for images 0..3, [14] loop end
   auto stamp = [&](int k) {
-    if (cb.stamps && tid == 0 && blockIdx.x < 1024) cb.stamps[(STAMP_CONV_FWD - STAMP_CONV_BWD + blockIdx.x) * 16 + k] = wall_clock64();
+    if (cb.stamps && stamper && blockIdx.x < 1024) cb.stamps[(STAMP_CONV_FWD - STAMP_CONV_BWD + blockIdx.x) * 16 + k] = wall_clock64();
   };
   stamp(0);
 
@@ -142,7 +148,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   // stage, and images past the batch are masked with `valid`.
   auto fetch = [&](int t) -> Raw {  // software pipeline: image t+1's bytes are in flight during image t
     Raw r;
-    const bool live = t < ipb && unit * ipb + t < br.B;  // wave-uniform
+    const bool live = t < ipb && first + t < br.B;  // wave-uniform
     const uint8_t* rowp = br.images + (size_t)bidx[live ? t : 0] * 784 + min(sy - 2, 27) * 28;
 #pragma unroll
     for (int k = 0; k < 5; ++k) r.d[k] = *reinterpret_cast<const uint32_t*>(rowp + min(max(8 * sg - 4 + 4 * k, 0), 24));
@@ -253,7 +259,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
       for (int j = 0; j < NT; ++j) a[j] = an[j];
     }
   };
-  auto c2_epi = [&](int mt, const f32x4& acc) {
+  auto c2_epi = [&](int t, bool valid, int mt, const f32x4& acc) {
     const int n = row, pp = mt * 4 + grp;
     if (pp < 25) {
       float mx = acc[0];
@@ -262,21 +268,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
       for (int i = 1; i < 4; ++i)
         if (acc[i] > mx) { mx = acc[i]; am = i; }
       const float pre = mx + bias2;
-      p2s[n * 25 + pp] = to_t<T>(fmaxf(pre, 0.f));
+      if constexpr (XROWS) xrows[t * XPITCH + n * 25 + pp] = to_t<T>(valid ? fmaxf(pre, 0.f) : 0.f);
+      else p2s[n * 25 + pp] = to_t<T>(fmaxf(pre, 0.f));
       m2s[n * 25 + pp] = (uint8_t)(am | (pre > 0.f ? 4 : 0));
     }
   };
   auto flush_p2 = [&](int bprev) {  // previous image's pool2 outputs -> HBM (16-byte stores)
     if (bprev >= 0 && bprev < br.B) {
-      copy_out16(reinterpret_cast<T*>(cb.p2) + (size_t)bprev * K0P, p2s, 400 * (int)sizeof(T));
-      if (TRAIN) copy_out16(cb.m2 + (size_t)bprev * 400, m2s, 400);
+      if constexpr (!XROWS) copy_out16(reinterpret_cast<T*>(cb.p2) + (size_t)bprev * K0P, p2s, 400 * (int)sizeof(T), tid, 256);
+      if (TRAIN) copy_out16(cb.m2 + (size_t)bprev * 400, m2s, 400, tid, 256);
     }
   };
 
-  zero_lds<T>(xs, 8 * S::XP + S::XTAIL);
+  zero_lds<T>(xs, 8 * S::XP + S::XTAIL, tid, 256);
   if (TRAIN) {
-    zero_lds<T>(p1c, P1IMG);
-    zero_lds<uint8_t>(m1s, M1IMG);
+    zero_lds<T>(p1c, P1IMG, tid, 256);
+    zero_lds<uint8_t>(m1s, M1IMG, tid, 256);
   }
   // b1 / b2r / biases are loop-invariant registers loaded from global memory above (image 0's pixels
   // are also in flight and consumed right after this barrier anyway)
@@ -284,7 +291,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
   __syncthreads();
   stamp(1);
   for (int t = 0; t < ipb; ++t) {
-    const int b = unit * ipb + t;
+    const int b = first + t;
     const bool valid = b < br.B;
     const Raw u = u_next;
     // ---- stage: normalise once, 4 aligned 16-byte plane stores per thread
@@ -376,8 +383,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
 
     // ---- pool1 -> HBM for the backward pass (16-byte stores), overlapped with conv2
     if (TRAIN && valid && !(cb.ablate & 1024)) {
-      copy_out16<true>(reinterpret_cast<T*>(cb.p1) + (size_t)b * P1IMG, p1c, P1IMG * (int)sizeof(T));
-      copy_out16<true>(cb.m1 + (size_t)b * M1IMG, m1s, M1IMG);
+      copy_out16<true>(reinterpret_cast<T*>(cb.p1) + (size_t)b * P1IMG, p1c, P1IMG * (int)sizeof(T), tid, 256);
+      copy_out16<true>(cb.m1 + (size_t)b * M1IMG, m1s, M1IMG, tid, 256);
     }
     // ---- conv2 + bias + ReLU + maxpool: 100 rows (25 pooled x 4) = 7 M-tiles, N = 16
     if (!(cb.ablate & 4)) {
@@ -385,33 +392,353 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
         const int mts[2] = {2 * w, 2 * w + 1};
         f32x4 acc[2] = {zero4(), zero4()};
         c2_acc(std::integral_constant<int, 2>{}, mts, acc);
-        c2_epi(2 * w, acc[0]);
-        c2_epi(2 * w + 1, acc[1]);
+        c2_epi(t, valid, 2 * w, acc[0]);
+        c2_epi(t, valid, 2 * w + 1, acc[1]);
       } else {
         const int mts[1] = {6};
         f32x4 acc[1] = {zero4()};
         c2_acc(std::integral_constant<int, 1>{}, mts, acc);
-        c2_epi(6, acc[0]);
+        c2_epi(t, valid, 6, acc[0]);
       }
     }
     __syncthreads();
     if (t < 4) stamp(4 + 3 * t);
   }
   stamp(14);
-  if (cb.stamps && tid == 0 && blockIdx.x < 1024) cb.stamps[(STAMP_CONV_FWD - STAMP_CONV_BWD + blockIdx.x) * 16 + 15] = hw_location();
-  flush_p2(unit * ipb + ipb - 1);
+  if (cb.stamps && stamper && blockIdx.x < 1024) cb.stamps[(STAMP_CONV_FWD - STAMP_CONV_BWD + blockIdx.x) * 16 + 15] = hw_location();
+  flush_p2(first + ipb - 1);
+}
+
+template <typename T, bool TRAIN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void conv_fwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
+  __shared__ __attribute__((aligned(16))) char smem[FwdSmem<T>::TOTAL];
+  const int unit = xcd_unit(blockIdx.x, gridDim.x, br.xcd);  // this workgroup's images: [unit * ipb, +ipb)
+  conv_fwd_images<T, TRAIN>(br, cb, unit * ipb, ipb, smem, threadIdx.x, wave_id(), threadIdx.x == 0, nullptr);
+}
+
+// ====================================================================================
+// forward + FC head in ONE kernel (LeNet-5 training, large batches)
+// A 512-thread workgroup owns 16 consecutive batch rows = one 16-row MFMA tile of the head.  Its two
+// 4-wave halves each run the conv_fwd image loop over 8 of the rows (the same per-image code and LDS
+// layout as conv_fwd_kernel, so per CU the conv work keeps 16 waves in flight), writing pool2 straight
+// into the head's LDS input tile.  The 8 waves then run the whole head on the tile:
+//   L1 (wave w: n-tile w) -> L2 -> L3 -> softmax-CE + metrics -> dH2 -> dH1 -> dX (= pool2 grads)
+// B operands come straight from the L2-resident packed weights into registers, each phase's fragments
+// issued one or more phases ahead (a 16-row tile reads every weight fragment exactly once, so an LDS copy
+// would buy nothing).  This removes the head kernel, its kernel boundary, the pool2 HBM round trip and
+// the head's per-workgroup weight staging (replaces head_kernel's LeNet path at B >= FH_MIN_B; the FC
+// wgrad reads the same transposed activations / gradients the head wrote).
+// Reference: the forward/loss/backward of ddp_tutorial_multi_gpu.py:72-79 for the LeNet-5 model.
+constexpr int FH_MIN_B = 4096;
+template <typename T>
+struct FwdHeadSmem {
+  using H = LenetModel::Head;
+  static constexpr int PX = H::K0P + 8, P1 = H::N1P + 8, P2 = H::N2P + 8, PD = H::NCK + 8;
+  static constexpr int HALF = FwdSmem<T>::TOTAL;             // one conv image stream
+  static constexpr int OFF_X = 2 * HALF;                      // [16][PX] T   head input tile (pool2 rows)
+  static constexpr int TOTAL = rup(OFF_X + 16 * PX * (int)sizeof(T), 16);
+  // after the image loops the two conv regions are dead: the head's small tiles live there
+  static constexpr int OFF_H1 = 0;                                               // [16][P1] T
+  static constexpr int OFF_H2 = rup(OFF_H1 + 16 * P1 * (int)sizeof(T), 16);      // [16][P2] T
+  static constexpr int OFF_D = rup(OFF_H2 + 16 * P2 * (int)sizeof(T), 16);       // [16][PD] T  dZ
+  static constexpr int OFF_L = rup(OFF_D + 16 * PD * (int)sizeof(T), 16);        // [16][16] f32 logits
+  static constexpr int OFF_LAB = OFF_L + 16 * 16 * 4;                            // [16] int
+  static constexpr int OFF_PART = OFF_LAB + 16 * 4;                              // [8][4] f32
+  static constexpr int OFF_DX = rup(OFF_PART + 8 * 4 * 4, 16);                   // [16][PX] T dX tile
+  static constexpr int HEAD_END = OFF_DX + 16 * PX * (int)sizeof(T);
+  static_assert(HEAD_END <= 2 * HALF, "head tiles must fit in the dead conv regions");
+};
+
+template <typename T>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void fwd_head_kernel(BatchRef br, LenetConvBuffers cb,
+                                                                                           HeadBuffers hb) {
+  using H = LenetModel::Head;
+  using S = FwdHeadSmem<T>;
+  using M = Mma<T>;
+  using Frag = typename M::Frag;
+  constexpr int KV = M::KV, KC = M::KC;
+  static_assert(sizeof(T) == 2, "fwd_head_kernel: bf16 operand layout");
+  __shared__ __attribute__((aligned(16))) char smem[S::TOTAL];
+  T* sX = reinterpret_cast<T*>(smem + S::OFF_X);
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
+  const int half = w >> 2;  // wave-uniform (an SGPR: the image stream's addresses stay scalar)
+  const int r0 = xcd_unit(blockIdx.x, gridDim.x, br.xcd) * 16;  // this workgroup's batch rows [r0, r0 + 16)
+  const int B = br.B;
+  // the head tile's padding columns (400..415) must be zero: cleared once, before the loop's first barrier
+  for (int e = tid; e < 16 * S::PX * (int)sizeof(T) / 16; e += 512) reinterpret_cast<uint4*>(sX)[e] = make_uint4(0, 0, 0, 0);
+  conv_fwd_images<T, true, true, S::PX>(br, cb, r0 + 8 * half, 8, smem + half * S::HALF, tid & 255, w & 3, tid == 0,
+                                        sX + 8 * half * S::PX);
+  __syncthreads();  // every pool2 row of the tile is in sX; the conv regions are dead
+  // optional head-phase stamps (profiling; the head's own row range): [0] conv loops done, [9] X^T stored,
+  // [1] L1, [2] L2, [3] L3, [4] softmax, [5] dH2, [6] dH1, [7] dX, [8] end
+  auto hstamp = [&](int k) {
+    if (hb.stamps && tid == 0 && blockIdx.x < 1024) hb.stamps[blockIdx.x * 16 + k] = wall_clock64();
+  };
+  hstamp(0);
+
+  T* sH1 = reinterpret_cast<T*>(smem + S::OFF_H1);
+  T* sH2 = reinterpret_cast<T*>(smem + S::OFF_H2);
+  T* sD = reinterpret_cast<T*>(smem + S::OFF_D);
+  T* sDX = reinterpret_cast<T*>(smem + S::OFF_DX);
+  float* sLog = reinterpret_cast<float*>(smem + S::OFF_L);
+  int* sLab = reinterpret_cast<int*>(smem + S::OFF_LAB);
+  float* sPart = reinterpret_cast<float*>(smem + S::OFF_PART);
+  const T* pack = reinterpret_cast<const T*>(hb.pack);
+  const float* prm = hb.params;
+  const int ldB = hb.ldB;
+  constexpr int KCH1 = H::K0P / KC, KCH2 = H::N1P / KC, KCH3 = H::N2P / KC, KCHX = H::N1P / KC;
+  constexpr int NT2 = H::N2P / 16, NTX = H::K0 / 16, XJ = (NTX + 7) / 8;  // dX: tiles w + 8j
+  static_assert(H::N1P / 16 == 8, "one layer-1 n-tile per wave");
+
+  // ---- every B fragment of L1, L2, L3, dH2 and dH1 for this wave, issued now (L1's first: in-order
+  //      vmcnt lets L1 start while the rest is in flight); biases and labels with them
+  Frag b1[KCH1], b2[KCH2], b3[KCH3], bd2, bd1[KCH3];
+  {  // fragment-major W1 (models.h FM1): each fragment is one contiguous 1 KB (bf16) wave load
+    const T* p = pack + H::FM1 + (w * KCH1 * 64 + lane) * KV;
+#pragma unroll
+    for (int kc = 0; kc < KCH1; ++kc) b1[kc] = M::load(p + kc * 64 * KV);
+  }
+  const int w2 = min(w, NT2 - 1);  // waves 6, 7 have no L2 / dH2 tile: they load (and ignore) tile 5
+  {
+    const T* p = pack + H::F2 + (w2 * 16 + row) * H::N1P + grp * KV;
+#pragma unroll
+    for (int kc = 0; kc < KCH2; ++kc) b2[kc] = M::load(p + kc * KC);
+  }
+  bd2 = M::load(pack + H::F3T + (w2 * 16 + row) * H::NCK + grp * KV);
+  {
+    const T* p = pack + H::F2T + (w * 16 + row) * H::N2P + grp * KV;
+#pragma unroll
+    for (int kc = 0; kc < KCH3; ++kc) bd1[kc] = M::load(p + kc * KC);
+  }
+  const int n1 = w * 16 + row, n2 = w2 * 16 + row;
+  const float bias1 = prm[H::B1 + min(n1, H::N1 - 1)], bias2 = prm[H::B2 + min(n2, H::N2 - 1)];
+  const float bias3 = prm[H::B3 + min(row, H::NC - 1)];
+  if (tid >= 512 - 16) {  // labels of the tile (the last wave: its L2 tile is a dummy)
+    const int t = tid - (512 - 16), rg = r0 + t;
+    const int id = rg < B ? br.idx_epoch[(size_t)br.step_ptr[0] * br.batch_stride + rg] : -1;
+    sLab[t] = id >= 0 ? (int)br.labels[id] : 0;
+  }
+
+  // ---- X^T for the wgrad GEMM: item = (8-column chunk, 4-row quad), 4 rows read as 16-byte LDS chunks
+  //      and written as 4-row (8-byte) column stores
+  {
+    T* xT = reinterpret_cast<T*>(hb.xT);
+    constexpr int NCH = H::K0P / 8;
+    for (int e = tid; e < NCH * 4; e += 512) {
+      const int c = e >> 2, rq = (e & 3) * 4;
+      u32x4 v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const u32x4*>(sX + (rq + q) * S::PX + c * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int wd = j >> 1, sh = 16 * (j & 1);
+        const uint32_t lo = ((v[0][wd] >> sh) & 0xFFFFu) | (((v[1][wd] >> sh) & 0xFFFFu) << 16);
+        const uint32_t hi = ((v[2][wd] >> sh) & 0xFFFFu) | (((v[3][wd] >> sh) & 0xFFFFu) << 16);
+        *reinterpret_cast<u32x2*>(xT + (size_t)(c * 8 + j) * ldB + r0 + rq) = u32x2{lo, hi};
+      }
+    }
+  }
+  hstamp(9);
+  auto store4 = [&](T* base, const float* v) {  // 4 consecutive rows of one column of a [col][ldB] buffer
+    bf16x4 q;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) q[i] = (bf16)v[i];
+    *reinterpret_cast<bf16x4*>(base) = q;
+  };
+
+  // ---------------------------------------------------------------- L1: H1 = relu(X W1^T + b1)
+  {
+    f32x4 acc = zero4();
+    const T* ap = sX + row * S::PX + grp * KV;
+#pragma unroll
+    for (int kc = 0; kc < KCH1; ++kc) M::mma(acc, M::load(ap + kc * KC), b1[kc]);
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = grp * 4 + i;
+      float x = fmaxf(acc[i] + bias1, 0.f);
+      if (n1 >= H::N1 || r0 + r >= B) x = 0.f;
+      sH1[r * S::P1 + n1] = to_t<T>(x);
+      v[i] = to_f(to_t<T>(x));
+    }
+    store4(reinterpret_cast<T*>(hb.h1T) + (size_t)n1 * ldB + r0 + grp * 4, v);
+  }
+  {  // L3's fragments (used by wave 7 only) and the dX fragments (W1^T, the largest operand): issued now
+     // that L1's registers are free; they arrive during L2 .. dH1
+    const T* p = pack + H::F3 + row * H::N2P + grp * KV;
+#pragma unroll
+    for (int kc = 0; kc < KCH3; ++kc) b3[kc] = M::load(p + kc * KC);
+  }
+  Frag bx[XJ][KCHX];
+#pragma unroll
+  for (int j = 0; j < XJ; ++j) {
+    const int nt = min(w + 8 * j, NTX - 1);
+    const T* p = pack + H::FM1T + (nt * KCHX * 64 + lane) * KV;  // fragment-major W1^T (models.h FM1T)
+#pragma unroll
+    for (int kc = 0; kc < KCHX; ++kc) bx[j][kc] = M::load(p + kc * 64 * KV);
+  }
+  __syncthreads();
+  hstamp(1);
+
+  // ---------------------------------------------------------------- L2: H2 = relu(H1 W2^T + b2)
+  if (w < NT2) {
+    f32x4 acc = zero4();
+    const T* ap = sH1 + row * S::P1 + grp * KV;
+#pragma unroll
+    for (int kc = 0; kc < KCH2; ++kc) M::mma(acc, M::load(ap + kc * KC), b2[kc]);
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int r = grp * 4 + i;
+      float x = fmaxf(acc[i] + bias2, 0.f);
+      if (n2 >= H::N2 || r0 + r >= B) x = 0.f;
+      sH2[r * S::P2 + n2] = to_t<T>(x);
+      v[i] = to_f(to_t<T>(x));
+    }
+    store4(reinterpret_cast<T*>(hb.h2T) + (size_t)n2 * ldB + r0 + grp * 4, v);
+  }
+  __syncthreads();
+  hstamp(2);
+
+  // ---------------------------------------------------------------- L3: logits = H2 W3^T + b3
+  if (w == 7) {
+    f32x4 acc = zero4();
+    const T* ap = sH2 + row * S::P2 + grp * KV;
+#pragma unroll
+    for (int kc = 0; kc < KCH3; ++kc) M::mma(acc, M::load(ap + kc * KC), b3[kc]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) sLog[(grp * 4 + i) * 16 + row] = acc[i] + bias3;
+  }
+  __syncthreads();
+  hstamp(3);
+
+  // ---------------------------------------------------------------- softmax cross-entropy (waves 0-3)
+  if (tid < 256) {
+    const int r = tid >> 4, c = tid & 15, rg = r0 + r;
+    const bool valid = rg < B;
+    const float z = c < H::NC ? sLog[r * 16 + c] : -INFINITY;
+    const float mx = row16_max(z);
+    const int am = row16_min(z == mx ? c : 16);
+    const float e = c < H::NC ? __expf(z - mx) : 0.f;
+    const float se = row16_sum(e);
+    const int y = sLab[r];
+    const float zy = sLog[r * 16 + y];
+    float loss = 0.f, corr = 0.f, cnt = 0.f;
+    if (c == 0 && valid) {
+      loss = mx + __logf(se) - zy;
+      corr = (am == y) ? 1.f : 0.f;
+      cnt = 1.f;
+    }
+    const float d = (valid && c < H::NC) ? e / se - (c == y ? 1.f : 0.f) : 0.f;
+    sD[r * S::PD + c] = to_t<T>(d);
+    sD[r * S::PD + 16 + c] = to_t<T>(0.f);  // K padding of the dH2 product (NCK = 32)
+    auto rows4 = [](float v) { return (lane_f(v, 0) + lane_f(v, 16)) + (lane_f(v, 32) + lane_f(v, 48)); };
+    loss = rows4(loss);
+    corr = rows4(corr);
+    cnt = rows4(cnt);
+    if (lane == 0) {
+      sPart[w * 4 + 0] = loss;
+      sPart[w * 4 + 1] = corr;
+      sPart[w * 4 + 2] = cnt;
+    }
+  }
+  __syncthreads();
+  hstamp(4);
+
+  // ---------------------------------------------------------------- dH2 = (dZ W3) * [H2 > 0]
+  if (w < NT2) {
+    f32x4 acc = zero4();
+    M::mma(acc, M::load(sD + row * S::PD + grp * KV), bd2);
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      T* h = &sH2[(grp * 4 + i) * S::P2 + n2];
+      const float x = to_f(*h) > 0.f ? acc[i] : 0.f;
+      *h = to_t<T>(x);  // in place: H2 becomes dH2
+      v[i] = to_f(to_t<T>(x));
+    }
+    store4(reinterpret_cast<T*>(hb.dy2T) + (size_t)n2 * ldB + r0 + grp * 4, v);
+  } else {  // waves 6, 7: dZ^T for the wgrad GEMM
+    T* dy3T = reinterpret_cast<T*>(hb.dy3T);
+    const int e = tid - NT2 * 64, c = e >> 3, rq = (e & 7) * 2;  // 128 threads: (class, row pair)
+    dy3T[(size_t)c * ldB + r0 + rq] = sD[rq * S::PD + c];
+    dy3T[(size_t)c * ldB + r0 + rq + 1] = sD[(rq + 1) * S::PD + c];
+  }
+  __syncthreads();
+  hstamp(5);
+
+  // ---------------------------------------------------------------- dH1 = (dH2 W2) * [H1 > 0]
+  {
+    f32x4 acc = zero4();
+    const T* ap = sH2 + row * S::P2 + grp * KV;
+#pragma unroll
+    for (int kc = 0; kc < KCH3; ++kc) M::mma(acc, M::load(ap + kc * KC), bd1[kc]);
+    float v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      T* h = &sH1[(grp * 4 + i) * S::P1 + n1];
+      const float x = to_f(*h) > 0.f ? acc[i] : 0.f;
+      *h = to_t<T>(x);  // in place: H1 becomes dH1
+      v[i] = to_f(to_t<T>(x));
+    }
+    store4(reinterpret_cast<T*>(hb.dy1T) + (size_t)n1 * ldB + r0 + grp * 4, v);
+  }
+  __syncthreads();
+  hstamp(6);
+
+  // ---------------------------------------------------------------- dX = dH1 W1 -> pool2 grads
+  {
+    const T* ap = sH1 + row * S::P1 + grp * KV;
+    Frag a[KCHX];
+#pragma unroll
+    for (int kc = 0; kc < KCHX; ++kc) a[kc] = M::load(ap + kc * KC);
+#pragma unroll
+    for (int j = 0; j < XJ; ++j) {
+      const int nt = w + 8 * j;
+      if (nt >= NTX) break;
+      f32x4 acc = zero4();
+#pragma unroll
+      for (int kc = 0; kc < KCHX; ++kc) M::mma(acc, a[kc], bx[j][kc]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sDX[(grp * 4 + i) * S::PX + nt * 16 + row] = to_t<T>(acc[i]);
+    }
+  }
+  if (tid == 0) {  // tile metric totals -> this workgroup's own metrics row (summed on the host)
+    float a = 0.f, b = 0.f, c = 0.f;
+    for (int i = 0; i < 4; ++i) {
+      a += sPart[i * 4 + 0];
+      b += sPart[i * 4 + 1];
+      c += sPart[i * 4 + 2];
+    }
+    float* m = hb.metrics + (size_t)blockIdx.x * 4;
+    const f32x4 old = *reinterpret_cast<const f32x4*>(m);
+    *reinterpret_cast<f32x4*>(m) = f32x4{old[0] + a, old[1] + b, old[2] + c, 0.f};
+  }
+  __syncthreads();
+  hstamp(7);
+  {  // dX rows -> HBM as whole 16-byte chunks (400 columns = 50 chunks per row)
+    T* dx = reinterpret_cast<T*>(hb.dx);
+    for (int e = tid; e < 16 * 50; e += 512) {
+      const int r = e / 50, c = e - 50 * r;
+      if (r0 + r < B)
+        *reinterpret_cast<uint4*>(dx + (size_t)(r0 + r) * H::K0P + c * 8) = *reinterpret_cast<const uint4*>(sDX + r * S::PX + c * 8);
+    }
+  }
+  hstamp(8);
 }
 
 // ====================================================================================
 // backward
 // LDS images chosen so that every MFMA operand fragment is ONE aligned 16-byte read:
-//   XS  [5][32][32]     xs[kw][y][x]  = xpad[y][x+kw]          conv1 wgrad B (im2col^T rows)
+//   XS  [5][32][32]     xs[kw][y][x]  = xpad[y][x+kw]          conv1 wgrad B (im2col^T rows), + a ones plane
 //   P1T [5][6][14][16]  p1t[kw][c][y][x] = pool1[y][x+kw][c]   conv2 wgrad B
 //   DY2T[16][10*16]     conv2 pre-act grad, channel-major, rows padded 10->16   conv2 wgrad A
 //   DYS [18][18][16]    same grad, position-major (NHWC), zero border of 4 so the full-correlation
 //                       dgrad reads it without bounds checks                     conv2 dgrad A
 //   W2  [16][424]       packed conv2 dgrad operand (C2d)                         conv2 dgrad B
 //   DY1T[8][28*32]      conv1 pre-act grad, channel-major, rows padded 28->32    conv1 wgrad A
+//                       (zero prefix + >= one zero image row after each channel: the wgrad reads
+//                       rows y - 1 .. y + 1 of it, see phase C)
 // The pool1 un-pooling (argmax + ReLU) is fused into the conv2-dgrad epilogue, which writes DY1T
 // directly; pool2 un-pooling is a cooperative scatter.  Both scatters write every position of
 // their map (2x2 windows tile it), so nothing but the padding is ever zero-filled.
@@ -428,20 +755,26 @@ struct BwdSmem {
   // W2R: conv2 dgrad B operand for TWO output rows per tile, [16 = (r, c)][30 taps x 16 ch + pad]
   // (pitches from scripts/lds_model.py, a bank model of every LDS access of this kernel that matches
   //  the measured SQ_LDS_BANK_CONFLICT share: 38.5 % modelled vs 38.9 % measured at 488/1048/240/176/912)
-  static constexpr int W2P = 496, XP = 1040, P1P = 240, D2P = 168, D1P = 920;
-  // XS has 7 planes (5 shifted copies + an all-zero + an all-ones plane) and P1T 32 (30 + zero +
-  // ones): padding / bias-gradient columns read a constant plane instead of branching per lane
-  static constexpr int XPL = 7, PPL = 32;
+  // XP / D1P / ONES and the phase-C lane maps below: conflict-free A reads and 1.5-way B reads in the
+  // conv1 wgrad (scripts/lds_model.py C2 model; 616 -> 290 LDS cycles per image for that phase)
+  static constexpr int W2P = 496, XP = 1048, P1P = 240, D2P = 168, D1P = 944;
+  static constexpr int D1PRE = 32;  // zero elements before channel 0 of DY1T (row y - 1 of the first row)
+  // XS: 5 shifted planes, then an all-ones plane at ONES (bias-gradient column; its position sets the
+  // bank of that column); P1T has 32 planes (30 + zero + ones): padding / bias-gradient columns read a
+  // constant plane instead of branching per lane
+  static constexpr int ONES = 5 * XP + 120, ONES_N = 944;
+  static constexpr int XS_N = ONES + ONES_N, PPL = 32;
   static constexpr int OFF_XS = 0;
-  static constexpr int OFF_P1T = rup(OFF_XS + (HD ? XPL * XP * (int)sizeof(T) : 0), 16);
+  static constexpr int OFF_P1T = rup(OFF_XS + (HD ? XS_N * (int)sizeof(T) : 0), 16);
   static constexpr int OFF_DY2T = rup(OFF_P1T + (HW ? PPL * P1P * (int)sizeof(T) : 0), 16);
   static constexpr int OFF_DYS = rup(OFF_DY2T + (HW ? 16 * D2P * (int)sizeof(T) : 0), 16);  // [18][18][16] zero-padded
   static constexpr int OFF_W2 = rup(OFF_DYS + (HD ? 18 * 18 * 16 * (int)sizeof(T) : 0), 16);
   static constexpr int OFF_DY1T = rup(OFF_W2 + (HD ? 16 * W2P * (int)sizeof(T) : 0), 16);
-  static constexpr int OFF_M1 = rup(OFF_DY1T + (HD ? 8 * D1P * (int)sizeof(T) : 0), 16);  // [6][M1CP] u8 pool1 codes
+  static constexpr int OFF_M1 = rup(OFF_DY1T + (HD ? (D1PRE + 8 * D1P) * (int)sizeof(T) : 0), 16);  // [6][M1CP] u8 pool1 codes
   static constexpr int TOTAL = rup(OFF_M1 + (HD ? M1IMG : 0), 16);
-  static constexpr int OFF_RED = OFF_XS;  // [4][2][256] f32 scratch after the image loop (dgrad side)
-  static_assert(!HD || 4 * 2 * 256 * 4 <= XPL * XP * (int)sizeof(T), "reduction scratch must fit in the aliased XS region");
+  static constexpr int OFF_RED = OFF_XS;  // [4][256] f32 scratch after the image loop (dgrad side)
+  static_assert(!HD || 4 * 256 * 4 <= XS_N * (int)sizeof(T), "reduction scratch must fit in the aliased XS region");
+  static_assert(D1P >= 928 && 4 * XP + 4 * 32 + 928 <= ONES, "phase C reads stay inside zeroed rows");
 };
 
 template <typename T, int MODE>
@@ -457,7 +790,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   T* dy2t = reinterpret_cast<T*>(smem + S::OFF_DY2T);
   T* dys = reinterpret_cast<T*>(smem + S::OFF_DYS);
   T* w2 = reinterpret_cast<T*>(smem + S::OFF_W2);
-  T* dy1t = reinterpret_cast<T*>(smem + S::OFF_DY1T);
+  T* dy1t = reinterpret_cast<T*>(smem + S::OFF_DY1T) + S::D1PRE;  // channel 0 row 0
   uint8_t* m1s = reinterpret_cast<uint8_t*>(smem + S::OFF_M1);
   float* red = reinterpret_cast<float*>(smem + S::OFF_RED);
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
@@ -529,15 +862,14 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
 
   constexpr int W2CH = 160 / KC;              // conv2 wgrad: 10 rows x 16 positions
   constexpr int D2CH = 480 / KC;              // conv2 dgrad K = 30 taps (kh' = -1..4) x 16 ch (15 bf16 / 30 f32)
-  constexpr int W1CH = 896 / KC;              // conv1 wgrad: 28 rows x 32 positions (28 bf16 / 56 f32)
   // (measured: a register-resident dgrad B operand pushed the kernel to 245 VGPRs and made hipcc
   //  shuttle accumulators VGPR<->AGPR around every MFMA -- the B operand is read from LDS)
 
   // ---- once per workgroup: zero every padded image, stage C2d
   if constexpr (HD) {
-    zero_lds<T>(xs, 6 * S::XP);
-    for (int e = tid; e < S::XP; e += 256) xs[6 * S::XP + e] = to_t<T>(1.f);
-    zero_lds<T>(dy1t, 8 * S::D1P);
+    zero_lds<T>(xs, S::ONES);
+    for (int e = tid; e < S::ONES_N; e += 256) xs[S::ONES + e] = to_t<T>(1.f);
+    zero_lds<T>(dy1t - S::D1PRE, S::D1PRE + 8 * S::D1P);
     zero_lds<T>(dys, 18 * 18 * 16);
   }
   if constexpr (HW) {
@@ -576,13 +908,16 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     w2off[i] = kcol < 150 ? ((tap % 5) * 6 + c) * S::P1P + (tap / 5) * 16 : (kcol == 150 ? 31 : 30) * S::P1P;
     if (i >= nw) w2off[i] = 30 * S::P1P;  // no third tile on this wave: zero plane
   }
-  int w1off[2], w1sel[2];  // conv1 wgrad B: tiles over kcol = tap (25 = bias)
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    const int tap = nt * 16 + row;
-    w1sel[nt] = tap < 25 ? 0 : (tap == 25 ? 1 : 2);
-    w1off[nt] = tap < 25 ? (tap % 5) * S::XP + (tap / 5) * 32 : (tap == 25 ? 6 : 5) * S::XP;
-  }
+  // conv1 wgrad (phase C) as ONE 16x16 tile per image: M row m = (r, n) reads channel n of DY1T shifted
+  // back r image rows, N column j = (kernel-row base khb in {0, 2, 4}, kw) reads XS plane kw at row khb,
+  // so C[(r, n)][(khb, kw)] = dW1[n][khb + r][kw] (khb + r = 5: discarded) and column 15 (ones plane) is
+  // the bias gradient.  Was two tiles (M = 6 of 16 channels, N = 26 of 32 taps): 56 -> 29 MFMAs and
+  // 84 -> 58 fragment reads per image (bf16).  The row -> (r, n) and column -> (khb, kw) assignments
+  // are lane permutations chosen by the bank model (scripts/lds_model.py, C2).
+  constexpr uint8_t C_AMAP[16] = {8, 11, 0, 10, 4, 12, 5, 13, 15, 3, 2, 14, 9, 7, 6, 1};  // r * 8 + n
+  constexpr uint8_t C_BMAP[16] = {8, 9, 12, 4, 5, 15, 10, 13, 2, 14, 6, 11, 1, 7, 3, 0};  // (khb / 2) * 5 + kw | 15
+  const int c_aoff = (C_AMAP[row] & 7) * S::D1P - 32 * (C_AMAP[row] >> 3);
+  const int c_boff = C_BMAP[row] < 15 ? (C_BMAP[row] % 5) * S::XP + 2 * (C_BMAP[row] / 5) * 32 : S::ONES;
   const Frag ones = ones_frag<T>(), zf = M::zero();
   int doff[D2CH];  // conv2 dgrad A: -(tap row, col) shift of the lane's K-chunk inside the padded DYS
 #pragma unroll
@@ -594,11 +929,9 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     doff[kc] = (-khp * 18 - kw) * 16 + n0;
   }
 
-  f32x4 accW2[NWT], accW1[2];
+  f32x4 accW2[NWT], accW1 = zero4();
 #pragma unroll
   for (int i = 0; i < NWT; ++i) accW2[i] = zero4();
-  accW1[0] = zero4();
-  accW1[1] = zero4();
   wait_vm_all();  // loop-invariant loads done here (image 0's inputs, also in flight, are consumed next)
   __syncthreads();
   stamp(1);
@@ -869,30 +1202,26 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     __syncthreads();
     if (t < 4) stamp(3 + 3 * t);
 
-    // ---- phase C: conv1 wgrad  dW1[n][tap] += sum_pos dY1[pos][n] * xpad[pos + tap]
+    // ---- phase C: conv1 wgrad  dW1[n][kh][kw] += sum_pos dY1[pos][n] * xpad[pos + kh * 32 + kw]
+    //      K = positions 0..927 (28 image rows + the zero row 28 that row-shifted A rows need)
     if constexpr (HD) {
-      // chunks kc = w, w + 4, ... (W1CH / 4 per wave), straight-line with one chunk of prefetch
-      static_assert(W1CH % 4 == 0, "conv1 wgrad chunks split evenly over the 4 waves");
+      constexpr int CCH = 928 / KC, CPW = CCH / 4;  // chunks per wave: CPW, + 1 on waves < CCH % 4
       if (!(cb.ablate & 512)) {
-        auto ld_a = [&](int kc) { return M::load(dy1t + min(row, 7) * S::D1P + kc * KC + grp * KV); };  // rows 6..15: zero rows
-        auto ld_b = [&](int kc, int nt) {
-          const int p0 = kc * KC + grp * KV;
-          return M::load(xs + w1off[nt] + (p0 >> 5) * 32 + (p0 & 31));
-        };
-        Frag a = ld_a(w), b0 = ld_b(w, 0), b1 = ld_b(w, 1);
+        auto ld_a = [&](int kc) { return M::load(dy1t + c_aoff + kc * KC + grp * KV); };
+        auto ld_b = [&](int kc) { return M::load(xs + c_boff + kc * KC + grp * KV); };
+        Frag a = ld_a(w), b = ld_b(w);
 #pragma unroll
-        for (int j = 0; j < W1CH / 4; ++j) {
-          Frag an = a, bn0 = b0, bn1 = b1;
-          if (j + 1 < W1CH / 4) {
+        for (int j = 0; j < CPW; ++j) {
+          Frag an = a, bn = b;
+          if (j + 1 < CPW || w < CCH % 4) {
             const int kn = w + 4 * (j + 1);
             an = ld_a(kn);
-            bn0 = ld_b(kn, 0);
-            bn1 = ld_b(kn, 1);
+            bn = ld_b(kn);
           }
-          M::mma(accW1[0], a, b0);
-          M::mma(accW1[1], a, b1);
-          a = an; b0 = bn0; b1 = bn1;
+          M::mma(accW1, a, b);
+          a = an; b = bn;
         }
+        if (w < CCH % 4) M::mma(accW1, a, b);
       }
       __syncthreads();
       if (t < 4) stamp(4 + 3 * t);
@@ -915,17 +1244,19 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   }
   if constexpr (HD) {
 #pragma unroll
-    for (int nt = 0; nt < 2; ++nt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) red[(w * 2 + nt) * 256 + (grp * 4 + r) * 16 + row] = accW1[nt][r];
+    for (int i = 0; i < 4; ++i) red[w * 256 + (grp * 4 + i) * 16 + row] = accW1[i];
     __syncthreads();
-    for (int e = tid; e < 512; e += 256) {
-      const int nt = e >> 8, ix = e & 255, n = ix >> 4, kcol = nt * 16 + (ix & 15);
-      const float v = (red[(0 * 2 + nt) * 256 + ix] + red[(1 * 2 + nt) * 256 + ix]) +
-                      (red[(2 * 2 + nt) * 256 + ix] + red[(3 * 2 + nt) * 256 + ix]);
+    {
+      const int m = tid >> 4, j = tid & 15;  // C row m = (r, n), column j = (khb, kw) | bias
+      const float v = (red[0 * 256 + tid] + red[1 * 256 + tid]) + (red[2 * 256 + tid] + red[3 * 256 + tid]);
+      const int r = C_AMAP[m] >> 3, n = C_AMAP[m] & 7, bj = C_BMAP[j];
       if (n < 6) {
-        if (kcol < 25) out[L::CW1 + n * 25 + kcol] = v;
-        else if (kcol == 25) out[L::CB1 + n] = v;
+        if (bj == 15) {
+          if (r == 0) out[L::CB1 + n] = v;
+        } else {
+          const int kh = 2 * (bj / 5) + r, kw = bj % 5;
+          if (kh <= 4) out[L::CW1 + n * 25 + kh * 5 + kw] = v;
+        }
       }
     }
   }
@@ -973,6 +1304,21 @@ void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetC
     if (train) hipLaunchKernelGGL((conv_fwd_kernel<bf16, true>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
     else hipLaunchKernelGGL((conv_fwd_kernel<bf16, false>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
   }
+}
+
+bool lenet_fwd_head_applies(DType t, int B) {
+  static const int mode = [] {
+    const char* e = std::getenv("MNIST_AMD_FWD_HEAD");  // A/B knob: 0 = separate conv_fwd + head kernels
+    return e ? std::atoi(e) : 1;
+  }();
+  return mode != 0 && t == DType::BF16 && B >= FH_MIN_B && (B & 15) == 0;
+}
+
+int launch_lenet_fwd_head(DType t, const BatchRef& br, const LenetConvBuffers& cb, const HeadBuffers& hb, hipStream_t s) {
+  if (!lenet_fwd_head_applies(t, br.B)) return 0;
+  const int grid = br.B / 16;
+  hipLaunchKernelGGL(fwd_head_kernel<bf16>, dim3(grid), dim3(512), 0, s, br, cb, hb);
+  return 32;
 }
 
 void launch_lenet_conv_bwd(DType t, const BatchRef& br, const LenetConvBuffers& cb, int* nslab_out, hipStream_t s,

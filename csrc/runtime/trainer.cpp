@@ -216,12 +216,16 @@ void Trainer::forward_backward(int B, uintptr_t stream) {
   if (B <= 0 || B > batch_) throw std::invalid_argument("forward_backward: bad batch size");
   const BatchRef br = batch_ref(B);
   const HeadBuffers hb = head_buffers(ptr<float>(p_.metrics));
+  int hrows = 0;
   if (model_ == ModelKind::LENET) {
-    launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(), s);
+    if (fwd_head_active(B)) hrows = launch_lenet_fwd_head(dtype_, br, conv_buffers(), hb, s);
+    else launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(), s);
     post_launch(s);
   }
-  const int hrows = launch_head(model_, dtype_, true, br, hb, head_rows_per_block(model_, dtype_, batch_), s);
-  post_launch(s);
+  if (!hrows) {
+    hrows = launch_head(model_, dtype_, true, br, hb, head_rows_per_block(model_, dtype_, batch_), s);
+    post_launch(s);
+  }
   launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s, hrows);
   post_launch(s);
   if (model_ == ModelKind::LENET) {
@@ -289,19 +293,31 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
   const int cp = model_conv_params(model_);
   const bool comm = use_comm();
   last_stream_ = s;
+  // deferred join of the previous step's aux branch: the head overwrites the activations its FC wgrad
+  // read and reads the FC weights its FC update wrote (conv_fwd touches neither, so with separate
+  // kernels it runs without waiting: the join's cross-queue latency is off the conv_bwd -> conv update ->
+  // conv_fwd chain; the fused forward + head kernel contains the head, so it joins first)
+  auto join_aux = [&] {
+    if (aux_pending_) {
+      HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));
+      aux_pending_ = false;
+    }
+  };
+  int hrows = 0;
   if (model_ == ModelKind::LENET) {
-    launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(), s);
+    if (fwd_head_active(B)) {
+      join_aux();
+      hrows = launch_lenet_fwd_head(dtype_, br, conv_buffers(), hb, s);
+    } else {
+      launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(), s);
+    }
     post_launch(s);
   }
-  if (aux_pending_) {
-    // deferred join of the previous step's aux branch: the head overwrites the activations its FC wgrad
-    // read and reads the FC weights its FC update wrote (conv_fwd touches neither, so it ran without
-    // waiting: the join's cross-queue latency is off the conv_bwd -> conv update -> conv_fwd chain)
-    HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));
-    aux_pending_ = false;
+  join_aux();
+  if (!hrows) {
+    hrows = launch_head(model_, dtype_, true, br, hb, head_rows_per_block(model_, dtype_, batch_), s);
+    post_launch(s);
   }
-  const int hrows = launch_head(model_, dtype_, true, br, hb, head_rows_per_block(model_, dtype_, batch_), s);
-  post_launch(s);
 
   if (model_ == ModelKind::LENET && (comm || concurrent_)) {
     // fork: conv_bwd on the main stream (enqueued first, so its one-round grid is dispatched whole:
@@ -546,7 +562,7 @@ void Trainer::drop(GraphSlot& g) {
 // replays back to back; anything that changes the kernels' arguments clears the cache (invalidate).
 uint64_t Trainer::schedule_key(int nsteps) const {
   return (static_cast<uint64_t>(nsteps) << 40) | (static_cast<uint64_t>(bwd_blocks_) << 8) |
-         (static_cast<uint64_t>(comm_enabled_) << 3) | (static_cast<uint64_t>(concurrent_) << 2) |
+         (static_cast<uint64_t>(fwd_head_) << 4) | (static_cast<uint64_t>(comm_enabled_) << 3) | (static_cast<uint64_t>(concurrent_) << 2) |
          static_cast<uint64_t>(plan_);
 }
 

@@ -67,6 +67,11 @@ class Trainer {
   bool concurrent() const { return concurrent_; }
   // MLP, one GPU, one FC batch split: SGD as the wgrad kernel's epilogue (true) or wgrad + reduce_sgd
   void set_fuse_wgrad_sgd(bool on) { fuse_wgrad_sgd_ = on; invalidate(); }
+  // LeNet bf16 (large batches): conv_fwd + FC head as ONE kernel (fwd_head_kernel, true) or the two
+  // kernels (false).  Part of the graph-cache key, so a calibration can compare both.
+  void set_fwd_head(bool on) { fwd_head_ = on; }
+  bool fwd_head() const { return fwd_head_; }
+  bool fwd_head_active(int B) const { return model_ == ModelKind::LENET && fwd_head_ && lenet_fwd_head_applies(dtype_, B); }
   bool fuse_wgrad_sgd() const { return fuse_wgrad_sgd_; }
   // conv_bwd workgroup target (0 = default); the grid actually used for the full batch is bwd_grid()
   void set_bwd_blocks(int n) {
@@ -150,6 +155,7 @@ class Trainer {
   Plan plan_ = Plan::JOIN;
   bool concurrent_ = true;
   bool fuse_wgrad_sgd_ = true;
+  bool fwd_head_ = true;
   bool comm_enabled_ = true;
   hipStream_t last_stream_ = nullptr;  // stream of the last graph launch / capture (drained by invalidate)
   int bwd_blocks_ = 0;

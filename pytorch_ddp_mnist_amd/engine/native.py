@@ -227,6 +227,12 @@ class NativeTrainer:
         if self.model_name == "lenet5":
             self.rt.set_bwd_blocks(int(bwd_blocks))
 
+    def fwd_head_applies(self, B: Optional[int] = None) -> bool:
+        """LeNet bf16: a full step of B rows (default: the trainer batch) can run conv_fwd + the FC head as
+        ONE kernel (fwd_head_kernel); the installed schedule uses it unless ``fwd_head: False``."""
+        return self.model_name == "lenet5" and bool(self.C.fwd_head_applies(1 if self.dtype_name == "bf16" else 0,
+                                                                               int(B or self.batch)))
+
     @property
     def plan(self) -> str:
         return PLAN_NAMES[self.rt.plan]
@@ -292,15 +298,16 @@ class NativeTrainer:
     def current_schedule(self) -> dict:
         """The installed schedule as a complete :meth:`apply_plan` candidate."""
         return {"plan": self.plan, "bwd_blocks": int(self.rt.bwd_blocks) if self.model_name == "lenet5" else 0,
-                "concurrent": bool(self.rt.concurrent)}
+                "concurrent": bool(self.rt.concurrent), "fwd_head": bool(self.rt.fwd_head)}
 
     def apply_plan(self, cfg: dict) -> None:
-        """Install one candidate of :meth:`autotune_plan` ({plan, bwd_blocks, concurrent, comm}).  Keys a
-        candidate leaves out take their defaults (join, default conv_bwd grid, concurrent, comm on), so
-        a candidate names ONE cached graph whatever was installed before it.  ``comm: False`` (timing
-        only) runs the local schedule without collectives."""
+        """Install one candidate of :meth:`autotune_plan` ({plan, bwd_blocks, concurrent, fwd_head, comm}).
+        Keys a candidate leaves out take their defaults (join, default conv_bwd grid, concurrent, fused
+        forward + head kernel, comm on), so a candidate names ONE cached graph whatever was installed
+        before it.  ``comm: False`` (timing only) runs the local schedule without collectives."""
         self.rt.comm_enabled = bool(cfg.get("comm", True))
         self.rt.set_concurrent(bool(cfg.get("concurrent", True)))
+        self.rt.set_fwd_head(bool(cfg.get("fwd_head", True)))
         self.set_plan(cfg.get("plan", "join"), int(cfg.get("bwd_blocks", 0)))
 
     def time_schedules(self, candidates: Dict[str, dict], iters: int = 48, warmup: int = 8,
@@ -390,7 +397,7 @@ class NativeTrainer:
                 else:
                     candidates = mlp_plan_candidates()
             elif self.model_name == "lenet5":
-                candidates = local_plan_candidates()
+                candidates = local_plan_candidates(fwd_head=self.fwd_head_applies())
             else:
                 return {"chosen": "local", "timings_ms": {}}
         prefer = "join" if self.comm is not None else "concurrent"

@@ -81,10 +81,15 @@ def mlp_plan_candidates() -> Dict[str, dict]:
     return {"join": dict(plan="join"), "split": dict(plan="split")}
 
 
-def local_plan_candidates() -> Dict[str, dict]:
+def local_plan_candidates(fwd_head: bool = False) -> Dict[str, dict]:
     """Single-GPU LeNet schedules: the FC weight gradient + FC update on an aux stream beside
-    conv_bwd (``concurrent``, the default) or after it (``serial``)."""
-    return {"concurrent": dict(concurrent=True), "serial": dict(concurrent=False)}
+    conv_bwd (``concurrent``, the default) or after it (``serial``).  ``fwd_head`` (bf16, large
+    batches: the fused forward + FC head kernel applies): also the same schedule with the two separate
+    kernels (``separate``), so the calibration measures what the fusion is worth on this box."""
+    c = {"concurrent": dict(concurrent=True), "serial": dict(concurrent=False)}
+    if fwd_head:
+        c["separate"] = dict(concurrent=True, fwd_head=False)
+    return c
 
 
 def choose_plan(timings_ms: Dict[str, float], prefer: str = "join", margin: float = 0.015) -> str:

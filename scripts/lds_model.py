@@ -192,12 +192,28 @@ def model(P):
                 c, Y = row & 7, y0 + (row >> 3)
                 if c < 6:
                     rd[l] = OFF_M1 + (c * P["M1CP"] + Y * 16 if P.get("NEWA") else (c * 14 + Y) * 16) + grp * 4
-                    st0[l] = OFF_DY1T + T * (c * D1P + 2 * Y * D1R + grp * 8)
+                    st0[l] = OFF_DY1T + T * (P.get("PRE", 0) + c * D1P + 2 * Y * D1R + grp * 8)
                     st1[l] = st0[l] + T * D1R
             add("B2.m1s", "r32", rd)
             add("B2.dy1t", "w128", st0)
             add("B2.dy1t", "w128", st1)
         # ---- phase C: conv1 wgrad
+        if P.get("C2"):  # one tile: M = (r, n) rows (A shifted back r image rows), N = (khb, kw) + bias
+            for kc in range(w, 29, 4):
+                ad = {}
+                for l in range(64):
+                    row, grp = l & 15, l >> 4
+                    r, n = P["AMAP"][row]
+                    ad[l] = OFF_DY1T + T * (P["PRE"] + n * D1P + kc * 32 + grp * 8 - 32 * r)
+                add("C.dy1t", "r128", ad)
+                ad = {}
+                for l in range(64):
+                    row, grp = l & 15, l >> 4
+                    j = P["BMAP"][row]
+                    off = (j % 5) * XP + 2 * (j // 5) * XR if j < 15 else P["ONES"]
+                    ad[l] = OFF_XS + T * (off + kc * 32 + grp * 8)
+                add("C.xs", "r128", ad)
+            continue
         for kc in range(w, 28, 4):
             ad = {}
             for l in range(64):
@@ -219,9 +235,14 @@ def model(P):
 
 R1 = dict(XP=1048, P1P=240, D2P=176, D1P=912, W2P=488, XR=32, P1R=16, D2R=16, D1R=32, DYS_N=18 * 18 * 16,
           dys_idx=lambda oh, ow, n: ((oh + 4) * 18 + ow + 4) * 16 + n)
-CUR = dict(XP=1040, P1P=240, D2P=168, D1P=920, W2P=496, XR=32, P1R=16, D2R=16, D1R=32, DYS_N=18 * 18 * 16,
-           DENSE=1, NEWA=1, M1CP=240,
-           dys_idx=lambda oh, ow, n: ((oh + 4) * 18 + ow + 4) * 16 + n)
+PREV = dict(XP=1040, P1P=240, D2P=168, D1P=920, W2P=496, XR=32, P1R=16, D2R=16, D1R=32, DYS_N=18 * 18 * 16,
+            DENSE=1, NEWA=1, M1CP=240,
+            dys_idx=lambda oh, ow, n: ((oh + 4) * 18 + ow + 4) * 16 + n)
+# round 3: conv1 wgrad as one (r, n) x (khb, kw) tile (lenet.hip C_AMAP / C_BMAP; XS ones plane at ONES)
+AMAP_CODES = [8, 11, 0, 10, 4, 12, 5, 13, 15, 3, 2, 14, 9, 7, 6, 1]  # r * 8 + n
+CUR = dict(PREV, XP=1048, D1P=944, C2=1, PRE=32, ONES=5 * 1048 + 120,
+           AMAP=[(c >> 3, c & 7) for c in AMAP_CODES],
+           BMAP=[8, 9, 12, 4, 5, 15, 10, 13, 2, 14, 6, 11, 1, 7, 3, 0])
 
 
 def report(P, title=""):
@@ -241,6 +262,9 @@ if __name__ == "__main__":
     if "r1" in sys.argv[1:]:
         report(R1, "round-1 conv_bwd bf16")
         sys.argv.remove("r1")
+    if "prev" in sys.argv[1:]:
+        report(PREV, "round-2 conv_bwd bf16")
+        sys.argv.remove("prev")
     P = dict(CUR)
     for kv in sys.argv[1:]:
         k, v = kv.split("=")

@@ -46,9 +46,24 @@ def report(title, st, names, last):
     print(f"  {'total':16s} mean {tot.mean():7.2f} us  min {tot.min():7.2f}  max {tot.max():7.2f}")
 
 
-rows = 16 if B <= tr.C.L1_SPLIT_MAX_B else 64  # split path: 16-row tiles
+# head rows per workgroup (head.hip head_rows_per_block; the split path at small batches uses 16)
+if B <= tr.C.L1_SPLIT_MAX_B and model == "mlp" or B <= 256:
+    rows = 16
+elif dtype == "fp32" or model == "lenet5":
+    rows = 32
+else:
+    rows = 64 if B >= 4096 else 32
 nblk = (B + rows - 1) // rows
-if model == "lenet5":
+fused = tr.fwd_head_applies() and tr.rt.fwd_head
+if fused:  # fwd_head_kernel: 16-row workgroups; head rows hold the head phases after the conv loops
+    nblk = B // 16
+    st = allst[:nblk][:, [0, 9, 1, 2, 3, 4, 5, 6, 7, 8]]
+    report("fwd_head (head part)", st, ["X^T + L1 issue", "L1", "L2", "L3", "softmax", "dH2", "dH1", "dX", "dX store"], 9)
+    report("fwd_head (conv loops, half 0)", allst[2048:2048 + min(nblk, 1024)],
+           ["setup"] + [f"img{t} {p}" for t in range(4) for p in ("stage", "conv1", "conv2")], 14)
+    fw = allst[2048:2048 + nblk]
+    print(f"  conv loop start -> head end: {((allst[:nblk, 8] - fw[:, 0]) * 10 / 1000).mean():.2f} us mean")
+elif model == "lenet5":
     report("head", allst[:nblk], ["idx+stage X", "L1", "L2", "L3", "softmax", "dH2", "dH1", "dX"], 8)
     # inside the staging phase: [0] entry -> [9] loads issued -> [10] weights stored -> [11] X stored -> [1] barrier
     hs = allst[:nblk][:, [0, 9, 10, 11, 1]]
@@ -66,7 +81,7 @@ if model == "lenet5":
 else:  # no dX phase: stamp 7 is never written, dH1 ends at stamp 8
     allst[:nblk, 7] = allst[:nblk, 8]
     report("head", allst[:nblk], ["idx+stage X", "L1", "L2", "L3", "softmax", "dH2", "dH1"], 8)
-if model == "lenet5":
+if model == "lenet5" and not fused:
     per_img = []
     for t in range(4):
         per_img += [f"img{t} stage" if t == 0 else f"img{t} stage(+prev)", f"img{t} conv1", f"img{t} conv2"]

@@ -254,6 +254,39 @@ def test_fused_step_equals_phased(native, small_mnist, model_name, dtype):
     assert rel_err(a.grad.cpu(), b.grad.cpu()) < 1e-5
 
 
+def test_fwd_head_fused_equals_separate(native, small_mnist):
+    """LeNet bf16 at a large batch: the fused forward + FC head kernel (fwd_head_kernel) against the two
+    separate kernels (conv_fwd_kernel + head_kernel) -- gradients, metrics and 6 graph-replayed training
+    steps (incl. a 4-step graph with the deferred aux join).  Layer 1 of the head sums its K in a different
+    order in the two (the head kernel splits it over wave pairs), so agreement is to bf16 rounding."""
+    x, y, _, _ = small_mnist
+    torch.manual_seed(21)
+    module = build_model("lenet5")
+    B = 4096
+    a = make_trainer("lenet5", "bf16", B, x, y, module, momentum=0.9, lr=0.05, max_indices=8 * B)
+    b = make_trainer("lenet5", "bf16", B, x, y, module, momentum=0.9, lr=0.05, max_indices=8 * B)
+    assert a.fwd_head_applies() and a.rt.fwd_head
+    b.rt.set_fwd_head(False)
+    idx = torch.cat([torch.randperm(len(y), generator=torch.Generator().manual_seed(s)) for s in range(8)]).to(torch.int32)
+    for t in (a, b):
+        t.set_epoch_indices(idx)
+        t.reset_metrics()
+        t.forward_backward(B)
+    ga, gb = a.grads(), b.grads()
+    assert rel_err(ga, gb) < 5e-3, rel_err(ga, gb)
+    ma, mb = a.read_metrics(), b.read_metrics()
+    assert ma.count == mb.count == B
+    assert abs(ma.loss_sum - mb.loss_sum) / mb.loss_sum < 1e-3
+    assert abs(ma.correct - mb.correct) <= B // 200
+    for t in (a, b):
+        t.set_epoch_indices(idx)
+        t.step(B, use_graph=True)
+        t.step(B, use_graph=True)
+        t.run_steps(4, use_graph=True, k=4)
+        t.synchronize()
+    assert rel_err(a.params.cpu(), b.params.cpu()) < 2e-3, rel_err(a.params.cpu(), b.params.cpu())
+
+
 @pytest.mark.parametrize("model_name,dtype", [("mlp", "fp32"), ("mlp", "bf16"), ("lenet5", "fp32"), ("lenet5", "bf16")])
 def test_graph_replay_equals_eager(native, small_mnist, model_name, dtype):
     x, y, _, _ = small_mnist
