@@ -118,6 +118,10 @@ void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetC
 int launch_lenet_fwd_head(DType t, const BatchRef& br, const LenetConvBuffers& cb, const HeadBuffers& hb,
                           hipStream_t s);
 bool lenet_fwd_head_applies(DType t, int B);
+// LeNet training head alone as the 16-row register-B head (lenet.hip head16_kernel) on the pool2 rows of
+// conv_fwd: bf16, B <= MNIST_AMD_HEAD16 (default 2048).  Returns launch_head's rows value, or 0 when it
+// does not apply (the caller launches launch_head).
+int launch_lenet_head16(DType t, const BatchRef& br, const HeadBuffers& hb, hipStream_t s);
 // mode 0: full backward; 1: conv2 dgrad + conv1 wgrad half; 2: conv2 wgrad half (lenet.hip MODE)
 // target_blocks: workgroup count to aim for (0 = default, one full round of 2 blocks per CU); each
 // block walks ceil(B / target) images, so a smaller target leaves whole CUs free (for RCCL kernels).

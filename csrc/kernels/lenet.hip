@@ -430,14 +430,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void c
 // wgrad reads the same transposed activations / gradients the head wrote).
 // Reference: the forward/loss/backward of ddp_tutorial_multi_gpu.py:72-79 for the LeNet-5 model.
 constexpr int FH_MIN_B = 4096;
+// LDS of the 16-row register-B head (head16_tile): the input tile X, and the small per-phase tiles
 template <typename T>
-struct FwdHeadSmem {
+struct Head16Smem {
   using H = LenetModel::Head;
   static constexpr int PX = H::K0P + 8, P1 = H::N1P + 8, P2 = H::N2P + 8, PD = H::NCK + 8;
-  static constexpr int HALF = FwdSmem<T>::TOTAL;             // one conv image stream
-  static constexpr int OFF_X = 2 * HALF;                      // [16][PX] T   head input tile (pool2 rows)
-  static constexpr int TOTAL = rup(OFF_X + 16 * PX * (int)sizeof(T), 16);
-  // after the image loops the two conv regions are dead: the head's small tiles live there
+  static constexpr int X_BYTES = rup(16 * PX * (int)sizeof(T), 16);           // [16][PX] T input tile
   static constexpr int OFF_H1 = 0;                                               // [16][P1] T
   static constexpr int OFF_H2 = rup(OFF_H1 + 16 * P1 * (int)sizeof(T), 16);      // [16][P2] T
   static constexpr int OFF_D = rup(OFF_H2 + 16 * P2 * (int)sizeof(T), 16);       // [16][PD] T  dZ
@@ -445,9 +443,19 @@ struct FwdHeadSmem {
   static constexpr int OFF_LAB = OFF_L + 16 * 16 * 4;                            // [16] int
   static constexpr int OFF_PART = OFF_LAB + 16 * 4;                              // [8][4] f32
   static constexpr int OFF_DX = rup(OFF_PART + 8 * 4 * 4, 16);                   // [16][PX] T dX tile
-  static constexpr int HEAD_END = OFF_DX + 16 * PX * (int)sizeof(T);
-  static_assert(HEAD_END <= 2 * HALF, "head tiles must fit in the dead conv regions");
+  static constexpr int HEAD_END = rup(OFF_DX + 16 * PX * (int)sizeof(T), 16);
 };
+template <typename T>
+struct FwdHeadSmem : Head16Smem<T> {
+  static constexpr int HALF = FwdSmem<T>::TOTAL;  // one conv image stream
+  static constexpr int OFF_X = 2 * HALF;           // head input tile (pool2 rows)
+  static constexpr int TOTAL = OFF_X + Head16Smem<T>::X_BYTES;
+  // after the image loops the two conv regions are dead: the head's small tiles live there
+  static_assert(Head16Smem<T>::HEAD_END <= 2 * HALF, "head tiles must fit in the dead conv regions");
+};
+
+template <typename T>
+DEV void head16_tile(const BatchRef& br, const HeadBuffers& hb, char* ht, T* sX, int r0);
 
 template <typename T>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void fwd_head_kernel(BatchRef br, LenetConvBuffers cb,
@@ -469,20 +477,35 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
   conv_fwd_images<T, true, true, S::PX>(br, cb, r0 + 8 * half, 8, smem + half * S::HALF, tid & 255, w & 3, tid == 0,
                                         sX + 8 * half * S::PX);
   __syncthreads();  // every pool2 row of the tile is in sX; the conv regions are dead
-  // optional head-phase stamps (profiling; the head's own row range): [0] conv loops done, [9] X^T stored,
+  head16_tile<T>(br, hb, smem, sX, r0);
+}
+
+// The 16-row register-B head (fwd_head_kernel after its conv loops; head16_kernel): 8 waves, X in sX
+// (rows past the batch zero), the small per-phase tiles at `ht` (Head16Smem offsets).
+template <typename T>
+DEV void head16_tile(const BatchRef& br, const HeadBuffers& hb, char* ht, T* sX, int r0) {
+  using H = LenetModel::Head;
+  using S = Head16Smem<T>;
+  using M = Mma<T>;
+  using Frag = typename M::Frag;
+  constexpr int KV = M::KV, KC = M::KC;
+  static_assert(sizeof(T) == 2, "head16_tile: bf16 operand layout");
+  const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
+  const int B = br.B;
+  // optional head-phase stamps (profiling; the head's own row range): [0] X ready, [9] X^T stored,
   // [1] L1, [2] L2, [3] L3, [4] softmax, [5] dH2, [6] dH1, [7] dX, [8] end
   auto hstamp = [&](int k) {
     if (hb.stamps && tid == 0 && blockIdx.x < 1024) hb.stamps[blockIdx.x * 16 + k] = wall_clock64();
   };
   hstamp(0);
 
-  T* sH1 = reinterpret_cast<T*>(smem + S::OFF_H1);
-  T* sH2 = reinterpret_cast<T*>(smem + S::OFF_H2);
-  T* sD = reinterpret_cast<T*>(smem + S::OFF_D);
-  T* sDX = reinterpret_cast<T*>(smem + S::OFF_DX);
-  float* sLog = reinterpret_cast<float*>(smem + S::OFF_L);
-  int* sLab = reinterpret_cast<int*>(smem + S::OFF_LAB);
-  float* sPart = reinterpret_cast<float*>(smem + S::OFF_PART);
+  T* sH1 = reinterpret_cast<T*>(ht + S::OFF_H1);
+  T* sH2 = reinterpret_cast<T*>(ht + S::OFF_H2);
+  T* sD = reinterpret_cast<T*>(ht + S::OFF_D);
+  T* sDX = reinterpret_cast<T*>(ht + S::OFF_DX);
+  float* sLog = reinterpret_cast<float*>(ht + S::OFF_L);
+  int* sLab = reinterpret_cast<int*>(ht + S::OFF_LAB);
+  float* sPart = reinterpret_cast<float*>(ht + S::OFF_PART);
   const T* pack = reinterpret_cast<const T*>(hb.pack);
   const float* prm = hb.params;
   const int ldB = hb.ldB;
@@ -490,7 +513,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
   constexpr int NT2 = H::N2P / 16, NTX = H::K0 / 16, XJ = (NTX + 7) / 8;  // dX: tiles w + 8j
   static_assert(H::N1P / 16 == 8, "one layer-1 n-tile per wave");
 
-  // ---- every B fragment of L1, L2, L3, dH2 and dH1 for this wave, issued now (L1's first: in-order
+  // ---- the B fragments of L1, L2 and dH2 for this wave, issued now (L1's first: in-order
   //      vmcnt lets L1 start while the rest is in flight); biases and labels with them
   Frag b1[KCH1], b2[KCH2], b3[KCH3], bd2, bd1[KCH3];
   {  // fragment-major W1 (models.h FM1): each fragment is one contiguous 1 KB (bf16) wave load
@@ -505,11 +528,6 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
     for (int kc = 0; kc < KCH2; ++kc) b2[kc] = M::load(p + kc * KC);
   }
   bd2 = M::load(pack + H::F3T + (w2 * 16 + row) * H::NCK + grp * KV);
-  {
-    const T* p = pack + H::F2T + (w * 16 + row) * H::N2P + grp * KV;
-#pragma unroll
-    for (int kc = 0; kc < KCH3; ++kc) bd1[kc] = M::load(p + kc * KC);
-  }
   const int n1 = w * 16 + row, n2 = w2 * 16 + row;
   const float bias1 = prm[H::B1 + min(n1, H::N1 - 1)], bias2 = prm[H::B2 + min(n2, H::N2 - 1)];
   const float bias3 = prm[H::B3 + min(row, H::NC - 1)];
@@ -519,12 +537,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
     sLab[t] = id >= 0 ? (int)br.labels[id] : 0;
   }
 
-  // ---- X^T for the wgrad GEMM: item = (8-column chunk, 4-row quad), 4 rows read as 16-byte LDS chunks
-  //      and written as 4-row (8-byte) column stores
-  {
+  // ---- X^T for the wgrad GEMM (only the wgrad kernel reads it: stored by waves 4-7 while waves 0-3 run
+  //      the softmax): item = (8-column chunk, 4-row quad), 4 rows read as 16-byte LDS chunks and written
+  //      as 4-row (8-byte) column stores
+  auto store_xT = [&](int t0, int nth) {
     T* xT = reinterpret_cast<T*>(hb.xT);
     constexpr int NCH = H::K0P / 8;
-    for (int e = tid; e < NCH * 4; e += 512) {
+    for (int e = tid - t0; e < NCH * 4; e += nth) {
       const int c = e >> 2, rq = (e & 3) * 4;
       u32x4 v[4];
 #pragma unroll
@@ -537,7 +556,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
         *reinterpret_cast<u32x2*>(xT + (size_t)(c * 8 + j) * ldB + r0 + rq) = u32x2{lo, hi};
       }
     }
-  }
+  };
   hstamp(9);
   auto store4 = [&](T* base, const float* v) {  // 4 consecutive rows of one column of a [col][ldB] buffer
     bf16x4 q;
@@ -613,6 +632,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
   hstamp(3);
 
   // ---------------------------------------------------------------- softmax cross-entropy (waves 0-3)
+  {  // dH1's fragments (two phases ahead; issued here to keep L1..L3 under the register budget)
+    const T* p = pack + H::F2T + (w * 16 + row) * H::N2P + grp * KV;
+#pragma unroll
+    for (int kc = 0; kc < KCH3; ++kc) bd1[kc] = M::load(p + kc * KC);
+  }
   if (tid < 256) {
     const int r = tid >> 4, c = tid & 15, rg = r0 + r;
     const bool valid = rg < B;
@@ -641,6 +665,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
       sPart[w * 4 + 1] = corr;
       sPart[w * 4 + 2] = cnt;
     }
+  } else {
+    store_xT(256, 256);
   }
   __syncthreads();
   hstamp(4);
@@ -725,6 +751,27 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
     }
   }
   hstamp(8);
+}
+
+// LeNet bf16 head alone (the 16-row register-B head of fwd_head_kernel on pool2 rows from conv_fwd_kernel):
+// small batches, where the LDS-staged head_kernel spends most of its time staging weights for 8 tiles.
+template <typename T>
+__global__ __launch_bounds__(512) void head16_kernel(BatchRef br, HeadBuffers hb) {
+  using S = Head16Smem<T>;
+  using H = LenetModel::Head;
+  __shared__ __attribute__((aligned(16))) char smem[S::X_BYTES + S::HEAD_END];
+  T* sX = reinterpret_cast<T*>(smem);
+  const int tid = threadIdx.x;
+  const int r0 = xcd_unit(blockIdx.x, gridDim.x, br.xcd) * 16;
+  const T* xin = reinterpret_cast<const T*>(hb.xin);
+  constexpr int CH = H::K0P * (int)sizeof(T) / 16;  // 16-byte chunks per row (52)
+  for (int e = tid; e < 16 * CH; e += 512) {
+    const int r = e / CH, c = e - CH * r;
+    const uint4 v = r0 + r < br.B ? reinterpret_cast<const uint4*>(xin + (size_t)(r0 + r) * H::K0P)[c] : make_uint4(0, 0, 0, 0);
+    *reinterpret_cast<uint4*>(sX + r * S::PX + c * (16 / (int)sizeof(T))) = v;
+  }
+  __syncthreads();
+  head16_tile<T>(br, hb, smem + S::X_BYTES, sX, r0);
 }
 
 // ====================================================================================
@@ -1319,6 +1366,17 @@ int launch_lenet_fwd_head(DType t, const BatchRef& br, const LenetConvBuffers& c
   const int grid = br.B / 16;
   hipLaunchKernelGGL(fwd_head_kernel<bf16>, dim3(grid), dim3(512), 0, s, br, cb, hb);
   return 32;
+}
+
+int launch_lenet_head16(DType t, const BatchRef& br, const HeadBuffers& hb, hipStream_t s) {
+  static const int maxb = [] {
+    const char* e = std::getenv("MNIST_AMD_HEAD16");  // largest batch for head16_kernel (A/B knob; 0 = never)
+    return e ? std::atoi(e) : 2048;
+  }();
+  if (t != DType::BF16 || br.B <= 0 || br.B > maxb) return 0;
+  const int grid = (br.B + 15) / 16;
+  hipLaunchKernelGGL(head16_kernel<bf16>, dim3(grid), dim3(512), 0, s, br, hb);
+  return (grid % 8 == 0 && br.B % 32 == 0) ? 32 : 16;  // wgrad XCD mapping: as launch_lenet_fwd_head
 }
 
 void launch_lenet_conv_bwd(DType t, const BatchRef& br, const LenetConvBuffers& cb, int* nslab_out, hipStream_t s,

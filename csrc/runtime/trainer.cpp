@@ -223,7 +223,8 @@ void Trainer::forward_backward(int B, uintptr_t stream) {
     post_launch(s);
   }
   if (!hrows) {
-    hrows = launch_head(model_, dtype_, true, br, hb, head_rows_per_block(model_, dtype_, batch_), s);
+    if (model_ == ModelKind::LENET) hrows = launch_lenet_head16(dtype_, br, hb, s);
+    if (!hrows) hrows = launch_head(model_, dtype_, true, br, hb, head_rows_per_block(model_, dtype_, batch_), s);
     post_launch(s);
   }
   launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s, hrows);
@@ -315,7 +316,8 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
   }
   join_aux();
   if (!hrows) {
-    hrows = launch_head(model_, dtype_, true, br, hb, head_rows_per_block(model_, dtype_, batch_), s);
+    if (model_ == ModelKind::LENET) hrows = launch_lenet_head16(dtype_, br, hb, s);
+    if (!hrows) hrows = launch_head(model_, dtype_, true, br, hb, head_rows_per_block(model_, dtype_, batch_), s);
     post_launch(s);
   }
 

@@ -26,7 +26,9 @@ FLOP_PER_IMG = {
     "head": 2 * 2 * (400 * 120 + 120 * 84 + 84 * 10),
     "wgrad": 2 * (400 * 120 + 120 * 84 + 84 * 10),
     "conv_bwd": 2 * (16 * 100 * 150 * 2 + 6 * 784 * 25),
+    "head16": 2 * 2 * (400 * 120 + 120 * 84 + 84 * 10),
 }
+FLOP_PER_IMG["fwd_head"] = FLOP_PER_IMG["conv_fwd"] + FLOP_PER_IMG["head"]  # fused forward + FC head
 FLOP_PER_IMG_MLP = {  # reference MLP: head = forward + dgrad of layers 3, 2 (no input grad); wgrad = all three layers
     "head": 2 * (784 * 128 + 128 * 128 + 128 * 10) + 2 * (10 * 128 + 128 * 128),
     "wgrad": 2 * (784 * 128 + 128 * 128 + 128 * 10),
@@ -34,7 +36,7 @@ FLOP_PER_IMG_MLP = {  # reference MLP: head = forward + dgrad of layers 3, 2 (no
 
 
 def short(name: str) -> str:
-    for k in ("conv_fwd", "conv_bwd", "head_kernel", "wgrad", "reduce_sgd", "reduce_slabs", "sgd_pack"):
+    for k in ("fwd_head", "head16", "conv_fwd", "conv_bwd", "head_kernel", "wgrad", "reduce_sgd", "reduce_slabs", "sgd_pack"):
         if k in name:
             return k.replace("_kernel", "")
     return name[:24]

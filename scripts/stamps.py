@@ -49,10 +49,8 @@ def report(title, st, names, last):
 # head rows per workgroup (head.hip head_rows_per_block; the split path at small batches uses 16)
 if B <= tr.C.L1_SPLIT_MAX_B and model == "mlp" or B <= 256:
     rows = 16
-elif dtype == "fp32" or model == "lenet5":
-    rows = 32
 else:
-    rows = 64 if B >= 4096 else 32
+    rows = 32
 nblk = (B + rows - 1) // rows
 fused = tr.fwd_head_applies() and tr.rt.fwd_head
 if fused:  # fwd_head_kernel: 16-row workgroups; head rows hold the head phases after the conv loops
