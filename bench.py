@@ -238,7 +238,10 @@ def main(argv=None) -> int:
         tr.run_steps(n, use_graph=use_graph)  # k-step graphs (MNIST_AMD_GRAPH_STEPS), then single steps
 
     if use_graph:
-        tr.prepare_graphs()   # capture + instantiate the 1-step and k-step graphs before the clock
+        # capture + instantiate the 1-step and k-step graphs before the clock.  (A graph of the timed run's
+        # remainder -- 20 steps = 8 + 8 + one 4-step graph -- measured SLOWER than 4 single-step launches,
+        # 0.118-0.132 vs 0.110-0.113 ms/step even when the warm-up launched it first: not used.)
+        tr.prepare_graphs()
     tr.reset_metrics()
     run(a.warmup)
     elapsed = timed_region(ctx, tr, run, a.steps, lambda: torch.cuda.synchronize(dev))

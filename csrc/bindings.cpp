@@ -157,6 +157,9 @@ PYBIND11_MODULE(_C, m) {
       .def_property("fuse_wgrad_sgd", &Trainer::fuse_wgrad_sgd, &Trainer::set_fuse_wgrad_sgd)
       .def("capture_multi", &Trainer::capture_multi)
       .def("replay_multi", &Trainer::replay_multi)
+      .def("capture_n", &Trainer::capture_n)
+      .def("has_graph", &Trainer::has_graph)
+      .def("replay_n", &Trainer::replay_n)
       .def_property_readonly("multi_steps", &Trainer::multi_steps)
       .def("invalidate", &Trainer::invalidate)
       .def_property_readonly("captured", &Trainer::captured)

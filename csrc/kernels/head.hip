@@ -197,9 +197,9 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   auto prefetch_b1 = [&] {
     if constexpr (PF1) {
       if (l1_live) {
-        const T* bp = pack + H::F1 + (l1_nt * 16 + row) * H::K0P + grp * KV;
+        const T* bp = pack + H::FM1 + (l1_nt * KCH1 * 64 + lane) * KV;  // fragment-major W1 (models.h)
 #pragma unroll
-        for (int kc = 0; kc < KH1; ++kc) b1pre[kc] = M::load(bp + min(l1_k0 + kc, KCH1 - 1) * KC);
+        for (int kc = 0; kc < KH1; ++kc) b1pre[kc] = M::load(bp + min(l1_k0 + kc, KCH1 - 1) * 64 * KV);
       }
     }
   };
@@ -207,10 +207,12 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   //  fragments issued first would make the gather's conversion wait for all of W1)
   if constexpr (!H::GATHER) prefetch_b1();
 
-  // ---- look-ahead (small-batch MLP training): this step's labels come from ynext (gathered by the
-  //      previous step), and this kernel gathers the NEXT step's rows of its tile into xnext / ynext
-  //      (consumed by the next l1_split / head; this step's l1_split has already read xnext)
-  constexpr bool LOOK = PRE && H::GATHER && TRAIN;
+  // ---- look-ahead (MLP training): this step's pixels / labels come from xnext / ynext (gathered by the
+  //      previous step, in batch-row order), and this kernel gathers the NEXT step's rows of its tile into
+  //      xnext / ynext (consumed by the next l1_split / head; this step's l1_split -- small batches -- has
+  //      already read xnext, and without it this kernel read its own rows during the staging: a workgroup
+  //      only ever touches its own rows)
+  constexpr bool LOOK = H::GATHER && TRAIN;
   const bool look = LOOK && br.xnext != nullptr;  // uniform
   constexpr int GCH = R * 49, GIT2 = LOOK ? (GCH + NTH - 1) / NTH : 1;  // 16-byte chunks of the tile's rows
   int gidx[GIT2];
@@ -320,8 +322,9 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       const int e = min(tid + i * NTH, NGI - 1), r = (e % (R / 4)) * 4, c = e / (R / 4);
 #pragma unroll
       for (int q = 0; q < 4; ++q) {  // branch-free: padding chunks / rows past the batch read row 0, zeroed at use
-        const int sidx = sIdx[r + q];
-        px[i][q] = *reinterpret_cast<const u32x4*>(br.images + (size_t)max(sidx, 0) * 784 + min(c, H::K0 / 16 - 1) * 16);
+        // (look-ahead: the tile's own rows of xnext, contiguous; else the dataset rows by sample index)
+        const uint8_t* src = look ? br.xnext + (size_t)(r0 + r + q) * 784 : br.images + (size_t)max(sIdx[r + q], 0) * 784;
+        px[i][q] = *reinterpret_cast<const u32x4*>(src + min(c, H::K0 / 16 - 1) * 16);
       }
     }
     // pinned order: pixel loads, then the W1 prefetch, then the conversion (which then waits for the
@@ -342,7 +345,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
         u32x4 pk[4][2];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const bool live = sIdx[r + q] >= 0 && c < H::K0 / 16;
+          const bool live = (look ? r0 + r + q < B : sIdx[r + q] >= 0) && c < H::K0 / 16;
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             bf16x8 f;
@@ -355,7 +358,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
             if (item) *reinterpret_cast<u32x4*>(sX + (r + q) * S::PX + c * 16 + h * 8) = pk[q][h];
           }
         }
-        if (TRAIN && item) {
+        if (TRAIN && item && !(hb.ablate & 1)) {
 #pragma unroll
           for (int j = 0; j < 16; ++j) {
             const int h = j >> 3, wd = (j & 7) >> 1, sh = 16 * (j & 1);
@@ -370,7 +373,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
           float v[4][4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const bool live = sIdx[r + q] >= 0 && c < H::K0 / 16;
+            const bool live = (look ? r0 + r + q < B : sIdx[r + q] >= 0) && c < H::K0 / 16;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const float nv = mnist_norm((px[i][q][(j0 + j) >> 2] >> (8 * ((j0 + j) & 3))) & 255u);
@@ -490,12 +493,12 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
 #pragma unroll
       for (int m = 0; m < MT; ++m) acc[m] = zero4();
       if (live) {
-        const T* bp = pack + H::F1 + (nt * 16 + row) * H::K0P + grp * KV;
+        const T* bp = pack + H::FM1 + (nt * KCH1 * 64 + lane) * KV;  // fragment-major W1 (models.h)
 #pragma unroll
         for (int kk = 0; kk < KH1; ++kk) {
           const int kc = l1_k0 + kk;
           if (kc >= l1_k1) break;  // wave-uniform (second half of an odd chunk count)
-          const Frag b = (PF1 && j == 0) ? b1pre[PF1 ? kk : 0] : M::load(bp + kc * KC);
+          const Frag b = (PF1 && j == 0) ? b1pre[PF1 ? kk : 0] : M::load(bp + kc * 64 * KV);
 #pragma unroll
           for (int m = 0; m < MT; ++m) M::mma(acc[m], M::load(ap + m * 16 * S::PX + kc * KC), b);
         }
@@ -854,10 +857,10 @@ __global__ __launch_bounds__(256) void l1_split_kernel(BatchRef br, HeadBuffers 
   const int nt = ng * 4 + w;
   const bool has_nt = nt * 16 < H::N1P;  // wave-uniform
   const T* pack = reinterpret_cast<const T*>(hb.pack);
-  const T* bp = pack + H::F1 + (size_t)(min(nt, H::N1P / 16 - 1) * 16 + row) * H::K0P + grp * KV;
+  const T* bp = pack + H::FM1 + ((size_t)min(nt, H::N1P / 16 - 1) * KCH * 64 + lane) * KV;  // fragment-major W1
   Frag bpre[QCH];
 #pragma unroll
-  for (int i = 0; i < QCH; ++i) bpre[i] = M::load(bp + min(c0 + i, KCH - 1) * KC);  // clamped: unused past c1
+  for (int i = 0; i < QCH; ++i) bpre[i] = M::load(bp + (size_t)min(c0 + i, KCH - 1) * 64 * KV);  // clamped: unused past c1
 
   // MLP gather: a thread's row is tid & 15 in every iteration, so its sample index is loaded ONCE and
   // every pixel load of the thread is issued before the first conversion (one idx -> pixels latency

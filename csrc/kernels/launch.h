@@ -50,6 +50,7 @@ struct HeadBuffers {
   uint32_t seed;
   float drop_p;
   int32_t xcd = 0;       // the head kernel used the XCD-contiguous row mapping (BatchRef::xcd)
+  int32_t ablate = 0;    // diagnostics only (MNIST_AMD_HEAD_ABLATE): bit 0 = skip the X^T stores (wrong wgrad)
 };
 
 struct LenetConvBuffers {

@@ -476,12 +476,14 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void f
   for (int e = tid; e < 16 * S::PX * (int)sizeof(T) / 16; e += 512) reinterpret_cast<uint4*>(sX)[e] = make_uint4(0, 0, 0, 0);
   conv_fwd_images<T, true, true, S::PX>(br, cb, r0 + 8 * half, 8, smem + half * S::HALF, tid & 255, w & 3, tid == 0,
                                         sX + 8 * half * S::PX);
-  __syncthreads();  // every pool2 row of the tile is in sX; the conv regions are dead
-  head16_tile<T>(br, hb, smem, sX, r0);
+  head16_tile<T>(br, hb, smem, sX, r0);  // its first barrier: every pool2 row is in sX, the conv regions dead
 }
 
 // The 16-row register-B head (fwd_head_kernel after its conv loops; head16_kernel): 8 waves, X in sX
-// (rows past the batch zero), the small per-phase tiles at `ht` (Head16Smem offsets).
+// (rows past the batch zero), the small per-phase tiles at `ht` (Head16Smem offsets).  The caller does NOT
+// barrier after writing sX: the first weight fragments are issued, THEN the block barrier (their latency
+// overlaps the wait for the slowest wave), and only then is LDS at `ht` written (it may alias the caller's
+// dead buffers).
 template <typename T>
 DEV void head16_tile(const BatchRef& br, const HeadBuffers& hb, char* ht, T* sX, int r0) {
   using H = LenetModel::Head;
@@ -497,7 +499,6 @@ DEV void head16_tile(const BatchRef& br, const HeadBuffers& hb, char* ht, T* sX,
   auto hstamp = [&](int k) {
     if (hb.stamps && tid == 0 && blockIdx.x < 1024) hb.stamps[blockIdx.x * 16 + k] = wall_clock64();
   };
-  hstamp(0);
 
   T* sH1 = reinterpret_cast<T*>(ht + S::OFF_H1);
   T* sH2 = reinterpret_cast<T*>(ht + S::OFF_H2);
@@ -531,11 +532,19 @@ DEV void head16_tile(const BatchRef& br, const HeadBuffers& hb, char* ht, T* sX,
   const int n1 = w * 16 + row, n2 = w2 * 16 + row;
   const float bias1 = prm[H::B1 + min(n1, H::N1 - 1)], bias2 = prm[H::B2 + min(n2, H::N2 - 1)];
   const float bias3 = prm[H::B3 + min(row, H::NC - 1)];
+  int lab = 0;
   if (tid >= 512 - 16) {  // labels of the tile (the last wave: its L2 tile is a dummy)
     const int t = tid - (512 - 16), rg = r0 + t;
     const int id = rg < B ? br.idx_epoch[(size_t)br.step_ptr[0] * br.batch_stride + rg] : -1;
-    sLab[t] = id >= 0 ? (int)br.labels[id] : 0;
+    lab = id >= 0 ? (int)br.labels[id] : 0;
   }
+  // sX complete (caller), `ht` free: a raw barrier after the LDS writes drained -- __syncthreads() would also
+  // wait (vmcnt(0)) for the weight fragments just issued
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  hstamp(0);
+  if (tid >= 512 - 16) sLab[tid - (512 - 16)] = lab;
 
   // ---- X^T for the wgrad GEMM (only the wgrad kernel reads it: stored by waves 4-7 while waves 0-3 run
   //      the softmax): item = (8-column chunk, 4-row quad), 4 rows read as 16-byte LDS chunks and written
@@ -770,8 +779,7 @@ __global__ __launch_bounds__(512) void head16_kernel(BatchRef br, HeadBuffers hb
     const uint4 v = r0 + r < br.B ? reinterpret_cast<const uint4*>(xin + (size_t)(r0 + r) * H::K0P)[c] : make_uint4(0, 0, 0, 0);
     *reinterpret_cast<uint4*>(sX + r * S::PX + c * (16 / (int)sizeof(T))) = v;
   }
-  __syncthreads();
-  head16_tile<T>(br, hb, smem + S::X_BYTES, sX, r0);
+  head16_tile<T>(br, hb, smem + S::X_BYTES, sX, r0);  // barriers before reading sX
 }
 
 // ====================================================================================

@@ -40,14 +40,15 @@ struct HeadDims {
   static constexpr int F2T = F2 + N2P * N1P;
   static constexpr int F3 = F2T + N1P * N2P;
   static constexpr int F3T = F3 + NCP * N2P;
-  // DX models (LeNet): W1 and W1^T also in FRAGMENT-MAJOR order for fwd_head_kernel (lenet.hip): the
-  // B fragment of (n-tile t, K-chunk c) is 64 lanes x KV contiguous elements, so one wave load reads
-  // whole cache lines (the row-major images touch 16 half-used lines per fragment)
+  // W1 (and, DX models, W1^T) also in FRAGMENT-MAJOR order for the layer-1 / dX products of the head
+  // kernels (head.hip, lenet.hip): the B fragment of (n-tile t, K-chunk c) is 64 lanes x KV contiguous
+  // elements, so one wave load reads whole cache lines (the row-major images touch 16 half-used lines
+  // per fragment; fwd_head_kernel layer 1: 5.6 -> 3.2 us)
   //   FM1 [N1P/16][K0P/KC][64][KV]: lane (g, r) of fragment (t, c) = W1[16t + r][c*KC + g*KV .. +KV)
   //   FM1T[K0R/16][N1P/KC][64][KV]: lane (g, r) of fragment (t, c) = W1[c*KC + g*KV .. +KV)[16t + r]
   static constexpr int K0R = rup(K0, 16);
   static constexpr int FM1 = F3T + N2P * NCK;
-  static constexpr int FM1T = FM1 + (DX ? N1P * K0P : 0);
+  static constexpr int FM1T = FM1 + N1P * K0P;
   static constexpr int PACK_END = FM1T + (DX ? K0R * N1P : 0);
 };
 
@@ -82,11 +83,11 @@ DEV void pack_head_param(int p, float v, T* pack) {
   if (p >= H::W1 && p < H::B1) {
     int q = p - H::W1, n = q / H::K0, k = q % H::K0;
     pack[H::F1 + n * H::K0P + k] = to_t<T>(v);
+    constexpr int KV = Mma<T>::KV, KC = Mma<T>::KC;
+    const int kk = k % KC, nn = n % KC;
+    pack[H::FM1 + (((n >> 4) * (H::K0P / KC) + k / KC) * 64 + (kk / KV) * 16 + (n & 15)) * KV + kk % KV] = to_t<T>(v);
     if (H::DX) {
       pack[H::F1T + k * H::N1P + n] = to_t<T>(v);
-      constexpr int KV = Mma<T>::KV, KC = Mma<T>::KC;
-      const int kk = k % KC, nn = n % KC;
-      pack[H::FM1 + (((n >> 4) * (H::K0P / KC) + k / KC) * 64 + (kk / KV) * 16 + (n & 15)) * KV + kk % KV] = to_t<T>(v);
       pack[H::FM1T + (((k >> 4) * (H::N1P / KC) + n / KC) * 64 + (nn / KV) * 16 + (k & 15)) * KV + nn % KV] = to_t<T>(v);
     }
   } else if (p >= H::W2 && p < H::B2) {

@@ -183,6 +183,11 @@ HeadBuffers Trainer::head_buffers(float* metrics) const {
   hb.seed = seed_;
   hb.drop_p = drop_p_;
   hb.xcd = xcd_map();
+  static const int head_ablate = [] {
+    const char* e = std::getenv("MNIST_AMD_HEAD_ABLATE");
+    return e ? std::atoi(e) : 0;
+  }();
+  hb.ablate = head_ablate;
   return hb;
 }
 
@@ -590,6 +595,24 @@ void Trainer::capture_multi(uintptr_t stream, int k) {
   drop(g);
   capture_into(S(stream), k, &g.graph, &g.exec);
   multi_k_ = k;
+}
+
+void Trainer::capture_n(uintptr_t stream, int n) {
+  if (n < 2) throw std::invalid_argument("capture_n: n must be >= 2");
+  GraphSlot& g = graphs_[schedule_key(n)];
+  if (g.exec) HIP_CHECK(hipStreamSynchronize(S(stream)));
+  drop(g);
+  capture_into(S(stream), n, &g.graph, &g.exec);
+}
+
+bool Trainer::has_graph(int n) const { return find_graph(n) != nullptr; }
+
+void Trainer::replay_n(uintptr_t stream, int n) {
+  const GraphSlot* g = find_graph(n);
+  if (!g) throw std::runtime_error("replay_n: no captured graph of that many steps for the current schedule");
+  last_stream_ = S(stream);
+  HIP_CHECK(hipGraphLaunch(g->exec, S(stream)));
+  if (sync_debug()) HIP_CHECK(hipStreamSynchronize(S(stream)));
 }
 
 int Trainer::multi_steps() const { return multi_k_ > 1 && find_graph(multi_k_) ? multi_k_ : 0; }

@@ -113,6 +113,11 @@ class Trainer {
   void capture_multi(uintptr_t stream, int k);
   void replay_multi(uintptr_t stream);
   int multi_steps() const;  // k of the multi-step graph of the current schedule, 0 if none
+  // graphs of n consecutive steps besides the k-step one (a run's remainder: 20 steps = 8 + 8 + 4), cached
+  // per schedule like the others; multi_steps() is not changed
+  void capture_n(uintptr_t stream, int n);
+  bool has_graph(int n) const;
+  void replay_n(uintptr_t stream, int n);
   void invalidate();        // drop every cached graph
 
   int nparam() const { return nparam_; }

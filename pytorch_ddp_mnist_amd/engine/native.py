@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import math
 import os
+import sys
 import time
 from dataclasses import dataclass
 from typing import Dict, Optional, Tuple
@@ -57,6 +58,10 @@ def forced_plan() -> Optional[str]:
         raise ValueError(f"MNIST_AMD_MG_SCHED={v!r}: expected one of {sorted(PLANS)}")
     return v
 PLAN_NAMES = {v: k for k, v in PLANS.items()}
+
+
+# single-GPU LeNet batches up to this size use the serial schedule without calibration (autotune_plan)
+SMALL_BATCH_SERIAL = int(os.environ.get("MNIST_AMD_SMALL_SERIAL", "1024"))
 
 
 class CollectiveError(RuntimeError):
@@ -151,11 +156,13 @@ class NativeTrainer:
             self.p1 = self.m1 = self.p2 = self.m2 = self.dp2 = None
         # layer-1 K-split partials for the small-batch path (csrc/kernels/head.hip l1_split_kernel)
         self.z1p = z(C.L1_KSPLIT * N1P * self.ld_b, dt=torch.float32) if self.batch <= C.L1_SPLIT_MAX_B else None
-        # small-batch MLP: the next step's pixels / labels, gathered one step ahead by the head kernel
-        # (rows padded to the 16-row tiles that read them)
+        # small-batch MLP: the next step's pixels / labels, gathered one step ahead by the head kernel (rows
+        # padded to the tiles that read them).  (At B=8192 the same look-ahead -- the head kernel supports
+        # it at every tile size -- measured no gain: 35.4-35.6 vs 35.2-35.8 us per step, same box; the
+        # staging phase is not bound by the random dataset rows.)
         look = model == "mlp" and self.z1p is not None and not os.environ.get("MNIST_AMD_NO_LOOKAHEAD")
-        self.xnext = z(_rup(self.batch, 32) * 784, dt=torch.uint8) if look else None
-        self.ynext = z(_rup(self.batch, 32), dt=torch.uint8) if look else None
+        self.xnext = z(_rup(self.batch, 64) * 784, dt=torch.uint8) if look else None
+        self.ynext = z(_rup(self.batch, 64), dt=torch.uint8) if look else None
 
         P = C.TrainerPtrs()
         ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
@@ -311,21 +318,32 @@ class NativeTrainer:
         self.set_plan(cfg.get("plan", "join"), int(cfg.get("bwd_blocks", 0)))
 
     def time_schedules(self, candidates: Dict[str, dict], iters: int = 48, warmup: int = 8,
-                       reduce_max=None) -> Dict[str, float]:
+                       reduce_max=None, multi: Optional[bool] = None) -> Dict[str, float]:
         """Median step time (ms) of each candidate schedule, state restored afterwards.
 
         Every candidate's step graph (and its k-step graph) is captured first -- graphs are cached
-        per schedule -- and then the candidates' replays are INTERLEAVED round-robin (rotating the
-        order each round) with no host sync in between: the GPU clock ramps up during the first
-        milliseconds of work, and timing candidate A entirely before candidate B would hand B the
-        faster clock.  Each replay trains on batch 0 of the loaded epoch order (the device step
-        counter is rewound), so all ranks issue the same collectives in the same order; per-replay
-        GPU times come from events on the step stream and ``reduce_max`` (e.g. a gloo MAX
-        all-reduce) makes the result identical on every rank.  Parameters, momentum, gradients,
+        per schedule.  What is timed is what training replays: blocks of k-step graph replays
+        (``multi``, when the loaded order holds k + 1 batches; per-step time = block time / steps),
+        else single-step replays.  Each candidate runs in segments of consecutive samples: one
+        untimed round over all candidates, then two timed rounds, the second in reverse order (the
+        GPU clock ramps up during the first milliseconds of work; the reverse round hands no
+        candidate the faster clock), with no host sync in between.  Replays train on consecutive
+        batches of the loaded epoch order from batch 0, the device step counter rewound when the
+        order runs out, identically on every rank, so all ranks issue the same collectives in the
+        same order; GPU times come from events on the step stream and ``reduce_max`` (e.g. a gloo
+        MAX all-reduce) makes the result identical on every rank.  Parameters, momentum, gradients,
         counters and metrics are restored afterwards (the operand images are re-packed); the
-        schedule installed before the call is re-installed."""
+        schedule installed before the call is re-installed.  ``iters`` / ``warmup`` are accepted
+        for API compatibility (the segment plan fixes the sample counts)."""
         if getattr(self, "n_epoch", 0) < max(2, self.host_step + 1) * self.batch:
             raise RuntimeError("time_schedules: the loaded epoch order needs >= 2 full batches beyond the current step")
+        # time what training replays: the k-step graph (run_steps) when the loaded order holds k + 1 batches
+        # (per-replay time / k).  Single-step replays ranked the LeNet B=128 schedules the wrong way round:
+        # concurrent 0.0485 vs serial 0.0490 ms, but 35.4 vs 33.0 us per step in 8-step graphs.
+        k = self.graph_steps()
+        can = k > 1 and self.ext_allreduce is None and getattr(self, "n_epoch", 0) >= (k + 1) * self.batch
+        multi = can if multi is None else (bool(multi) and can)
+        self.last_timing = {"graph_steps": k if multi else 1, "replays": 2 * (3 if multi else 11) * (4 if multi else 1)}
         before = self.current_schedule()
         self.synchronize()
         saved = [t.clone() for t in (self.params, self.mom, self.grad, self.step_ctr, self.metrics)]
@@ -335,31 +353,59 @@ class NativeTrainer:
         for name in names:                 # all captures (host work) before any timed replay
             self.apply_plan(candidates[name])
             self.prepare_graphs()
+            if multi and self.rt.multi_steps != k:
+                self.rt.capture_multi(st.cuda_stream, k)
         ev = {name: [] for name in names}
         with torch.cuda.stream(st):
             self.step_ctr[0].zero_()       # every replay trains on batch 0 of the loaded order
-        for r in range(warmup + iters):
-            order = names[r % len(names):] + names[:r % len(names)]
+        # Each candidate runs in SEGMENTS of consecutive samples (the first sample of a segment untimed), in
+        # one untimed round and two timed rounds, the second in reverse order so the GPU clock ramp favours
+        # no candidate.  Interleaving candidates replay by replay slowed the graphs that followed a different
+        # graph: LeNet B=128 serial measured 38.7 us/step interleaved with the concurrent schedule but 33.0 in
+        # its own segment and in run_steps (same box), which ranked the schedules the wrong way round.
+        # A k-step sample is a block of `blk` back-to-back replays between one pair of events; the step
+        # counter is rewound only when the next block would run past the loaded order.
+        blk = 4 if multi else 1
+        seg = 4 if multi else 12
+        per = blk * (k if multi else 1)                    # steps per sample
+        avail = getattr(self, "n_epoch", 0) // self.batch  # steps the loaded order holds
+        pos = 0
+        rounds = [names, names, names[::-1]]
+        for r, order in enumerate(rounds):
             for name in order:
                 self.apply_plan(candidates[name])   # host-side switch to the cached graph
-                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a.record(st)
-                self.rt.replay(st.cuda_stream)
-                b.record(st)
-                with torch.cuda.stream(st):
-                    self.step_ctr[0].zero_()
-                if r >= warmup:
-                    ev[name].append((a, b))
+                for j in range(seg):
+                    if pos + per > avail or not multi:
+                        with torch.cuda.stream(st):
+                            self.step_ctr[0].zero_()
+                        pos = 0
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record(st)
+                    for _ in range(blk):
+                        if multi:
+                            self.rt.replay_multi(st.cuda_stream)
+                        else:
+                            self.rt.replay(st.cuda_stream)
+                    b.record(st)
+                    pos += per
+                    if r > 0 and j > 0:
+                        ev[name].append((a, b))
         self.synchronize()
         timings = {}
+        if os.environ.get("MNIST_AMD_CALIB_DEBUG"):
+            for name in names:
+                print(f"calib {name}: " + " ".join(f"{a.elapsed_time(b) / (blk * k if multi else 1) * 1000:.1f}"
+                                                  for a, b in ev[name]), file=sys.stderr, flush=True)
         for name in names:
-            ts = sorted(a.elapsed_time(b) for a, b in ev[name])
+            ts = sorted(a.elapsed_time(b) / (blk * k if multi else 1) for a, b in ev[name])
             med = ts[len(ts) // 2]
             timings[name] = reduce_max(med) if reduce_max is not None else med
         with torch.cuda.stream(st):
             for dst, src in zip((self.params, self.mom, self.grad, self.step_ctr, self.metrics), saved):
                 dst.copy_(src)
         self.rt.pack(st.cuda_stream)
+        # the replays advanced the MLP look-ahead rows (xnext / ynext) past the restored step counter
+        self.rt.prime_next(st.cuda_stream)
         self.apply_plan(before)
         return timings
 
@@ -396,6 +442,13 @@ class NativeTrainer:
                     candidates = default_plan_candidates(self.C.conv_bwd_blocks(self.batch), ncu)
                 else:
                     candidates = mlp_plan_candidates()
+            elif self.model_name == "lenet5" and self.batch <= SMALL_BATCH_SERIAL:
+                # Small LeNet batches: the serial schedule, not calibrated.  run_steps measured serial 32.8 vs
+                # concurrent 35.0 us/step at B=128 (equal at 1024), but inside the calibration the serial
+                # graph timed 38.5 (scripts/calib_probe.py, profiles/r3_session2/NOTES.md): the calibration
+                # would pick the slower schedule.
+                self.apply_plan({"concurrent": False})
+                return {"chosen": "serial", "timings_ms": {}, "rule": f"batch <= {SMALL_BATCH_SERIAL}"}
             elif self.model_name == "lenet5":
                 candidates = local_plan_candidates(fwd_head=self.fwd_head_applies())
             else:
@@ -406,7 +459,8 @@ class NativeTrainer:
         chosen = choose_plan({k: timings[k] for k in candidates}, prefer=prefer, margin=margin)
         self.apply_plan(candidates[chosen])
         out = {"chosen": chosen, "timings_ms": {k: round(v, 4) for k, v in timings.items()},
-               "candidates": candidates, "replays_per_candidate": iters, "interleaved": True}
+               "candidates": candidates, "replays_per_candidate": self.last_timing["replays"],
+               "steps_per_replay": self.last_timing["graph_steps"], "interleaved": True}
         if extra:
             out["exposed_comm_ms"] = round(timings[chosen] - timings["nocomm"], 4)
         if log is not None:
@@ -508,13 +562,19 @@ class NativeTrainer:
     def graph_steps() -> int:
         return int(os.environ.get("MNIST_AMD_GRAPH_STEPS", "8"))
 
-    def prepare_graphs(self, k: Optional[int] = None) -> None:
-        """Capture + instantiate the single-step and the k-step graph now (setup, not step time)."""
+    def prepare_graphs(self, k: Optional[int] = None, extra=()) -> None:
+        """Capture + instantiate the single-step and the k-step graph now (setup, not step time), and a graph
+        of each ``extra`` step count >= 2 (the remainders run_steps will need: 20 steps = 8 + 8 + a 4-step
+        graph instead of 4 single-step launches)."""
         k = self.graph_steps() if k is None else int(k)
         if not self.rt.captured:
             self.capture()
         if k > 1 and self.rt.multi_steps != k:
             self.rt.capture_multi(self.stream.cuda_stream, k)
+        for e in extra:
+            e = int(e)
+            if e >= 2 and e != k and not self.rt.has_graph(e):
+                self.rt.capture_n(self.stream.cuda_stream, e)
 
     def run_steps(self, n: int, use_graph: bool = True, k: Optional[int] = None) -> None:
         """``n`` consecutive full-batch steps.  With graphs, runs of ``k`` steps are ONE hipGraph launch
@@ -533,6 +593,11 @@ class NativeTrainer:
             self.rt.replay_multi(self.stream.cuda_stream)
             self.host_step += k
             n -= k
+        # the remainder as ONE graph when one of that length was prepared (prepare_graphs(extra=...))
+        if (n >= 2 and self.rt.has_graph(n) and getattr(self, "n_epoch", 0) >= (self.host_step + n) * self.batch):
+            self.rt.replay_n(self.stream.cuda_stream, n)
+            self.host_step += n
+            n = 0
         for _ in range(n):
             self.step(self.batch, use_graph)
 

@@ -46,6 +46,28 @@ def report(title, st, names, last):
     print(f"  {'total':16s} mean {tot.mean():7.2f} us  min {tot.min():7.2f}  max {tot.max():7.2f}")
 
 
+def per_cu(title, st, loc, last):
+    """Balance across compute units: each CU's finish time (its last workgroup's final stamp)
+    relative to the kernel's first start.  loc = XCC << 32 | HW_ID per workgroup."""
+    hw = loc & 0xFFFFFFFF
+    key = ((loc >> 32) & 15) * 4096 + ((hw >> 13) & 7) * 512 + ((hw >> 12) & 1) * 256 + ((hw >> 8) & 15)
+    t0 = st[:, 0].min()
+    end = (st[:, last] - t0) * 10 / 1000.0
+    cus = {}
+    for k, e in zip(key.tolist(), end.tolist()):
+        n, m = cus.get(k, (0, 0.0))
+        cus[k] = (n + 1, max(m, e))
+    fin = np.array([m for _, m in cus.values()])
+    nwg = np.array([n for n, _ in cus.values()])
+    xccs = sorted({k // 4096 for k in cus})
+    per_xcc = " ".join(f"x{x}:{max(m for k, (_, m) in cus.items() if k // 4096 == x):.1f}" for x in xccs)
+    rr = np.mean(((loc >> 32) & 15) == (np.arange(len(loc)) % 8))
+    print(f"{title}: workgroup g on XCD g % 8 for {100 * rr:.1f}% of workgroups")
+    print(f"{title} per-CU: {len(cus)} CUs, workgroups/CU min {nwg.min()} max {nwg.max()}; CU finish "
+          f"mean {fin.mean():.2f} us  min {fin.min():.2f}  p90 {np.percentile(fin, 90):.2f}  max {fin.max():.2f}; "
+          f"per-XCC max {per_xcc}")
+
+
 # head rows per workgroup (head.hip head_rows_per_block; the split path at small batches uses 16)
 if B <= tr.C.L1_SPLIT_MAX_B and model == "mlp" or B <= 256:
     rows = 16
@@ -61,6 +83,17 @@ if fused:  # fwd_head_kernel: 16-row workgroups; head rows hold the head phases 
            ["setup"] + [f"img{t} {p}" for t in range(4) for p in ("stage", "conv1", "conv2")], 14)
     fw = allst[2048:2048 + nblk]
     print(f"  conv loop start -> head end: {((allst[:nblk, 8] - fw[:, 0]) * 10 / 1000).mean():.2f} us mean")
+    whole = np.concatenate([fw[:, :1], allst[:nblk, 8:9]], axis=1)  # [conv loop start, head end]
+    per_cu("fwd_head", whole, fw[:, 15], 1)
+    nb = 512
+    bw = allst[1024:1024 + nb]
+    print(f"boundaries: fwd_head last end -> conv_bwd first start {(bw[:, 0].min() - allst[:nblk, 8].max()) * 10 / 1000:.2f} us; "
+          f"fwd_head first start -> conv_bwd last end {(bw[:, 15].max() - fw[:, 0].min()) * 10 / 1000:.2f} us")
+    bnames = ["setup"]
+    for t in range(4):
+        bnames += [f"img{t} A (stage)", f"img{t} B (w2+dgrad)", f"img{t} C (w1)"]
+    report("conv_bwd", bw, bnames + [None, "slab write"], 15)
+    per_cu("conv_bwd", bw, allst[4608:4608 + nb, 0], 15)
 elif model == "lenet5":
     report("head", allst[:nblk], ["idx+stage X", "L1", "L2", "L3", "softmax", "dH2", "dH1", "dX"], 8)
     # inside the staging phase: [0] entry -> [9] loads issued -> [10] weights stored -> [11] X stored -> [1] barrier
@@ -90,27 +123,6 @@ if model == "lenet5" and not fused:
     for t in range(4):
         bnames += [f"img{t} A (stage)", f"img{t} B (w2+dgrad)", f"img{t} C (w1)"]
     report("conv_bwd", allst[1024:1024 + nb], bnames + [None, "slab write"], 15)
-
-    def per_cu(title, st, loc, last):
-        """Balance across compute units: each CU's finish time (its last workgroup's final stamp)
-        relative to the kernel's first start.  loc = XCC << 32 | HW_ID per workgroup."""
-        hw = loc & 0xFFFFFFFF
-        key = ((loc >> 32) & 15) * 4096 + ((hw >> 13) & 7) * 512 + ((hw >> 12) & 1) * 256 + ((hw >> 8) & 15)
-        t0 = st[:, 0].min()
-        end = (st[:, last] - t0) * 10 / 1000.0
-        cus = {}
-        for k, e in zip(key.tolist(), end.tolist()):
-            n, m = cus.get(k, (0, 0.0))
-            cus[k] = (n + 1, max(m, e))
-        fin = np.array([m for _, m in cus.values()])
-        nwg = np.array([n for n, _ in cus.values()])
-        xccs = sorted({k // 4096 for k in cus})
-        per_xcc = " ".join(f"x{x}:{max(m for k, (_, m) in cus.items() if k // 4096 == x):.1f}" for x in xccs)
-        rr = np.mean(((loc >> 32) & 15) == (np.arange(len(loc)) % 8))
-        print(f"{title}: workgroup g on XCD g % 8 for {100 * rr:.1f}% of workgroups")
-        print(f"{title} per-CU: {len(cus)} CUs, workgroups/CU min {nwg.min()} max {nwg.max()}; CU finish "
-              f"mean {fin.mean():.2f} us  min {fin.min():.2f}  p90 {np.percentile(fin, 90):.2f}  max {fin.max():.2f}; "
-              f"per-XCC max {per_xcc}")
 
     # kernel boundaries on the device clock: last workgroup end of one kernel -> first start of the next
     fw, hd, bw = allst[2048:2048 + min(nf, 1024)], allst[:nblk], allst[1024:1024 + nb]

@@ -60,7 +60,7 @@ def _emulate(model, dtype, batch, steps, dropout):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("model,dtype,batch", [("lenet5", "bf16", 512), ("mlp", "fp32", 128)])
+@pytest.mark.parametrize("model,dtype,batch", [("lenet5", "bf16", 2048), ("mlp", "fp32", 128)])
 def test_two_ranks_share_one_gpu(native, tmp_path, model, dtype, batch):
     steps, warmup = 4, 2
     out, err = _bench(["--gpus", "2", "--comm", "gloo", "--model", model, "--dtype", dtype, "--batch", str(batch),
@@ -70,7 +70,8 @@ def test_two_ranks_share_one_gpu(native, tmp_path, model, dtype, batch):
     assert "gloo" in out["config"]["comm"]
     if model == "lenet5":   # the rank-max calibration ran across the two processes
         assert set(out["config"]["plan_autotune"]["timings_ms"]) == {"concurrent", "serial"}
-    digests = dict(re.findall(r"digest rank=(\d) (\w+)", err))
+    # (the two ranks share stderr: their lines can interleave without a newline between them)
+    digests = dict(re.findall(r"digest rank=(\d) ([0-9a-f]{64})", err))
     assert set(digests) == {"0", "1"} and digests["0"] == digests["1"], err[-2000:]
     p = [torch.load(tmp_path / f"p.rank{r}.pt", weights_only=True) for r in range(2)]
     assert torch.equal(p[0], p[1])
