@@ -60,6 +60,21 @@ def forced_plan() -> Optional[str]:
 PLAN_NAMES = {v: k for k, v in PLANS.items()}
 
 
+def calib_blocks(avail: int, k: int, multi: bool):
+    """Sample shape of :meth:`NativeTrainer.time_schedules`: (multi, replays per sample, samples per
+    segment, steps per sample).  A sample replays from the rewound step counter, so it must never run
+    past the ``avail`` loaded steps: at most 4 k-step replays and no more than fit (a 4 x 20-step block
+    over a 28-step order once read past the index buffer -- a GPU memory fault)."""
+    blk = min(4, avail // k) if multi and k > 1 else 1
+    if blk < 1:
+        multi, blk = False, 1
+    seg = 4 if multi else 12
+    per = blk * (k if multi else 1)
+    if per > avail:
+        raise RuntimeError(f"time_schedules: a sample of {per} steps exceeds the {avail} loaded steps")
+    return bool(multi), blk, seg, per
+
+
 # single-GPU LeNet batches up to this size use the serial schedule without calibration (autotune_plan)
 SMALL_BATCH_SERIAL = int(os.environ.get("MNIST_AMD_SMALL_SERIAL", "1024"))
 
@@ -343,7 +358,9 @@ class NativeTrainer:
         k = self.graph_steps()
         can = k > 1 and self.ext_allreduce is None and getattr(self, "n_epoch", 0) >= (k + 1) * self.batch
         multi = can if multi is None else (bool(multi) and can)
-        self.last_timing = {"graph_steps": k if multi else 1, "replays": 2 * (3 if multi else 11) * (4 if multi else 1)}
+        avail = getattr(self, "n_epoch", 0) // self.batch  # steps the loaded order holds
+        multi, blk, seg, per = calib_blocks(avail, k, multi)
+        self.last_timing = {"graph_steps": k if multi else 1, "replays": 2 * (seg - 1) * blk}
         before = self.current_schedule()
         self.synchronize()
         saved = [t.clone() for t in (self.params, self.mom, self.grad, self.step_ctr, self.metrics)]
@@ -365,10 +382,6 @@ class NativeTrainer:
         # its own segment and in run_steps (same box), which ranked the schedules the wrong way round.
         # A k-step sample is a block of `blk` back-to-back replays between one pair of events; the step
         # counter is rewound only when the next block would run past the loaded order.
-        blk = 4 if multi else 1
-        seg = 4 if multi else 12
-        per = blk * (k if multi else 1)                    # steps per sample
-        avail = getattr(self, "n_epoch", 0) // self.batch  # steps the loaded order holds
         pos = 0
         rounds = [names, names, names[::-1]]
         for r, order in enumerate(rounds):

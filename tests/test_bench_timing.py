@@ -119,3 +119,19 @@ def test_synthetic_hard_mode():
     assert centroid_acc(xh, yh) < centroid_acc(xe, ye) - 0.2
     with pytest.raises(ValueError):
         make_split(10, seed=0, mode="nope")
+
+
+def test_calibration_samples_stay_inside_the_loaded_order():
+    """time_schedules replays samples from a rewound step counter: a sample must never need more steps
+    than the loaded order holds (a 4 x 20-step block over 28 loaded steps read past the index buffer)."""
+    from pytorch_ddp_mnist_amd.engine.native import calib_blocks
+    for avail in (1, 2, 9, 14, 20, 21, 28, 40, 468):
+        for k in (1, 2, 8, 10, 20, 32):
+            for multi in (True, False):
+                m, blk, seg, per = calib_blocks(avail, k, multi and avail >= k + 1)
+                assert per <= avail and blk >= 1 and seg >= 2
+                assert per == blk * (k if m else 1)
+    assert calib_blocks(28, 8, True) == (True, 3, 4, 24)
+    assert calib_blocks(28, 20, True) == (True, 1, 4, 20)
+    assert calib_blocks(468, 8, True) == (True, 4, 4, 32)
+    assert calib_blocks(10, 8, False) == (False, 1, 12, 1)
