@@ -573,7 +573,9 @@ class NativeTrainer:
 
     @staticmethod
     def graph_steps() -> int:
-        return int(os.environ.get("MNIST_AMD_GRAPH_STEPS", "8"))
+        # 10: the 20-step driver shape is two whole graphs (0.1081-0.1098 vs 0.1097-0.1103 ms with 8, same box;
+        # equal at 2000 steps)
+        return int(os.environ.get("MNIST_AMD_GRAPH_STEPS", "10"))
 
     def prepare_graphs(self, k: Optional[int] = None, extra=()) -> None:
         """Capture + instantiate the single-step and the k-step graph now (setup, not step time), and a graph
@@ -591,7 +593,7 @@ class NativeTrainer:
 
     def run_steps(self, n: int, use_graph: bool = True, k: Optional[int] = None) -> None:
         """``n`` consecutive full-batch steps.  With graphs, runs of ``k`` steps are ONE hipGraph launch
-        (``MNIST_AMD_GRAPH_STEPS``, default 8; the graph launch gap is paid once per k steps), the
+        (``MNIST_AMD_GRAPH_STEPS``, default 10; the graph launch gap is paid once per k steps), the
         remainder single-step graphs.  Same kernels, same order, same results as ``n`` x :meth:`step`."""
         k = self.graph_steps() if k is None else int(k)
         if not use_graph or k <= 1 or self.ext_allreduce is not None:
