@@ -821,8 +821,13 @@ struct BwdSmem {
   static constexpr int XS_N = ONES + ONES_N, PPL = 32;
   static constexpr int OFF_XS = 0;
   static constexpr int OFF_P1T = rup(OFF_XS + (HD ? XS_N * (int)sizeof(T) : 0), 16);
+  // TRA (full kernel, bf16): the conv2 wgrad reads its A operand (channel-major dY2) straight from the
+  // position-major DYS image with ds_read_b64_tr_b16 (transposing LDS reads), so there is no DY2T image
+  // and no second un-pooling scatter
+  static constexpr bool TRA = MODE == 0 && sizeof(T) == 2;
+  static constexpr bool DY2 = HW && !TRA;
   static constexpr int OFF_DY2T = rup(OFF_P1T + (HW ? PPL * P1P * (int)sizeof(T) : 0), 16);
-  static constexpr int OFF_DYS = rup(OFF_DY2T + (HW ? 16 * D2P * (int)sizeof(T) : 0), 16);  // [18][18][16] zero-padded
+  static constexpr int OFF_DYS = rup(OFF_DY2T + (DY2 ? 16 * D2P * (int)sizeof(T) : 0), 16);  // [18][18][16] zero-padded
   static constexpr int OFF_W2 = rup(OFF_DYS + (HD ? 18 * 18 * 16 * (int)sizeof(T) : 0), 16);
   static constexpr int OFF_DY1T = rup(OFF_W2 + (HD ? 16 * W2P * (int)sizeof(T) : 0), 16);
   static constexpr int OFF_M1 = rup(OFF_DY1T + (HD ? (D1PRE + 8 * D1P) * (int)sizeof(T) : 0), 16);  // [6][M1CP] u8 pool1 codes
@@ -930,7 +935,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   if constexpr (HW) {
     zero_lds<T>(p1t, 31 * S::P1P);
     for (int e = tid; e < S::P1P; e += 256) p1t[31 * S::P1P + e] = to_t<T>(1.f);
-    zero_lds<T>(dy2t, 16 * S::D2P);
+    if constexpr (S::DY2) zero_lds<T>(dy2t, 16 * S::D2P);
   }
   // conv2 dgrad, two output rows per tile: out (Y = y + r, x, c) = sum over kh' in [-1, 4], kw, n of
   // dY2[y - kh'][x - kw][n] * W2[n][c][kh' + r][kw]  ->  B[(kh'+1)*5 + kw, n][(r, c)], zero where
@@ -1104,7 +1109,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
           const int oh = 2 * py + (win >> 1), ow = 2 * px + (win & 1);
           if constexpr (HD) *reinterpret_cast<uint32_t*>(dys + ((oh + 4) * 18 + ow + 4) * 16 + n0) = pack2(v[0][win], v[1][win]);
         }
-        if constexpr (HW) {
+        if constexpr (S::DY2) {
 #pragma unroll
           for (int r = 0; r < 2; ++r)
 #pragma unroll
@@ -1141,7 +1146,25 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     //      chunk's fragments loaded before this chunk's MFMAs: a runtime trip count kept the loop
     //      rolled and every chunk waited for its own LDS reads.
     if (HW && !(cb.ablate & 64)) {
-      auto ld_a = [&](int kc) { return M::load(dy2t + row * S::D2P + kc * KC + grp * KV); };
+      auto ld_a = [&](int kc) -> Frag {
+        if constexpr (S::TRA) {
+          // positions p0 .. p0 + 7 (row y = p0 / 16, columns x0 .. x0 + 7; x >= 10 reads DYS's zero padding) of
+          // channel `row`: two 4-position x 16-channel blocks, transposed by the read.  Lane 4q + p of each
+          // 16-lane group addresses position x0 + q (+ 4), channels 4p .. 4p + 3; lane i receives channel i.
+          typedef short v4s __attribute__((ext_vector_type(4)));
+          const int p0 = kc * KC + grp * KV, y = p0 >> 4, x0 = p0 & 15;
+          const T* a = dys + ((y + 4) * 18 + x0 + ((lane & 15) >> 2) + 4) * 16 + 4 * (lane & 3);
+          const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) v4s*)(const_cast<T*>(a)));
+          const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) v4s*)(const_cast<T*>(a + 4 * 16)));
+          Frag f;
+          f.v = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          return f;
+        } else {
+          return M::load(dy2t + row * S::D2P + kc * KC + grp * KV);
+        }
+      };
       auto ld_b = [&](int kc, int i) {
         const int p0 = kc * KC + grp * KV;
         return M::load(p1t + w2off[i] + (p0 >> 4) * 16 + (p0 & 15));
