@@ -389,6 +389,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
         }
       }
     }
+    stamp(11);  // gathered tile converted and stored to LDS, xT stores issued
   } else {
     T* xT = reinterpret_cast<T*>(hb.xT);
     // element j of a 16-byte chunk, as raw bits (register extracts: a pointer-punned read of the chunk

@@ -112,6 +112,11 @@ elif model == "lenet5":
 else:  # no dX phase: stamp 7 is never written, dH1 ends at stamp 8
     allst[:nblk, 7] = allst[:nblk, 8]
     report("head", allst[:nblk], ["idx+stage X", "L1", "L2", "L3", "softmax", "dH2", "dH1"], 8)
+    # MLP staging: [0] entry -> [9] idx + bias loads issued -> [10] (no LDS weights) -> barrier + gather +
+    # convert + stores -> [11] -> [1] barrier
+    hs = allst[:nblk][:, [0, 9, 11, 1]]
+    if (hs[:, 1:3] > 0).all():
+        report("head staging", hs, ["idx/bias issue", "gather+convert+X/xT stores", "barrier"], 3)
 if model == "lenet5" and not fused:
     per_img = []
     for t in range(4):
