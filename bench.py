@@ -184,8 +184,15 @@ def main(argv=None) -> int:
     if a.model == "lenet5" and dropout:
         raise SystemExit("LeNet-5 has no dropout layer")
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    ctx = init_distributed(None, parallel=world_env > 1, device="cuda", comm=a.comm,
-                           share_device=a.comm == "gloo")
+    from pytorch_ddp_mnist_amd.parallel.comm import CommInitError
+    try:
+        ctx = init_distributed(None, parallel=world_env > 1, device="cuda", comm=a.comm,
+                               share_device=a.comm == "gloo")
+    except CommInitError as e:
+        # bounded RCCL bring-up failed (MNIST_AMD_COMM_INIT_TIMEOUT): name the rank and leave at once -- the
+        # launcher tears the other ranks down; no interpreter teardown that could wait on the dead peers
+        print(f"[bench] {e}", file=sys.stderr, flush=True)
+        os._exit(3)
     if ctx.world != a.gpus and ctx.rank == 0:
         print(f"[bench] note: --gpus {a.gpus} but WORLD_SIZE={ctx.world}; using {ctx.world}", file=sys.stderr)
     W, rank, dev = ctx.world, ctx.rank, ctx.device
@@ -229,8 +236,12 @@ def main(argv=None) -> int:
     # start-up schedule calibration (multi-GPU plan on the communicator, or the single-GPU
     # schedule): interleaved captured-step replays per candidate, state restored, choice in the JSON.
     # With an external data plane the step is not a graph: the local schedules are still timed (rank-max)
-    if a.plan == "auto" and (use_graph or external):
+    if a.plan == "auto" and use_graph:
         tune = tr.autotune_plan(reduce_max=ctx.all_reduce_max)
+    elif a.plan == "auto" and external:
+        # the external data plane runs the eager phase API (forward_backward -> host all-reduce -> SGD), not
+        # the captured schedules a calibration would time: nothing to choose
+        tune = {"chosen": "eager-phases", "timings_ms": {}, "note": "external data plane: no graph schedules"}
     if comm is not None and use_graph:
         prof = tr.comm_profile(reduce_max=ctx.all_reduce_max, tune=tune)
 
@@ -313,7 +324,7 @@ def main(argv=None) -> int:
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
-    ctx.finalize()
+    ctx.finalize(tr)
     return 0
 
 

@@ -46,6 +46,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("L1_KSPLIT") = L1_KSPLIT;
   m.def("metric_rows", [](int B) { return metric_rows(B); });
   m.attr("L1_SPLIT_MAX_B") = L1_SPLIT_MAX_B;
+  m.attr("STAMP_ROWS") = STAMP_ROWS;  // rows of the MNIST_AMD_STAMPS buffer (launch.h)
   m.def("device_count", [] {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -88,11 +89,42 @@ PYBIND11_MODULE(_C, m) {
 
   py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
       .def_static("make_unique_id", [] { return py::bytes(RcclComm::make_unique_id()); })
-      .def(py::init([](py::bytes uid, int rank, int world, int device) {
-        std::string id(uid);  // copy while holding the GIL; init blocks on peers, so release it then
-        py::gil_scoped_release nogil;
-        return std::make_shared<RcclComm>(id, rank, world, device);
-      }))
+      .def(py::init([](py::bytes uid, int rank, int world, int device, double init_timeout) {
+             std::string id(uid);  // copy while holding the GIL; init waits on peers, so release it then
+             py::gil_scoped_release nogil;
+             return std::make_shared<RcclComm>(id, rank, world, device, init_timeout);
+           }),
+           py::arg("uid"), py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("init_timeout") = 180.0)
+      // The bounded-bring-up logic of the constructor against a FAKE communicator (no GPU, no RCCL state):
+      // `ready_after` polls until it reports ready (< 0: never -- a peer that never arrives), `fail`: it reports
+      // an error instead.  Returns (error message or "", seconds waited, whether abort was called).
+      .def_static("_fake_init",
+                  [](int rank, int world, double timeout, int ready_after, bool fail) {
+                    int polls = 0;
+                    bool aborted = false;
+                    double waited = 0.0;
+                    ncclResult_t st;
+                    {
+                      py::gil_scoped_release nogil;
+                      st = RcclComm::poll_ready(
+                          [&] {
+                            ++polls;
+                            if (fail && polls > 2) return ncclSystemError;
+                            if (ready_after >= 0 && polls > ready_after) return ncclSuccess;
+                            return ncclInProgress;
+                          },
+                          timeout, &waited);
+                    }
+                    const std::string err =
+                        RcclComm::init_outcome(st, rank, world, timeout, waited, [&] { aborted = true; });
+                    return py::make_tuple(err, waited, aborted);
+                  },
+                  py::arg("rank"), py::arg("world"), py::arg("timeout"), py::arg("ready_after") = -1,
+                  py::arg("fail") = false)
+      .def("destroy", &RcclComm::destroy, py::arg("timeout") = 600.0, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("destroyed", &RcclComm::destroyed)
+      .def_property_readonly("nonblocking", &RcclComm::nonblocking)
+      .def_property_readonly("init_seconds", &RcclComm::init_seconds)
       .def("all_reduce_sum_f32",
            [](RcclComm& c, uintptr_t buf, size_t n, uintptr_t s) {
              c.all_reduce_sum_f32(reinterpret_cast<float*>(buf), n, reinterpret_cast<hipStream_t>(s));
@@ -116,7 +148,7 @@ PYBIND11_MODULE(_C, m) {
       .def("wait_stream",
            [](RcclComm& c, uintptr_t s, double timeout) { return c.wait_stream(reinterpret_cast<hipStream_t>(s), timeout); },
            py::call_guard<py::gil_scoped_release>())
-      .def("abort", &RcclComm::abort)
+      .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("aborted", &RcclComm::aborted)
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("world", &RcclComm::world);
@@ -162,6 +194,7 @@ PYBIND11_MODULE(_C, m) {
       .def("replay_n", &Trainer::replay_n)
       .def_property_readonly("multi_steps", &Trainer::multi_steps)
       .def("invalidate", &Trainer::invalidate)
+      .def("release", &Trainer::release, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("captured", &Trainer::captured)
       .def_property_readonly("nparam", &Trainer::nparam)
       .def_property_readonly("pack_size", &Trainer::pack_size)

@@ -358,7 +358,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
             if (item) *reinterpret_cast<u32x4*>(sX + (r + q) * S::PX + c * 16 + h * 8) = pk[q][h];
           }
         }
-        if (TRAIN && item && !(hb.ablate & 1)) {
+        if (TRAIN && item && !ABLATED(hb.ablate, 1)) {
 #pragma unroll
           for (int j = 0; j < 16; ++j) {
             const int h = j >> 3, wd = (j & 7) >> 1, sh = 16 * (j & 1);
@@ -1285,25 +1285,11 @@ __global__ __launch_bounds__(256) void wgrad_sgd_kernel(WgArgs<T> a) {
   stamp(2);
 }
 
-// Ring slots of K-step fragments per wave in wgrad_kernel (MNIST_AMD_WGRAD_DEPTH A/B knob): 1 = the next
-// step's fragments fetched while this one computes (default), 2 / 4 = two / four steps ahead (LeNet:
-// 1 and 2 within noise; 4 measured 0.3-1.6 % slower than 2 on both models)
-inline int wgrad_depth() {
-  static const int d = [] {
-    const char* e = std::getenv("MNIST_AMD_WGRAD_DEPTH");
-    return e ? std::atoi(e) : 1;
-  }();
-  return d;
-}
-// LDS-staged weight gradient (wgrad_lds_kernel): default for the MLP, whose wgrad runs alone on the chip;
-// MNIST_AMD_WGRAD_LDS=0/1 overrides (A/B knob)
-inline bool wgrad_lds(bool mlp) {
-  static const int e = [] {
-    const char* v = std::getenv("MNIST_AMD_WGRAD_LDS");
-    return v ? std::atoi(v) : -1;
-  }();
-  return e < 0 ? mlp : e != 0;
-}
+// wgrad_kernel keeps ONE ring slot of K-step fragments per wave (the next step's fragments fetched while this
+// one computes: two / four steps ahead measured within noise / 0.3-1.6 % slower on both models).  The
+// LDS-staged weight gradient (wgrad_lds_kernel) is used for the MLP, whose wgrad runs alone on the chip; the
+// LeNet wgrad runs beside conv_bwd, which holds the LDS.
+constexpr int WGRAD_DEPTH = 1;
 
 template <typename T, class H, class Model>
 int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab_ld, int xcd_ch, hipStream_t s,
@@ -1342,26 +1328,21 @@ int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab
   a.slab_ld = slab_ld;
   a.stamps = hb.stamps;
   a.xcd_ch = 0;
-  const bool lds_stage = wgrad_lds(std::is_same<Model, MlpModel>::value);
-  static const bool xcd_off = std::getenv("MNIST_AMD_NO_XCD") != nullptr;  // A/B knob
+  const bool lds_stage = std::is_same<Model, MlpModel>::value;
   // XCD-aware mapping when the head's row tiling is known and the split count divides over 8 XCDs
-  if (!fuse && !xcd_off && xcd_ch > 0 && xcd_ch % KC == 0 && splits % 8 == 0) {
+  if (!fuse && xcd_ch > 0 && xcd_ch % KC == 0 && splits % 8 == 0) {
     a.xcd_ch = xcd_ch;
     a.nch = (a.Bp + xcd_ch - 1) / xcd_ch;
     a.sx = splits / 8;
     const int head_grid = (rup(B, 32) + xcd_ch - 1) / xcd_ch;  // head_launch_mtw's grid
     a.contig = hb.xcd && head_grid % 8 == 0 && a.nch == head_grid;
     if (lds_stage) hipLaunchKernelGGL(wgrad_lds_kernel<T>, dim3(blk * splits), dim3(256), 0, s, a);
-    else if (wgrad_depth() == 4) hipLaunchKernelGGL((wgrad_kernel<T, 4>), dim3(blk * splits), dim3(256), 0, s, a);
-    else if (wgrad_depth() == 1) hipLaunchKernelGGL((wgrad_kernel<T, 1>), dim3(blk * splits), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((wgrad_kernel<T, 2>), dim3(blk * splits), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_kernel<T, WGRAD_DEPTH>), dim3(blk * splits), dim3(256), 0, s, a);
   } else if (a.fuse) {
     hipLaunchKernelGGL((wgrad_sgd_kernel<T, Model>), dim3(blk), dim3(256), 0, s, a);
   } else {
     if (lds_stage) hipLaunchKernelGGL(wgrad_lds_kernel<T>, dim3(blk, splits), dim3(256), 0, s, a);
-    else if (wgrad_depth() == 4) hipLaunchKernelGGL((wgrad_kernel<T, 4>), dim3(blk, splits), dim3(256), 0, s, a);
-    else if (wgrad_depth() == 1) hipLaunchKernelGGL((wgrad_kernel<T, 1>), dim3(blk, splits), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL((wgrad_kernel<T, 2>), dim3(blk, splits), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL((wgrad_kernel<T, WGRAD_DEPTH>), dim3(blk, splits), dim3(256), 0, s, a);
   }
   return splits;
 }
@@ -1376,15 +1357,10 @@ void head_launch_mtw(bool train, const BatchRef& br, const HeadBuffers& hb, hipS
     hipLaunchKernelGGL((head_kernel<T, H, MT, false, false, NWV>), dim3(grid), dim3(NWV * 64), 0, s, br, hb);
 }
 
+// 16 waves per head workgroup (swept 4 / 8 / 16 at B=8192: 16 waves, 4 per SIMD, best by 3 % step time)
 template <typename T, class H, int MT>
 void head_launch_mt(bool train, const BatchRef& br, const HeadBuffers& hb, hipStream_t s) {
-  static const int nwv = [] {
-    const char* e = std::getenv("MNIST_AMD_HEAD_NWV");  // tuning knob: waves per head workgroup
-    return e ? std::atoi(e) : 16;  // swept 4 / 8 / 16 at B=8192: 16 waves (4 per SIMD) best, -3% step time
-  }();
-  if (nwv == 8) head_launch_mtw<T, H, MT, 8>(train, br, hb, s);
-  else if (nwv == 16) head_launch_mtw<T, H, MT, 16>(train, br, hb, s);
-  else head_launch_mtw<T, H, MT, 4>(train, br, hb, s);
+  head_launch_mtw<T, H, MT, 16>(train, br, hb, s);
 }
 
 // small-batch path: layer-1 split GEMM, then the head with 16-row tiles consuming the partials;
@@ -1408,25 +1384,15 @@ void head_launch_split_w(bool train, const BatchRef& br, const HeadBuffers& hb, 
 
 template <typename T, class H>
 void head_launch_split(bool train, const BatchRef& br, const HeadBuffers& hb, hipStream_t s) {
-  static const int nwv = [] {
-    const char* e = std::getenv("MNIST_AMD_SPLIT_NWV");  // tuning knob: 4 / 8 / 16 waves
-    return e ? std::atoi(e) : SPLIT_NWV;
-  }();
-  if (nwv == 16) head_launch_split_w<T, H, 16>(train, br, hb, s);
-  else if (nwv == 4) head_launch_split_w<T, H, 4>(train, br, hb, s);
-  else head_launch_split_w<T, H, 8>(train, br, hb, s);
+  head_launch_split_w<T, H, SPLIT_NWV>(train, br, hb, s);
 }
 
 // returns the batch rows per workgroup actually used (the wgrad kernel's XCD-aware mapping needs it)
 template <typename T, class H>
 int head_launch_t(bool train, const BatchRef& br, const HeadBuffers& hb, int rows, hipStream_t s) {
   // the split layer 1 pays for its extra launch only on the 784-deep MLP layer; LeNet's 400-deep layer 1
-  // runs inside the head (B=128: 38.2 vs 39.9 us per step with the split).  MNIST_AMD_L1_SPLIT=0/1 overrides.
-  static const int l1s = [] {
-    const char* e = std::getenv("MNIST_AMD_L1_SPLIT");
-    return e ? std::atoi(e) : (std::getenv("MNIST_AMD_NO_L1_SPLIT") ? 0 : -1);
-  }();
-  const bool split_l1 = l1s < 0 ? H::K0 >= 512 : l1s != 0;
+  // runs inside the head (B=128: 38.2 vs 39.9 us per step with the split)
+  constexpr bool split_l1 = H::K0 >= 512;
   if (hb.z1p && br.B <= L1_SPLIT_MAX_B && split_l1) {
     head_launch_split<T, H>(train, br, hb, s);
     return 16;
@@ -1469,11 +1435,6 @@ void launch_gather_next(const BatchRef& br, hipStream_t s) {
 }
 
 int head_rows_per_block(ModelKind m, DType t, int B) {
-  static const int forced = [] {
-    const char* e = std::getenv("MNIST_AMD_HEAD_ROWS");  // tuning knob
-    return e ? std::atoi(e) : 0;
-  }();
-  if (forced) return forced;
   if (B <= 256) return 16;
   if (t == DType::F32) return 32;
   // MLP bf16, B=8192: 32-row tiles (256 workgroups, every CU) 34.8 us per step vs 38.8-39.3 with 64-row

@@ -66,6 +66,16 @@ struct LenetConvBuffers {
   unsigned long long* stamps = nullptr;  // optional phase timestamps (profiling): fwd [block][16], bwd [block][16]
 };
 
+// Timing-ablation switches (MNIST_AMD_ABLATE / MNIST_AMD_HEAD_ABLATE: skip kernel phases, WRONG results).
+// Compiled in only by an ablation build (-DMNIST_AMD_ABLATION_BUILD, scripts/ablate.sh); in the normal
+// build every ABLATED() is a constant false and the runtime refuses the variables instead of silently
+// training on skipped phases.
+#ifdef MNIST_AMD_ABLATION_BUILD
+#define ABLATED(flags, bit) (((flags) & (bit)) != 0)
+#else
+#define ABLATED(flags, bit) false
+#endif
+
 // MNIST_AMD_STAMPS profiling buffer: [STAMP_ROWS][16] uint64 wall-clock stamps, one row per workgroup,
 // each kernel in its own row range (scripts/stamps.py reads the same layout)
 constexpr int STAMP_HEAD = 0;          // head workgroups            [0, 1024)
@@ -112,22 +122,21 @@ int launch_head_wgrad(ModelKind m, DType t, const HeadBuffers& hb, int B, int sp
 void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetConvBuffers& cb,
                            hipStream_t s);
 // LeNet training forward + FC head (fwd, softmax-CE, dgrad) in one kernel (lenet.hip fwd_head_kernel):
-// replaces launch_lenet_conv_fwd + launch_head for bf16 batches B >= 4096, B % 16 == 0 (MNIST_AMD_FWD_HEAD=0
-// disables it).  Returns the head-rows value for launch_head_wgrad's XCD-aware mapping (32: the fused
+// replaces launch_lenet_conv_fwd + launch_head for bf16 batches B >= 4096, B % 16 == 0 (Trainer::set_fwd_head(false)
+// selects the two kernels).  Returns the head-rows value for launch_head_wgrad's XCD-aware mapping (32: the fused
 // kernel's 16-row units give each XCD the same contiguous eighth of the batch as 32-row head tiles), or 0
 // when it does not apply (the caller launches the two kernels).
 int launch_lenet_fwd_head(DType t, const BatchRef& br, const LenetConvBuffers& cb, const HeadBuffers& hb,
                           hipStream_t s);
 bool lenet_fwd_head_applies(DType t, int B);
 // LeNet training head alone as the 16-row register-B head (lenet.hip head16_kernel) on the pool2 rows of
-// conv_fwd: bf16, B <= MNIST_AMD_HEAD16 (default 2048).  Returns launch_head's rows value, or 0 when it
+// conv_fwd: bf16, B <= 2048.  Returns launch_head's rows value, or 0 when it
 // does not apply (the caller launches launch_head).
 int launch_lenet_head16(DType t, const BatchRef& br, const HeadBuffers& hb, hipStream_t s);
-// mode 0: full backward; 1: conv2 dgrad + conv1 wgrad half; 2: conv2 wgrad half (lenet.hip MODE)
 // target_blocks: workgroup count to aim for (0 = default, one full round of 2 blocks per CU); each
 // block walks ceil(B / target) images, so a smaller target leaves whole CUs free (for RCCL kernels).
 void launch_lenet_conv_bwd(DType t, const BatchRef& br, const LenetConvBuffers& cb, int* nslab_out,
-                           hipStream_t s, int mode = 0, int target_blocks = 0);
+                           hipStream_t s, int target_blocks = 0);
 int lenet_conv_bwd_blocks(int B, int target_blocks = 0);
 int lenet_conv_bwd_max_blocks(int B, int target_blocks = 0);  // slab rows needed for any batch <= B
 

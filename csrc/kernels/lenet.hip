@@ -295,7 +295,7 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
     const bool valid = b < br.B;
     const Raw u = u_next;
     // ---- stage: normalise once, 4 aligned 16-byte plane stores per thread
-    if (tid < 224 && !(cb.ablate & 1)) {
+    if (tid < 224 && !ABLATED(cb.ablate, 1)) {
       float f[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -351,7 +351,7 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
     flush_p2(t > 0 ? b - 1 : -1);
 
     // ---- conv1 + bias + ReLU + maxpool: 7 two-row tiles per wave
-    if (!(cb.ablate & 2)) {
+    if (!ABLATED(cb.ablate, 2)) {
       // software pipeline: tile t+1's fragments are loaded and tile t's MFMAs issued BEFORE tile
       // t-1's epilogue (the compiler cannot hoist xs loads over the epilogue's p1s stores itself)
       // Tile t+1 starts 4 input rows below tile t and K spans 8 rows, so its first half of K chunks
@@ -382,12 +382,12 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
     if (t < 4) stamp(3 + 3 * t);
 
     // ---- pool1 -> HBM for the backward pass (16-byte stores), overlapped with conv2
-    if (TRAIN && valid && !(cb.ablate & 1024)) {
+    if (TRAIN && valid && !ABLATED(cb.ablate, 1024)) {
       copy_out16<true>(reinterpret_cast<T*>(cb.p1) + (size_t)b * P1IMG, p1c, P1IMG * (int)sizeof(T), tid, 256);
       copy_out16<true>(cb.m1 + (size_t)b * M1IMG, m1s, M1IMG, tid, 256);
     }
     // ---- conv2 + bias + ReLU + maxpool: 100 rows (25 pooled x 4) = 7 M-tiles, N = 16
-    if (!(cb.ablate & 4)) {
+    if (!ABLATED(cb.ablate, 4)) {
       if (w < 3) {  // waves 0-2: tiles (2w, 2w+1) as a pair; wave 3: tile 6
         const int mts[2] = {2 * w, 2 * w + 1};
         f32x4 acc[2] = {zero4(), zero4()};
@@ -1003,7 +1003,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     const Pre cur = nxt;
     // ---- phase A: stage input (5 shifted copies), pool1 (5 shifted channel-major copies),
     //      pool1 codes, and the pool2 un-pooling scatter into DYS / DY2T
-    if (HD && tid < 112 && !(cb.ablate & 8)) {
+    if (HD && tid < 112 && !ABLATED(cb.ablate, 8)) {
       // XS: planes kw = 0..4 of row y, columns [8g, 8g+8): xs[kw][y][x] = xpad[y][x + kw] = w[kw + 2 + j]
       // with w[i] = normalised pixel at image column 8g - 4 + i (0 outside the image)
       const int y = 2 + (tid >> 2), g = tid & 3;
@@ -1043,9 +1043,9 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
         }
       }
     }
-    if (HD && tid >= 112 && tid < 112 + M1IMG / 16 && !(cb.ablate & 8))
+    if (HD && tid >= 112 && tid < 112 + M1IMG / 16 && !ABLATED(cb.ablate, 8))
       reinterpret_cast<uint4*>(m1s)[tid - 112] = valid ? cur.m : make_uint4(0, 0, 0, 0);
-    if (HW && tid >= 128 && tid < 128 + 84 && !(cb.ablate & 8)) {
+    if (HW && tid >= 128 && tid < 128 + 84 && !ABLATED(cb.ablate, 8)) {
       // P1T: row y of planes (kw, c), kw = 0..4: p1t[kw*6+c][y][x] = pool1[y][x + kw][c], 0 for x + kw >= 14
       const int i = tid - 128, c = i / 14, y = i - 14 * c;
       T pv[16];
@@ -1088,7 +1088,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     if constexpr (sizeof(T) == 2) {
       // pool2 un-pooling, two channels per thread: every DYS write is one 32-bit (channel pair) store and
       // every DY2T write one 32-bit (column pair) store -- half the store instructions of 16-bit writes
-      if (tid < 200 && !(cb.ablate & 32)) {
+      if (tid < 200 && !ABLATED(cb.ablate, 32)) {
         const int n0 = 2 * (tid & 7), p = tid >> 3, py = p / 5, px = p % 5;
         float v[2][4];  // [channel][window]
 #pragma unroll
@@ -1122,7 +1122,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
         const int e = tid + 256 * r;
-        if (e >= 400 || (cb.ablate & 32)) break;
+        if (e >= 400 || ABLATED(cb.ablate, 32)) break;
         const int n = e & 15, p = e >> 4, py = p / 5, px = p % 5;  // channel fastest: conflict-free DYS writes
         const uint32_t code = valid ? cur.c[r] : 0u;  // code 0: ReLU blocked, every window gets 0
         const float g = to_f(cur.g[r]);
@@ -1145,7 +1145,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     //      Straight-line (constant trip counts, the ablation test outside the loop) with the next
     //      chunk's fragments loaded before this chunk's MFMAs: a runtime trip count kept the loop
     //      rolled and every chunk waited for its own LDS reads.
-    if (HW && !(cb.ablate & 64)) {
+    if (HW && !ABLATED(cb.ablate, 64)) {
       auto ld_a = [&](int kc) -> Frag {
         if constexpr (S::TRA) {
           // positions p0 .. p0 + 7 (row y = p0 / 16, columns x0 .. x0 + 7; x >= 10 reads DYS's zero padding) of
@@ -1230,7 +1230,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
       };
       const int x = min(row, 13);
       const T* bq = w2 + row * S::W2P + grp * KV;
-      if (HD && !(cb.ablate & 128)) {
+      if (HD && !ABLATED(cb.ablate, 128)) {
         if (np == 2) {
           const int y0 = 2 * q0, y1 = y0 + 2;
           const T* a0 = dys + ((y0 + 4) * 18 + x + 4) * 16;
@@ -1284,7 +1284,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     //      K = positions 0..927 (28 image rows + the zero row 28 that row-shifted A rows need)
     if constexpr (HD) {
       constexpr int CCH = 928 / KC, CPW = CCH / 4;  // chunks per wave: CPW, + 1 on waves < CCH % 4
-      if (!(cb.ablate & 512)) {
+      if (!ABLATED(cb.ablate, 512)) {
         auto ld_a = [&](int kc) { return M::load(dy1t + c_aoff + kc * KC + grp * KV); };
         auto ld_b = [&](int kc) { return M::load(xs + c_boff + kc * KC + grp * KV); };
         Frag a = ld_a(w), b = ld_b(w);
@@ -1347,13 +1347,8 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
 }  // namespace
 
 static int fwd_ipb(int B) { return std::min(MAX_IPB, std::max(1, (B + 1023) / 1024)); }
-static int default_bwd_target() {
-  static const int def = [] {
-    const char* e = std::getenv("MNIST_AMD_BWD_BLOCKS");  // tuning knob: default target block count
-    return e ? std::max(1, std::atoi(e)) : 512;  // 512 = one full round of 2 blocks/CU; 1024/768 measured slower
-  }();
-  return def;
-}
+// default conv_bwd workgroup target: 512 = one full round of 2 blocks/CU (1024 / 768 measured slower)
+static int default_bwd_target() { return 512; }
 
 static int bwd_ipb(int B, int target) {
   const int div = target > 0 ? target : default_bwd_target();
@@ -1385,11 +1380,8 @@ void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetC
 }
 
 bool lenet_fwd_head_applies(DType t, int B) {
-  static const int mode = [] {
-    const char* e = std::getenv("MNIST_AMD_FWD_HEAD");  // A/B knob: 0 = separate conv_fwd + head kernels
-    return e ? std::atoi(e) : 1;
-  }();
-  return mode != 0 && t == DType::BF16 && B >= FH_MIN_B && (B & 15) == 0;
+  // (the start-up calibration also times the separate conv_fwd + head kernels: Trainer::set_fwd_head)
+  return t == DType::BF16 && B >= FH_MIN_B && (B & 15) == 0;
 }
 
 int launch_lenet_fwd_head(DType t, const BatchRef& br, const LenetConvBuffers& cb, const HeadBuffers& hb, hipStream_t s) {
@@ -1400,10 +1392,7 @@ int launch_lenet_fwd_head(DType t, const BatchRef& br, const LenetConvBuffers& c
 }
 
 int launch_lenet_head16(DType t, const BatchRef& br, const HeadBuffers& hb, hipStream_t s) {
-  static const int maxb = [] {
-    const char* e = std::getenv("MNIST_AMD_HEAD16");  // largest batch for head16_kernel (A/B knob; 0 = never)
-    return e ? std::atoi(e) : 2048;
-  }();
+  constexpr int maxb = 2048;  // largest batch for head16_kernel (the LDS-staged head_kernel above it)
   if (t != DType::BF16 || br.B <= 0 || br.B > maxb) return 0;
   const int grid = (br.B + 15) / 16;
   hipLaunchKernelGGL(head16_kernel<bf16>, dim3(grid), dim3(512), 0, s, br, hb);
@@ -1411,17 +1400,10 @@ int launch_lenet_head16(DType t, const BatchRef& br, const HeadBuffers& hb, hipS
 }
 
 void launch_lenet_conv_bwd(DType t, const BatchRef& br, const LenetConvBuffers& cb, int* nslab_out, hipStream_t s,
-                           int mode, int target_blocks) {
+                           int target_blocks) {
   const int ipb = bwd_ipb(br.B, target_blocks), grid = (br.B + ipb - 1) / ipb;
   if (nslab_out) *nslab_out = grid;
   if (br.B <= 0) return;
-  if (t == DType::F32) {
-    if (mode == 1) hipLaunchKernelGGL((conv_bwd_kernel<float, 1>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
-    else if (mode == 2) hipLaunchKernelGGL((conv_bwd_kernel<float, 2>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
-    else hipLaunchKernelGGL((conv_bwd_kernel<float, 0>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
-  } else {
-    if (mode == 1) hipLaunchKernelGGL((conv_bwd_kernel<bf16, 1>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
-    else if (mode == 2) hipLaunchKernelGGL((conv_bwd_kernel<bf16, 2>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
-    else hipLaunchKernelGGL((conv_bwd_kernel<bf16, 0>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
-  }
+  if (t == DType::F32) hipLaunchKernelGGL((conv_bwd_kernel<float, 0>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
+  else hipLaunchKernelGGL((conv_bwd_kernel<bf16, 0>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
 }

@@ -54,32 +54,12 @@ int concurrent_mode() {
   }();
   return m;
 }
-// MNIST_AMD_SPLIT_BWD=1 (concurrent schedule only): conv_bwd runs as its two halves, the dgrad side on
-// the main stream and the conv2-wgrad side on the aux stream (lenet.hip MODE 1 / 2).  Bitwise equal to
-// the full kernel (tests/test_schedules_gpu.py) but measured SLOWER (0.184 vs 0.157 ms/step: the two
-// halves contend for the same LDS bandwidth and the dgrad half alone is only 15% shorter), so off.
-bool split_bwd() {
-  static const bool on = [] {
-    const char* e = std::getenv("MNIST_AMD_SPLIT_BWD");
-    return e ? std::atoi(e) != 0 : false;
-  }();
-  return on;
-}
-// XCD-contiguous work mapping of conv_fwd / head / conv_bwd / FC wgrad (common.h xcd_unit): on unless
-// MNIST_AMD_NO_XCD is set (A/B knob; the mapping changes which images a conv_bwd slab row sums, so the
-// conv gradients differ from the unmapped run by float summation order only)
-int xcd_map() {
-  static const int on = std::getenv("MNIST_AMD_NO_XCD") == nullptr ? 1 : 0;
-  return on;
-}
-// Deferred aux-branch join inside multi-step graphs (default on; MNIST_AMD_DEFER_JOIN=0 joins every step)
-bool defer_join() {
-  static const bool on = [] {
-    const char* e = std::getenv("MNIST_AMD_DEFER_JOIN");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return on;
-}
+// (Measured and removed: conv_bwd as two concurrent halves on two streams -- bitwise equal, but 0.184 vs
+// 0.157 ms/step: the halves contend for the same LDS bandwidth.)
+// XCD-contiguous work mapping of conv_fwd / head / conv_bwd / FC wgrad (common.h xcd_unit), always on
+constexpr int xcd_map() { return 1; }
+// Deferred aux-branch join inside multi-step graphs: the next step's head joins the FC branch
+constexpr bool defer_join() { return true; }
 // MNIST_AMD_TRACE=1: log every orchestration call of a step to stderr (host-side debugging)
 void trace(const char* what) {
   static const bool on = [] {
@@ -87,6 +67,19 @@ void trace(const char* what) {
     return e && *e == '1';
   }();
   if (on) { std::fputs(what, stderr); std::fputc('\n', stderr); std::fflush(stderr); }
+}
+// Diagnostic phase-skipping masks (launch.h ABLATED): honoured only by an ablation build; the normal build
+// refuses a set variable (a stale MNIST_AMD_ABLATE on a box must not train on skipped phases unnoticed)
+int ablation_mask(const char* var) {
+  const char* e = std::getenv(var);
+  const int m = e && *e ? std::atoi(e) : 0;
+#ifndef MNIST_AMD_ABLATION_BUILD
+  if (m != 0)
+    throw std::runtime_error(std::string(var) + " is set, but this build has no ablation switches (they skip kernel "
+                             "phases and give wrong results): unset it, or build with -DMNIST_AMD_ABLATION_BUILD "
+                             "(scripts/ablate.sh)");
+#endif
+  return m;
 }
 inline hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 template <typename P> P* ptr(uintptr_t v) { return reinterpret_cast<P*>(v); }
@@ -115,10 +108,24 @@ Trainer::Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const
 
 Trainer::~Trainer() {
   invalidate();
+  // after an abort a replay may still sit in a collective that never completes: its graph execs (leaked by
+  // invalidate), streams and events stay alive rather than being destroyed under it (the process is failing)
+  if (comm_ && comm_->aborted()) return;
   for (auto& e : events_) hipEventDestroy(e);
   if (comm_stream_) hipStreamDestroy(comm_stream_);
   if (aux_stream_) hipStreamDestroy(aux_stream_);
   if (zero_counter_) hipFree(zero_counter_);
+}
+
+void Trainer::release() {
+  // teardown order (DistContext.finalize): every graph that captured a collective is dropped -- after its
+  // replays drained -- before the communicator is destroyed, then the communicator reference is released
+  invalidate();
+  if (comm_ && !comm_->aborted()) {
+    (void)hipStreamSynchronize(comm_stream_);
+    (void)hipStreamSynchronize(aux_stream_);
+  }
+  comm_.reset();
 }
 
 int Trainer::pack_size() const { return model_pack_size(model_); }
@@ -138,6 +145,13 @@ void Trainer::sync_own_streams() {
 
 void Trainer::invalidate() {
   if (graphs_.empty()) return;
+  if (comm_ && comm_->aborted()) {
+    // a replay may be stuck in an aborted collective: leak the graph execs (as RcclComm::time_all_reduce
+    // does) instead of destroying them under it
+    graphs_.clear();
+    multi_k_ = 0;
+    return;
+  }
   // configuration changes only, never in the step loop
   sync_own_streams();
   for (auto& kv : graphs_) drop(kv.second);
@@ -183,11 +197,7 @@ HeadBuffers Trainer::head_buffers(float* metrics) const {
   hb.seed = seed_;
   hb.drop_p = drop_p_;
   hb.xcd = xcd_map();
-  static const int head_ablate = [] {
-    const char* e = std::getenv("MNIST_AMD_HEAD_ABLATE");
-    return e ? std::atoi(e) : 0;
-  }();
-  hb.ablate = head_ablate;
+  hb.ablate = ablation_mask("MNIST_AMD_HEAD_ABLATE");
   return hb;
 }
 
@@ -201,11 +211,7 @@ LenetConvBuffers Trainer::conv_buffers() const {
   cb.m2 = ptr<uint8_t>(p_.m2);
   cb.dp2 = ptr<const void>(p_.dp2);
   cb.slab = ptr<float>(p_.slab_conv);
-  static const int ablate = [] {
-    const char* e = std::getenv("MNIST_AMD_ABLATE");
-    return e ? std::atoi(e) : 0;
-  }();
-  cb.ablate = ablate;
+  cb.ablate = ablation_mask("MNIST_AMD_ABLATE");
   // stamps layout: launch.h STAMP_* (the conv kernels address their rows relative to STAMP_CONV_BWD)
   cb.stamps = p_.stamps ? ptr<unsigned long long>(p_.stamps) + STAMP_CONV_BWD * 16 : nullptr;
   return cb;
@@ -235,7 +241,7 @@ void Trainer::forward_backward(int B, uintptr_t stream) {
   launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s, hrows);
   post_launch(s);
   if (model_ == ModelKind::LENET) {
-    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), nullptr, s, 0, bwd_blocks_);
+    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), nullptr, s, bwd_blocks_);
     post_launch(s);
   }
 }
@@ -333,15 +339,8 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     HIP_CHECK(hipEventRecord(events_[4], s));
     HIP_CHECK(hipStreamWaitEvent(aux_stream_, events_[4], 0));
     int nslab = 0;
-    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s, split_bwd() ? 1 : 0, bwd_blocks_);
+    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s, bwd_blocks_);
     post_launch(s);
-    if (split_bwd()) {
-      launch_lenet_conv_bwd(dtype_, br, conv_buffers(), nullptr, aux_stream_, 2, bwd_blocks_);
-      post_launch(aux_stream_);
-      // the conv update (main) reads the conv2-wgrad columns this half writes, and the next conv_fwd
-      // overwrites the activations it reads: the main stream waits for it before either (events_[3])
-      HIP_CHECK(hipEventRecord(events_[3], aux_stream_));
-    }
     if (comm) {
       const int splits =
           launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, aux_stream_, hrows);
@@ -372,7 +371,6 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     // kernel reads): with defer_join it follows conv_bwd directly, the join moves to the next head
     if (defer_join) aux_pending_ = true;
     else HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));
-    if (defer_join && split_bwd()) HIP_CHECK(hipStreamWaitEvent(s, events_[3], 0));
     launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
                       nparam_, splits, cp, 0, cp, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
                       ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, ptr<int32_t>(p_.step), s);
@@ -397,7 +395,7 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
   post_launch(s);
   int nslab = 0;
   if (model_ == ModelKind::LENET) {  // serial single-GPU schedule (MNIST_AMD_CONCURRENT=0)
-    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s, 0, bwd_blocks_);
+    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s, bwd_blocks_);
     post_launch(s);
   }
   // no communicator: ONE fused reduce + SGD + pack kernel (2 boundaries fewer than reduce -> sgd)
@@ -466,7 +464,6 @@ void Trainer::launch_lenet_comm_tail(int B, int nslab, int splits, hipStream_t s
   launch_reduce(ptr<const float>(p_.slab_fc), nparam_, splits, cp, nparam_, scale, g, aux_stream_);
   post_launch(aux_stream_);
   HIP_CHECK(hipEventRecord(events_[5], aux_stream_));
-  if (split_bwd()) HIP_CHECK(hipStreamWaitEvent(s, events_[3], 0));  // conv2 columns come from the aux half
   if (plan_ == Plan::JOIN) {
     launch_reduce(ptr<const float>(p_.slab_conv), cp, nslab, 0, cp, scale, g, s);
     post_launch(s);

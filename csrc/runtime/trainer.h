@@ -119,6 +119,8 @@ class Trainer {
   bool has_graph(int n) const;
   void replay_n(uintptr_t stream, int n);
   void invalidate();        // drop every cached graph
+  // teardown: drop the graphs (they captured collectives), drain the side streams, detach the communicator
+  void release();
 
   int nparam() const { return nparam_; }
   int pack_size() const;

@@ -30,9 +30,9 @@ import torch
 
 from ..models import MODEL_IDS, build_model, flatten_state, unflatten_state
 from ..ops.native import require_gpu
+from ..parallel.comm import comm_timeout  # noqa: F401  (re-exported: watchdog deadline)
 
 PLANS = {"join": 0, "split": 1}
-STAMP_ROWS = 5120  # csrc/kernels/launch.h
 
 
 def resolve_plan(name: Optional[str]) -> Optional[str]:
@@ -86,11 +86,6 @@ class CollectiveError(RuntimeError):
     def __init__(self, msg: str, detected_after: float = 0.0):
         super().__init__(msg)
         self.detected_after = detected_after
-
-
-def comm_timeout() -> float:
-    """Watchdog deadline in seconds (``MNIST_AMD_COMM_TIMEOUT``, default 600 = c10d's NCCL default)."""
-    return float(os.environ.get("MNIST_AMD_COMM_TIMEOUT", "600"))
 
 
 HEAD_DIMS = {  # K0P, N1P, N2P  (csrc/kernels/models.h)
@@ -191,7 +186,7 @@ class NativeTrainer:
         P.xnext, P.ynext = ptr(self.xnext), ptr(self.ynext)
         # MNIST_AMD_STAMPS=1: per-workgroup phase timestamps (wall clock, 100 MHz), 16 slots per workgroup,
         # one row range per kernel (csrc/kernels/launch.h STAMP_*; later workgroups skip)
-        self.stamps = z(STAMP_ROWS * 16, dt=torch.int64) if os.environ.get("MNIST_AMD_STAMPS") else None
+        self.stamps = z(C.STAMP_ROWS * 16, dt=torch.int64) if os.environ.get("MNIST_AMD_STAMPS") else None
         P.stamps = ptr(self.stamps)
         self._ptrs = P
         self.rt = C.Trainer(mid, did, self.batch, self.ld_b, fc_splits, P)
@@ -436,11 +431,21 @@ class NativeTrainer:
         (:func:`~pytorch_ddp_mnist_amd.parallel.ddp.local_plan_candidates`).
         ``MNIST_AMD_MG_SCHED=join|split`` pins the multi-GPU plan.
 
-        48 timed replays per candidate (after 8 untimed rounds): with RCCL in the step the per-replay
-        times jitter with the collective's latency, and the median of 48 separates plans a few percent
-        apart.  At W = 1 this is ~15 ms of GPU work (~25 ms for the multi-GPU candidates at W = 8);
-        it also brings the GPU from idle to its sustained clock before the caller's warm-up steps
-        (measured: steps 1-20 after a cold start run ~6 % slower than steps 100+, scripts/step_times.py).
+        Sample plan (:meth:`time_schedules`, :func:`calib_blocks`): every candidate runs in segments of
+        consecutive k-step graph replays (blocks of up to 4 replays between two events, k =
+        ``MNIST_AMD_GRAPH_STEPS``) -- one untimed round over all candidates, then two timed rounds, the
+        second in reverse order -- so each candidate gets 2 x (segment - 1) timed samples (``replays_per_
+        candidate`` in the result; ``iters`` / ``warmup`` are accepted for API compatibility only).  The
+        median per candidate is max-reduced over the ranks.  The run also brings the GPU from idle to its
+        sustained clock before the caller's warm-up steps (measured: steps 1-20 after a cold start run ~6 %
+        slower than steps 100+, scripts/step_times.py).
+
+        At world >= 2 only plans whose capture pattern is the plain one (every collective and the update
+        on the main step stream: JOIN) are candidates unless ``MNIST_AMD_TRY_SPLIT=1``: the SPLIT plans put
+        kernels on a side stream behind a captured RCCL call, a pattern that has not run on a real
+        multi-GPU communicator yet (it made hipStreamEndCapture fail on ROCm 7.0 in a related form).
+        ``exposed_comm_ms`` is measured against the local schedule with the chosen plan's fwd_head /
+        conv_bwd-grid settings and the faster of the concurrent / serial single-GPU branch.
         """
         from ..parallel.ddp import (choose_plan, default_plan_candidates, local_plan_candidates,
                                     mlp_plan_candidates)
@@ -455,6 +460,8 @@ class NativeTrainer:
                     candidates = default_plan_candidates(self.C.conv_bwd_blocks(self.batch), ncu)
                 else:
                     candidates = mlp_plan_candidates()
+                if self.world > 1 and not os.environ.get("MNIST_AMD_TRY_SPLIT"):
+                    candidates = {k: v for k, v in candidates.items() if v.get("plan", "join") == "join"}
             elif self.model_name == "lenet5" and self.batch <= SMALL_BATCH_SERIAL:
                 # Small LeNet batches: the serial schedule, not calibrated.  run_steps measured serial 32.8 vs
                 # concurrent 35.0 us/step at B=128 (equal at 1024), but inside the calibration the serial
@@ -467,7 +474,16 @@ class NativeTrainer:
             else:
                 return {"chosen": "local", "timings_ms": {}}
         prefer = "join" if self.comm is not None else "concurrent"
-        extra = {"nocomm": {"comm": False, "concurrent": True}} if self.comm is not None else {}
+        extra = {}
+        if self.comm is not None:
+            # the local step without collectives, in both single-GPU branch forms: exposed communication is
+            # measured against the faster one (the concurrent branch is not the local best at every batch)
+            for conc in (True, False):
+                extra[f"nocomm{'' if conc else '_serial'}"] = {"comm": False, "concurrent": conc}
+        if len(candidates) == 1 and not extra:
+            chosen = next(iter(candidates))
+            self.apply_plan(candidates[chosen])
+            return {"chosen": chosen, "timings_ms": {}, "candidates": candidates, "single_candidate": True}
         timings = self.time_schedules({**candidates, **extra}, iters=iters, warmup=warmup, reduce_max=reduce_max)
         chosen = choose_plan({k: timings[k] for k in candidates}, prefer=prefer, margin=margin)
         self.apply_plan(candidates[chosen])
@@ -475,7 +491,9 @@ class NativeTrainer:
                "candidates": candidates, "replays_per_candidate": self.last_timing["replays"],
                "steps_per_replay": self.last_timing["graph_steps"], "interleaved": True}
         if extra:
-            out["exposed_comm_ms"] = round(timings[chosen] - timings["nocomm"], 4)
+            local = min(timings[k] for k in extra)
+            out["nocomm_ms"] = round(local, 4)
+            out["exposed_comm_ms"] = round(timings[chosen] - local, 4)
         if log is not None:
             log(out)
         return out
@@ -509,16 +527,25 @@ class NativeTrainer:
             colls.append({"params": [a, b], "bytes": 4 * (b - a), "allreduce_us": round(med * 1000.0, 2)})
         tm = (tune or {}).get("timings_ms", {})
         chosen = (tune or {}).get("chosen")
-        if chosen in tm and "nocomm" in tm:
-            plan_ms, local_ms = tm[chosen], tm["nocomm"]
+        if chosen in tm and "nocomm_ms" in (tune or {}):
+            plan_ms, local_ms = tm[chosen], tune["nocomm_ms"]
         else:
             cur = self.current_schedule()
-            t = self.time_schedules({"plan": cur, "nocomm": {"comm": False, "concurrent": True}}, iters=iters,
-                                    warmup=warmup, reduce_max=reduce_max)
-            plan_ms, local_ms = t["plan"], t["nocomm"]
+            loc = {"nocomm": {**cur, "comm": False, "concurrent": True},
+                   "nocomm_serial": {**cur, "comm": False, "concurrent": False}}
+            t = self.time_schedules({"plan": cur, **loc}, iters=iters, warmup=warmup, reduce_max=reduce_max)
+            plan_ms, local_ms = t["plan"], min(t["nocomm"], t["nocomm_serial"])
         return {"rccl_world": int(self.comm.world), "collectives": colls,
                 "step_plan_ms": round(plan_ms, 4), "step_local_ms": round(local_ms, 4),
                 "exposed_comm_us": round((plan_ms - local_ms) * 1000.0, 2)}
+
+    def release(self) -> None:
+        """Teardown (before the communicator is destroyed): drain the streams, drop every cached graph --
+        they captured collectives -- and detach the communicator.  The trainer can still run local steps."""
+        if self.comm is not None and not self.comm.aborted:
+            self.synchronize()
+        self.rt.release()
+        self.comm = None
 
     # ------------------------------------------------------------------ training
     def set_epoch_indices(self, indices: torch.Tensor) -> None:

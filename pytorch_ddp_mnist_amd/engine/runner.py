@@ -393,5 +393,5 @@ def run(cfg: TrainConfig, entry: str = "ddp_tutorial_cpu", show_banner: bool = F
         save_model(sd, cfg.save_path)
     metrics.close()
     if own_ctx:
-        ctx.finalize()
+        ctx.finalize(getattr(engine, "tr", None))  # trainer graphs -> RCCL communicator -> process group
     return {"history": history, "state_dict": sd, "rank": ctx.rank, "world": ctx.world}

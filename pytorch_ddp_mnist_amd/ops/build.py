@@ -71,10 +71,13 @@ def build_c(force: bool = False, jobs: int = 8) -> Path:
     headers = list(CSRC.rglob("*.h"))
     hip_srcs = sorted((CSRC / "kernels").glob("*.hip"))
     cpp_srcs = sorted((CSRC / "runtime").glob("*.cpp")) + [CSRC / "bindings.cpp"]
+    # MNIST_AMD_BUILD_DEFINES: extra -D flags of a diagnostic build (e.g. -DMNIST_AMD_ABLATION_BUILD for
+    # scripts/ablate.sh); part of the object-cache key, so switching back rebuilds the normal objects
+    defs = os.environ.get("MNIST_AMD_BUILD_DEFINES", "").split()
     hip_cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", f"-I{CSRC}",
-               "-Wno-unused-result"]
+               "-Wno-unused-result"] + defs
     cpp_cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}",
-               f"-I{CSRC}", "-fvisibility=hidden"] + _pybind_includes()
+               f"-I{CSRC}", "-fvisibility=hidden"] + defs + _pybind_includes()
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         futs = [ex.submit(_compile, s, headers, hip_cmd, force) for s in hip_srcs]
         futs += [ex.submit(_compile, s, headers, cpp_cmd, force) for s in cpp_srcs]

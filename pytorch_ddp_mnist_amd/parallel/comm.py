@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import datetime
 import os
+import sys
 from dataclasses import dataclass
 from typing import Optional
 
@@ -62,8 +63,19 @@ class DistContext:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return t.tolist()
 
-    def finalize(self) -> None:
-        """Clean teardown (the reference never calls its finalize(), survey Q16)."""
+    def finalize(self, *trainers) -> None:
+        """Clean teardown in a fixed order (the reference never calls its finalize(), survey Q16):
+        1. every trainer that captured collectives drops its graphs and detaches (``release``);
+        2. the RCCL communicator is flushed and destroyed (``ncclCommFinalize`` -> ``ncclCommDestroy``,
+           bounded; aborted if the flush does not complete);
+        3. the gloo control plane: barrier, ``destroy_process_group``."""
+        for tr in trainers:
+            if tr is not None and hasattr(tr, "release"):
+                tr.release()
+        if self.rccl is not None:
+            err = self.rccl.destroy(comm_timeout())
+            if err:
+                print(f"[rank {self.rank}] RCCL teardown: {err}", file=sys.stderr, flush=True)
         self.rccl = None
         if dist.is_available() and dist.is_initialized():
             try:
@@ -129,17 +141,44 @@ def init_distributed(method: Optional[str] = None, parallel: bool = True, device
     return ctx
 
 
-def make_rccl(ctx: DistContext):
-    """Native RCCL communicator; the unique id travels over the c10d TCPStore."""
+def comm_timeout() -> float:
+    """Collective watchdog deadline in seconds (``MNIST_AMD_COMM_TIMEOUT``, default 600 = c10d's NCCL default)."""
+    return float(os.environ.get("MNIST_AMD_COMM_TIMEOUT", "600"))
+
+
+def comm_init_timeout() -> float:
+    """Deadline of the RCCL bring-up (unique-id exchange + communicator init), ``MNIST_AMD_COMM_INIT_TIMEOUT``
+    seconds, default 180.  A healthy 8-GPU init takes about a second; past the deadline the rank aborts its
+    half-built communicator and raises, naming itself, so the launcher tears the job down instead of every
+    rank hanging inside ncclCommInitRank (reference: init_process_group's c10d timeout,
+    ddp_tutorial_multi_gpu.py:133-134)."""
+    return float(os.environ.get("MNIST_AMD_COMM_INIT_TIMEOUT", "180"))
+
+
+class CommInitError(RuntimeError):
+    """The RCCL bring-up did not complete (peer missing, stalled or failed)."""
+
+
+def make_rccl(ctx: DistContext, timeout_s: Optional[float] = None):
+    """Native RCCL communicator; the unique id travels over the c10d TCPStore.  Bounded: see
+    :func:`comm_init_timeout`."""
     from ..ops.native import load_c
     from ..utils.logging import native_stdout_to_stderr
     C = load_c()
+    timeout_s = comm_init_timeout() if timeout_s is None else float(timeout_s)
     store = dist.distributed_c10d._get_default_store()
     with native_stdout_to_stderr():  # RCCL's init banner goes to stderr
         if ctx.rank == 0:
             uid = C.RcclComm.make_unique_id()
             store.set(UID_KEY, uid)
         else:
-            store.wait([UID_KEY], datetime.timedelta(seconds=300))
+            try:
+                store.wait([UID_KEY], datetime.timedelta(seconds=timeout_s))
+            except Exception as e:  # noqa: BLE001 -- c10d raises its own store timeout types
+                raise CommInitError(f"rank {ctx.rank} of {ctx.world}: no RCCL unique id from rank 0 within "
+                                    f"{timeout_s:.0f} s ({e})") from e
             uid = store.get(UID_KEY)
-        return C.RcclComm(bytes(uid), ctx.rank, ctx.world, ctx.local_rank)
+        try:
+            return C.RcclComm(bytes(uid), ctx.rank, ctx.world, ctx.local_rank, init_timeout=timeout_s)
+        except RuntimeError as e:
+            raise CommInitError(str(e)) from e

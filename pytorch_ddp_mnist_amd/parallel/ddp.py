@@ -112,15 +112,30 @@ def model_phases(model: str) -> List[Tuple[int, int]]:
     return [(c, n), (0, c)]
 
 
+def coalesce_buckets(buckets: Sequence[Range]) -> List[Range]:
+    """Merge a bucket into the previous one when they are contiguous and belong to different backward
+    phases (the JOIN plan's one all-reduce of the coalesced slab; csrc/runtime/trainer.cpp
+    ``coalesced_buckets``).  Splits inside a phase come from an explicit cap and are kept."""
+    out: List[List[int]] = []
+    for p0, p1, ph in sorted(buckets, key=lambda b: b[0]):
+        if out and out[-1][1] == p0 and out[-1][2] != ph:
+            out[-1][1], out[-1][2] = p1, ph
+        else:
+            out.append([p0, p1, ph])
+    return [tuple(b) for b in out]
+
+
 class GlooReducer:
-    """DDP semantics for the torch-CPU engine: broadcast at init, bucketed mean all-reduce."""
+    """DDP semantics for the torch-CPU engine: broadcast at init, bucketed mean all-reduce.  With the
+    default per-phase plan the two phases are coalesced into ONE all-reduce per step, as the reference's
+    single 1 MiB-capped DDP bucket does (survey §2.7); a capped plan keeps its cap splits."""
 
     def __init__(self, module: torch.nn.Module, world: int, buckets: Optional[List[Range]] = None):
         self.module = module
         self.world = world
         self.params = [p for p in module.parameters()]
         self.numel = sum(p.numel() for p in self.params)
-        self.buckets = buckets or [(0, self.numel, 0)]
+        self.buckets = coalesce_buckets(buckets) if buckets else [(0, self.numel, 0)]
         if world > 1 and dist.is_initialized():
             with torch.no_grad():
                 flat = torch.cat([p.detach().reshape(-1) for p in self.params])

@@ -1,5 +1,11 @@
 #!/bin/bash
-# Phase ablation of the LeNet conv kernels: per-kernel time with phases skipped (diagnostic only).
+# Phase ablation of the LeNet conv kernels: per-kernel time with phases skipped (diagnostic only; WRONG
+# results).  Needs the ablation build, made on the CPU host BEFORE the GPU call, and the normal build back
+# afterwards:
+#   MNIST_AMD_BUILD_DEFINES=-DMNIST_AMD_ABLATION_BUILD python -m pytorch_ddp_mnist_amd.ops.build
+#   ... gpurun -- scripts/ablate.sh TAG ...
+#   python -m pytorch_ddp_mnist_amd.ops.build
+# (the normal build refuses MNIST_AMD_ABLATE / MNIST_AMD_HEAD_ABLATE)
 OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out
 TAG=${1:-abl}
 mkdir -p "$OUT"

@@ -1,8 +1,8 @@
 """Train a few LeNet-5 steps through the native step graph per variant and print parameter digests.
 
 Used by tests/test_schedules_gpu.py to check that every step schedule gives bitwise-identical
-parameters: serial / concurrent FC wgrad (MNIST_AMD_CONCURRENT, read once per process), conv_bwd
-as two concurrent halves (MNIST_AMD_SPLIT_BWD), and with a world-1 RCCL communicator the JOIN and
+parameters: serial / concurrent FC wgrad (MNIST_AMD_CONCURRENT, read once per process), and with a
+world-1 RCCL communicator the JOIN and
 SPLIT multi-GPU plans, with the default or a capped conv_bwd grid.  ``w2`` variants emulate the
 1/W arithmetic of a 2-rank job on one GPU (world set to 2 on a world-1 communicator, so every
 rank's "all-reduced" gradient is its own): they must equal a local run at half the learning rate
