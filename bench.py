@@ -71,6 +71,14 @@ def parse(argv=None):
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--comm-world1", action="store_true",
                     help="attach a world-1 RCCL communicator (runs the multi-GPU step schedule on one GPU)")
+    ap.add_argument("--data", default="synthetic", choices=["synthetic", "netcdf"],
+                    help="synthetic: the split is built in host memory and uploaded; netcdf (BASELINE config 3, the "
+                         "PnetCDF loader path): rank 0 writes the same split as CDF-5 files (native writer, the "
+                         "notebook's layout) into --data-dir, every rank loads them through the bulk reader "
+                         "(threaded pread -> pinned host memory -> hipMemcpyAsync) and the JSON reports load_s / "
+                         "load_GBps; the timed steps are the same")
+    ap.add_argument("--data-dir", default=None,
+                    help="directory of the --data netcdf files (default: $TMPDIR/mnist_amd_bench_nc)")
     ap.add_argument("--synthetic-mode", default="easy", choices=["easy", "hard"],
                     help="synthetic data generator (hard: stronger noise / affine jitter, top-1 below 1.0)")
     ap.add_argument("--eval", action="store_true", default=True)
@@ -147,6 +155,44 @@ def bench_data(world: int, rank: int, batch: int, total_steps: int, mode: str = 
     return torch.from_numpy(images), torch.from_numpy(labels), idx_all, test_x, test_y
 
 
+def netcdf_data(ctx, images, labels, data_dir, mode: str):
+    """BASELINE config 3 (the PnetCDF loader path): rank 0 writes the run's train split as a CDF-5 file (the
+    notebook's to_nc() layout, nb#c2:83-104, through the native writer), every rank then loads it through the
+    bulk reader -- threaded pread straight into pinned host memory, one hipMemcpyAsync to HBM
+    (data/device_loader.py upload_netcdf; reference: MNISTNetCDF + DataLoader per-sample reads,
+    mnist_pnetcdf_cpu_mp.py:18-49,370-409).  Returns the device tensors and the load figures (timed on every
+    rank, the max reported)."""
+    import torch
+
+    from pytorch_ddp_mnist_amd.data.cdf5 import write_mnist_nc
+    from pytorch_ddp_mnist_amd.data.device_loader import upload_netcdf
+    d = data_dir or os.path.join(os.environ.get("TMPDIR", "/tmp"), "mnist_amd_bench_nc")
+    path = os.path.join(d, f"mnist_train_images_{images.shape[0]}_{mode}.nc")
+    if ctx.rank == 0:
+        os.makedirs(d, exist_ok=True)
+        t0 = time.perf_counter()
+        tmp = f"{path}.tmp{os.getpid()}"
+        write_mnist_nc(tmp, images.numpy().reshape(-1, 28, 28), labels.numpy())
+        os.replace(tmp, path)
+        write_s = time.perf_counter() - t0
+    else:
+        write_s = 0.0
+    ctx.barrier()
+    sync = (lambda: torch.cuda.synchronize(ctx.device)) if ctx.device.type == "cuda" else (lambda: None)
+    sync()
+    t0 = time.perf_counter()
+    dx, dy = upload_netcdf(path, ctx.device)
+    sync()
+    load_s = ctx.all_reduce_max(time.perf_counter() - t0)
+    if dx.shape[0] != images.shape[0]:
+        raise RuntimeError(f"{path}: {dx.shape[0]} rows, expected {images.shape[0]}")
+    nbytes = dx.numel() + dy.numel()
+    info = {"source": "netCDF CDF-5 (native writer) -> threaded pread -> pinned -> hipMemcpyAsync",
+            "file": path, "rows": int(dx.shape[0]), "bytes": int(nbytes), "write_s": round(write_s, 4),
+            "load_s": round(load_s, 4), "load_GBps": round(nbytes / max(load_s, 1e-9) / 1e9, 3)}
+    return dx, dy, info
+
+
 def timed_region(ctx, tr, run, steps: int, cuda_sync, clock=time.perf_counter) -> float:
     """Time exactly ``steps`` steps on every rank; returns the max over ranks (seconds).
 
@@ -198,9 +244,14 @@ def main(argv=None) -> int:
     W, rank, dev = ctx.world, ctx.rank, ctx.device
 
     images, labels, idx_all, test_x, test_y = bench_data(W, rank, a.batch, a.warmup + a.steps, a.synthetic_mode)
+    load = None
+    if a.data == "netcdf":
+        images, labels, load = netcdf_data(ctx, images, labels, a.data_dir, a.synthetic_mode)
+    else:
+        images, labels = images.to(dev), labels.to(dev)
 
     torch.manual_seed(0)
-    tr = NativeTrainer(a.model, a.dtype, a.batch, images.to(dev), labels.to(dev), device=dev, lr=a.lr,
+    tr = NativeTrainer(a.model, a.dtype, a.batch, images, labels, device=dev, lr=a.lr,
                        momentum=a.momentum, dropout=dropout, init=build_model(a.model), max_indices=idx_all.numel())
     tr.set_buckets(plan_buckets(model_phases(a.model)))
     tr.set_epoch_indices(idx_all)
@@ -290,7 +341,7 @@ def main(argv=None) -> int:
         "vs_baseline": None,
         "dtype": a.dtype,
         "data": f"synthetic (MNIST-shaped 28x28 uint8, class-template + noise, mode={a.synthetic_mode}; "
-                "random-init weights)",
+                "random-init weights)" + ("; loaded from a CDF-5 netCDF file" if load else ""),
         "config": {
             "model": "LeNet-5" if a.model == "lenet5" else "MLP-784-128-128-10",
             "global_batch": n_gpus * a.batch,
@@ -306,6 +357,7 @@ def main(argv=None) -> int:
             "hipgraph": use_graph,
         },
         "rccl_world": comm.world if comm is not None else None,
+        "input": load or {"source": "in-memory synthetic split -> HBM (one copy)"},
         "comm_profile": prof,
         "top1": None if top1 is None else round(top1, 4),
         "train_loss_mean": round(train.mean_loss, 4),

@@ -135,3 +135,18 @@ def test_calibration_samples_stay_inside_the_loaded_order():
     assert calib_blocks(28, 20, True) == (True, 1, 4, 20)
     assert calib_blocks(468, 8, True) == (True, 4, 4, 32)
     assert calib_blocks(10, 8, False) == (False, 1, 12, 1)
+
+
+def test_bench_netcdf_data_roundtrip(tmp_path):
+    """bench.py --data netcdf: the split written as CDF-5 and read back through the bulk loader is the
+    in-memory split, byte for byte (CPU device: the same write + pread path, no HBM copy)."""
+    import torch
+
+    import bench
+    from pytorch_ddp_mnist_amd.parallel.comm import DistContext
+    images, labels, idx, _, _ = bench.bench_data(1, 0, 512, 20)
+    ctx = DistContext(0, 1, 0, torch.device("cpu"))
+    dx, dy, info = bench.netcdf_data(ctx, images, labels, str(tmp_path), "easy")
+    assert torch.equal(dx.view(-1, 784), images.view(-1, 784)) and torch.equal(dy, labels)
+    assert info["rows"] == images.shape[0] and info["bytes"] == images.numel() + labels.numel()
+    assert info["load_s"] > 0 and info["load_GBps"] > 0
