@@ -64,6 +64,10 @@ def parse(argv=None):
                     help="dropout after layer 1 (default: the reference's 0.2 for --model mlp; LeNet-5 has none)")
     ap.add_argument("--comm", default="rccl", choices=["rccl", "torch", "gloo"],
                     help="gradient data plane: native RCCL (default), c10d nccl, or c10d gloo via host memory")
+    ap.add_argument("--allreduce", default="rccl", choices=["rccl", "oneshot"],
+                    help="gradient data plane of the captured step: RCCL (default) or the one-shot xGMI all-reduce "
+                         "(every rank pushes its slice into every peer's IPC-mapped slot, then sums its own slots in "
+                         "rank order; parallel/oneshot.py).  With --comm gloo the ranks may share one GPU")
     ap.add_argument("--plan", default="auto", choices=["auto", "join", "split", "fixed"],
                     help="step plan: auto = time the candidates at start-up and keep the fastest "
                          "(multi-GPU plans, or the single-GPU schedules); join/split = that multi-GPU plan; "
@@ -256,7 +260,14 @@ def main(argv=None) -> int:
     tr.set_buckets(plan_buckets(model_phases(a.model)))
     tr.set_epoch_indices(idx_all)
     comm, rccl_version, tune, prof = None, None, None, None
-    external = a.comm in ("torch", "gloo") and W > 1
+    oneshot = None
+    external = a.comm in ("torch", "gloo") and W > 1 and a.allreduce != "oneshot"
+    if a.allreduce == "oneshot":
+        if a.comm == "torch":
+            raise SystemExit("--allreduce oneshot needs --comm rccl (RCCL kept for broadcast / comparison) or gloo")
+        from pytorch_ddp_mnist_amd.parallel.oneshot import make_oneshot
+        oneshot = make_oneshot(ctx, tr.nparam)
+        tr.attach_oneshot(oneshot, W)
     if external:
         import torch.distributed as dist
         if a.comm == "gloo":
@@ -267,9 +278,7 @@ def main(argv=None) -> int:
             dist.broadcast(tr.params, 0)
             tr.load_flat(tr.params.clone())
         tr.attach_external_allreduce(lambda t: dist.all_reduce(t), W, host=a.comm == "gloo")
-    elif W > 1 or a.comm_world1:
-        if a.comm != "rccl":
-            raise SystemExit("--comm-world1 needs --comm rccl")
+    elif (W > 1 or a.comm_world1) and a.comm == "rccl":
         from pytorch_ddp_mnist_amd.ops.native import load_c
         C = load_c()
         comm = ctx.rccl
@@ -279,7 +288,15 @@ def main(argv=None) -> int:
                 comm = C.RcclComm(bytes(C.RcclComm.make_unique_id()), 0, 1, ctx.local_rank)
         rccl_version = C.rccl_version()
         tr.attach_comm(comm, W)
+        if oneshot is not None:
+            tr.attach_oneshot(oneshot, W)  # the step's collectives; RCCL broadcasts and is timed for comparison
         tr.broadcast_params(0)
+        if pinned is not None:
+            tr.set_plan(pinned)
+    elif a.comm_world1:
+        raise SystemExit("--comm-world1 needs --comm rccl")
+    elif oneshot is not None:
+        tr.broadcast_params(0)  # over the c10d control plane
         if pinned is not None:
             tr.set_plan(pinned)
 
@@ -293,7 +310,7 @@ def main(argv=None) -> int:
         # the external data plane runs the eager phase API (forward_backward -> host all-reduce -> SGD), not
         # the captured schedules a calibration would time: nothing to choose
         tune = {"chosen": "eager-phases", "timings_ms": {}, "note": "external data plane: no graph schedules"}
-    if comm is not None and use_graph:
+    if (comm is not None or oneshot is not None) and use_graph:
         prof = tr.comm_profile(reduce_max=ctx.all_reduce_max, tune=tune)
 
     def run(n):
@@ -318,7 +335,10 @@ def main(argv=None) -> int:
 
     n_gpus = comm.world if comm is not None else W
     info = tr.plan_info()
-    if comm is not None:
+    if oneshot is not None:
+        colls = " + ".join(f"{c['bytes'] // 1024} KiB" for c in info["collectives"])
+        comm_desc = f"one-shot xGMI all-reduce (IPC peer slots, fixed rank order), plan={info['plan']}: {colls} per step"
+    elif comm is not None:
         colls = " + ".join(f"{c['bytes'] // 1024} KiB" for c in info["collectives"])
         comm_desc = f"native RCCL {rccl_version}, plan={info['plan']}: all-reduce {colls} per step"
     elif external:
@@ -357,6 +377,7 @@ def main(argv=None) -> int:
             "hipgraph": use_graph,
         },
         "rccl_world": comm.world if comm is not None else None,
+        "allreduce": "oneshot" if oneshot is not None else ("rccl" if comm is not None else None),
         "input": load or {"source": "in-memory synthetic split -> HBM (one copy)"},
         "comm_profile": prof,
         "top1": None if top1 is None else round(top1, 4),

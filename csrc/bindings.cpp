@@ -153,10 +153,32 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("world", &RcclComm::world);
 
+  py::class_<OneShotAllReduce, std::shared_ptr<OneShotAllReduce>>(m, "OneShotAllReduce")
+      .def(py::init<int, int, int, int, int, double>(), py::arg("rank"), py::arg("world"), py::arg("device"),
+           py::arg("max_count"), py::arg("nblk") = 64, py::arg("timeout") = 30.0)
+      .def("handle", [](const OneShotAllReduce& o) { return py::bytes(o.handle()); })
+      .def("open_peers",
+           [](OneShotAllReduce& o, const std::vector<py::bytes>& hs) {
+             std::vector<std::string> v;
+             for (const auto& h : hs) v.emplace_back(std::string(h));
+             o.open_peers(v);
+           })
+      .def("all_reduce_sum_f32",
+           [](OneShotAllReduce& o, uintptr_t buf, size_t n, uintptr_t s) {
+             o.all_reduce_sum_f32(reinterpret_cast<float*>(buf), n, reinterpret_cast<hipStream_t>(s));
+           })
+      .def("check", &OneShotAllReduce::check)
+      .def_property_readonly("rank", &OneShotAllReduce::rank)
+      .def_property_readonly("world", &OneShotAllReduce::world)
+      .def_property_readonly("max_count", &OneShotAllReduce::max_count)
+      .def_property_readonly("ready", &OneShotAllReduce::ready);
+
   py::class_<Trainer>(m, "Trainer")
       .def(py::init<int, int, int, int, int, const TrainerPtrs&>(), py::arg("model"), py::arg("dtype"),
            py::arg("batch"), py::arg("ld_b"), py::arg("fc_splits"), py::arg("ptrs"))
       .def("set_comm", &Trainer::set_comm)
+      .def("set_oneshot", &Trainer::set_oneshot)
+      .def_property_readonly("has_oneshot", &Trainer::has_oneshot)
       .def("set_world", &Trainer::set_world)
       .def("set_optimizer", &Trainer::set_optimizer)
       .def("set_dropout", &Trainer::set_dropout)

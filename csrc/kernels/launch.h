@@ -140,6 +140,12 @@ void launch_lenet_conv_bwd(DType t, const BatchRef& br, const LenetConvBuffers& 
 int lenet_conv_bwd_blocks(int B, int target_blocks = 0);
 int lenet_conv_bwd_max_blocks(int B, int target_blocks = 0);  // slab rows needed for any batch <= B
 
+// One-shot all-reduce over xGMI peer memory (oneshot.hip; host side csrc/runtime/oneshot.h): in-place SUM of
+// `count` floats at buf; peer_data / peer_flags are device tables of every rank's receive region.
+void launch_oneshot_allreduce(float* buf, int count, int rank, int world, int max_count, float* const* peer_data,
+                              uint32_t* const* peer_flags, uint32_t* seq, uint32_t* err, int nblk,
+                              unsigned long long timeout_ticks, hipStream_t s);
+
 // grad[p] = scale * sum_s slab[s][p]  for p in [p0, p1)
 void launch_reduce(const float* slab, int slab_ld, int nslab, int p0, int p1, float scale, float* grad,
                    hipStream_t s);

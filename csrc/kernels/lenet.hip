@@ -91,7 +91,15 @@ struct FwdSmem {
   static constexpr int W2P = 232;                                          // C2F row pitch (224 + 8)
   // conv2's B operand: registers for bf16 (7 chunks = 28 VGPRs), an LDS image for f32 (13 chunks)
   static constexpr bool W2LDS = sizeof(T) != 2;
-  static constexpr int OFF_W2 = rup(OFF_M2 + 400, 16);                     // [16][W2P] T  conv2 B operand
+  // junk words: the epilogue stores of lanes without an output (padding columns / channels) go here instead of
+  // being branched around -- branch-free epilogues let the compiler count lgkmcnt exactly, so a tile's MFMAs do
+  // not wait for the previous tile's epilogue stores (a store inside an exec-masked branch forced lgkmcnt(0))
+  // The junk area covers every per-tile offset of the conv1 epilogue (6 tiles x 2*14*8 elements beyond a lane's
+  // base) plus the 64 lanes' bases, so an invalid lane's store address is its own junk base plus the SAME
+  // immediate offset a valid lane uses.
+  static constexpr int JUNK_BYTES = rup((6 * 2 * 14 * 8 + 64) * (int)sizeof(T), 16);
+  static constexpr int OFF_JUNK = rup(OFF_M2 + 400, 16);                   // junk stores
+  static constexpr int OFF_W2 = OFF_JUNK + JUNK_BYTES;                     // [16][W2P] T  conv2 B operand
   static constexpr int TOTAL = W2LDS ? rup(OFF_W2 + 16 * W2P * (int)sizeof(T), 16) : OFF_W2;
 };
 
@@ -203,22 +211,27 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
     }
   }
   const bool c1valid = 4 * w + grp < 14;  // wave 3, lane groups 2-3: padding columns 14, 15
-  auto c1_epi = [&](int t, const f32x4& acc) {  // pool + bias + ReLU, staged in LDS
-    const int n = row & 7, pp = (2 * t + (row >> 3)) * 14 + 4 * w + grp;
+  // Branch-free epilogues: a lane without an output (padding column / channel) stores into the junk area.  Each
+  // store address is a per-lane base (real or junk, chosen ONCE) plus a per-tile immediate offset, so the 7
+  // tiles' stores need 3 address registers, not 21, and no exec-masked branch breaks the lgkmcnt counting.
+  char* junk = smem + S::OFF_JUNK + (int)sizeof(T) * lane;
+  const int n1 = row & 7;
+  const bool st1 = c1valid && n1 < 6;
+  T* const e1_p1s = c1valid ? p1s + ((row >> 3) * 14 + 4 * w + grp) * 8 + n1 : reinterpret_cast<T*>(junk);
+  T* const e1_p1c = st1 ? p1c + n1 * P1CP + (row >> 3) * 16 + 4 * w + grp : reinterpret_cast<T*>(junk);
+  uint8_t* const e1_m1s = st1 ? m1s + n1 * M1CP + (row >> 3) * 16 + 4 * w + grp : reinterpret_cast<uint8_t*>(junk);
+  auto c1_epi = [&](int t, const f32x4& acc) {  // pool + bias + ReLU, staged in LDS (pooled row 2t + r)
     float mx = acc[0];
     int am = 0;
 #pragma unroll
     for (int i = 1; i < 4; ++i)
       if (acc[i] > mx) { mx = acc[i]; am = i; }
     const float pre = mx + bias1;
-    if (c1valid) {
-      const T v = to_t<T>(n < 6 ? fmaxf(pre, 0.f) : 0.f);
-      p1s[pp * 8 + n] = v;
-      if (TRAIN && n < 6) {
-        const int yx = (2 * t + (row >> 3)) * 16 + 4 * w + grp;  // CHW16 position
-        p1c[n * P1CP + yx] = v;
-        m1s[n * M1CP + yx] = (uint8_t)(am | (pre > 0.f ? 4 : 0));
-      }
+    const T v = to_t<T>(n1 < 6 ? fmaxf(pre, 0.f) : 0.f);
+    e1_p1s[t * 2 * 14 * 8] = v;
+    if (TRAIN) {
+      e1_p1c[t * 2 * 16] = v;
+      e1_m1s[t * 2 * 16] = (uint8_t)(am | (pre > 0.f ? 4 : 0));
     }
   };
   auto c2_base = [&](int mt) {  // im2col row of tile mt for this lane: pooled position x window element
@@ -235,7 +248,9 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
     return M::load(p1s + base + (kh * 14 + kw) * 8 + c0);
   };
   // NT tiles (1 or 2) sharing the B fragments, next chunk's A fragments in flight during this chunk's
-  // MFMAs (the rolled-up form waited for every A read before its MFMA)
+  // MFMAs (the rolled-up form waited for every A read before its MFMA).  (Measured: reading every A fragment
+  // of the tiles first -- 14 reads in flight, 56 VGPRs -- pushed the fused kernel past 128 VGPRs into
+  // scratch spills inside the image loop.)
   auto c2_acc = [&](auto ntc, const int* mts, f32x4* acc) {
     constexpr int NT = decltype(ntc)::value;
     int base[NT];
@@ -259,19 +274,18 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
       for (int j = 0; j < NT; ++j) a[j] = an[j];
     }
   };
-  auto c2_epi = [&](int t, bool valid, int mt, const f32x4& acc) {
-    const int n = row, pp = mt * 4 + grp;
-    if (pp < 25) {
-      float mx = acc[0];
-      int am = 0;
+  auto c2_epi = [&](int t, bool valid, int mt, const f32x4& acc) {  // branch-free: pp >= 25 stores to junk
+    const int n = row, pp = min(mt * 4 + grp, 24);
+    const bool live = mt * 4 + grp < 25;
+    float mx = acc[0];
+    int am = 0;
 #pragma unroll
-      for (int i = 1; i < 4; ++i)
-        if (acc[i] > mx) { mx = acc[i]; am = i; }
-      const float pre = mx + bias2;
-      if constexpr (XROWS) xrows[t * XPITCH + n * 25 + pp] = to_t<T>(valid ? fmaxf(pre, 0.f) : 0.f);
-      else p2s[n * 25 + pp] = to_t<T>(fmaxf(pre, 0.f));
-      m2s[n * 25 + pp] = (uint8_t)(am | (pre > 0.f ? 4 : 0));
-    }
+    for (int i = 1; i < 4; ++i)
+      if (acc[i] > mx) { mx = acc[i]; am = i; }
+    const float pre = mx + bias2;
+    if constexpr (XROWS) *(live ? xrows + t * XPITCH + n * 25 + pp : reinterpret_cast<T*>(junk)) = to_t<T>(valid ? fmaxf(pre, 0.f) : 0.f);
+    else *(live ? p2s + n * 25 + pp : reinterpret_cast<T*>(junk)) = to_t<T>(fmaxf(pre, 0.f));
+    *(live ? m2s + n * 25 + pp : reinterpret_cast<uint8_t*>(junk)) = (uint8_t)(am | (pre > 0.f ? 4 : 0));
   };
   auto flush_p2 = [&](int bprev) {  // previous image's pool2 outputs -> HBM (16-byte stores)
     if (bprev >= 0 && bprev < br.B) {
@@ -332,11 +346,16 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
           *reinterpret_cast<uint4*>(dst + (4 * sh + q) * S::XP) = o;
         }
       } else {
+        // bit blend instead of `sh ? f[i + 4 + q] : f[i + q]`: hipcc turned that select into a lane-indexed
+        // load of f[] from scratch memory (80 B/lane of scratch traffic per image)
+        const uint32_t msk = 0u - (uint32_t)sh;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           float o[8];
 #pragma unroll
-          for (int i = 0; i < 8; ++i) o[i] = sh ? f[i + 4 + q] : f[i + q];
+          for (int i = 0; i < 8; ++i)
+            o[i] = __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, f[i + q]) & ~msk) |
+                                                 (__builtin_bit_cast(uint32_t, f[i + 4 + q]) & msk));
           float* d = reinterpret_cast<float*>(dst) + (4 * sh + q) * S::XP;
           *reinterpret_cast<f32x4*>(d) = f32x4{o[0], o[1], o[2], o[3]};
           *reinterpret_cast<f32x4*>(d + 4) = f32x4{o[4], o[5], o[6], o[7]};
@@ -410,7 +429,8 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
 }
 
 template <typename T, bool TRAIN>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void conv_fwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
+// (f32: its ~64 KB of LDS allows 2 workgroups per CU anyway, so it may use up to 256 VGPRs instead of spilling)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 2 ? 4 : 2))) void conv_fwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
   __shared__ __attribute__((aligned(16))) char smem[FwdSmem<T>::TOTAL];
   const int unit = xcd_unit(blockIdx.x, gridDim.x, br.xcd);  // this workgroup's images: [unit * ipb, +ipb)
   conv_fwd_images<T, TRAIN>(br, cb, unit * ipb, ipb, smem, threadIdx.x, wave_id(), threadIdx.x == 0, nullptr);
@@ -787,24 +807,19 @@ __global__ __launch_bounds__(512) void head16_kernel(BatchRef br, HeadBuffers hb
 // LDS images chosen so that every MFMA operand fragment is ONE aligned 16-byte read:
 //   XS  [5][32][32]     xs[kw][y][x]  = xpad[y][x+kw]          conv1 wgrad B (im2col^T rows), + a ones plane
 //   P1T [5][6][14][16]  p1t[kw][c][y][x] = pool1[y][x+kw][c]   conv2 wgrad B
-//   DY2T[16][10*16]     conv2 pre-act grad, channel-major, rows padded 10->16   conv2 wgrad A
+//   DY2T[16][10*16]     (fp32 only) conv2 pre-act grad, channel-major, rows padded 10->16   conv2 wgrad A
 //   DYS [18][18][16]    same grad, position-major (NHWC), zero border of 4 so the full-correlation
 //                       dgrad reads it without bounds checks                     conv2 dgrad A
-//   W2  [16][424]       packed conv2 dgrad operand (C2d)                         conv2 dgrad B
+//                       (bf16: also the conv2 wgrad A operand, read with transposing ds_read_b64_tr_b16)
+//   W2  [16][496]       packed conv2 dgrad operand (C2d) for two output rows     conv2 dgrad B
 //   DY1T[8][28*32]      conv1 pre-act grad, channel-major, rows padded 28->32    conv1 wgrad A
 //                       (zero prefix + >= one zero image row after each channel: the wgrad reads
 //                       rows y - 1 .. y + 1 of it, see phase C)
 // The pool1 un-pooling (argmax + ReLU) is fused into the conv2-dgrad epilogue, which writes DY1T
 // directly; pool2 un-pooling is a cooperative scatter.  Both scatters write every position of
 // their map (2x2 windows tile it), so nothing but the padding is ever zero-filled.
-// MODE splits the kernel into two independent halves that run CONCURRENTLY on two streams, with the
-// block -> images mapping and per-block accumulation order of MODE 0 (so the slab rows are bitwise
-// those of the full kernel; each half writes its own columns):
-//   MODE 0 full | MODE 1 dgrad side (XS, DYS, W2R, DY1T, M1: conv2 dgrad, pool1 un-pooling, conv1
-//   wgrad) | MODE 2 conv2-wgrad side (P1T, DY2T: 21 KB of LDS, fills the room MODE 1 leaves per CU)
-template <typename T, int MODE = 0>
+template <typename T>
 struct BwdSmem {
-  static constexpr bool HD = MODE != 2, HW = MODE != 1;  // dgrad side / conv2-wgrad side present
   // pitches padded so the fragment reads and the un-pooling scatters are <= 2-way bank
   // conflicted (measured 60% conflict cycles with the unpadded 1024/224/160/896 pitches)
   // W2R: conv2 dgrad B operand for TWO output rows per tile, [16 = (r, c)][30 taps x 16 ch + pad]
@@ -820,30 +835,65 @@ struct BwdSmem {
   static constexpr int ONES = 5 * XP + 120, ONES_N = 944;
   static constexpr int XS_N = ONES + ONES_N, PPL = 32;
   static constexpr int OFF_XS = 0;
-  static constexpr int OFF_P1T = rup(OFF_XS + (HD ? XS_N * (int)sizeof(T) : 0), 16);
-  // TRA (full kernel, bf16): the conv2 wgrad reads its A operand (channel-major dY2) straight from the
-  // position-major DYS image with ds_read_b64_tr_b16 (transposing LDS reads), so there is no DY2T image
-  // and no second un-pooling scatter
-  static constexpr bool TRA = MODE == 0 && sizeof(T) == 2;
-  static constexpr bool DY2 = HW && !TRA;
-  static constexpr int OFF_DY2T = rup(OFF_P1T + (HW ? PPL * P1P * (int)sizeof(T) : 0), 16);
+  static constexpr int OFF_P1T = rup(OFF_XS + XS_N * (int)sizeof(T), 16);
+  // TRA (bf16): the conv2 wgrad reads its A operand (channel-major dY2) straight from the position-major
+  // DYS image with ds_read_b64_tr_b16 (transposing LDS reads), so there is no DY2T image and no second
+  // un-pooling scatter
+  static constexpr bool TRA = sizeof(T) == 2;
+  static constexpr bool DY2 = !TRA;
+  static constexpr int OFF_DY2T = rup(OFF_P1T + PPL * P1P * (int)sizeof(T), 16);
   static constexpr int OFF_DYS = rup(OFF_DY2T + (DY2 ? 16 * D2P * (int)sizeof(T) : 0), 16);  // [18][18][16] zero-padded
-  static constexpr int OFF_W2 = rup(OFF_DYS + (HD ? 18 * 18 * 16 * (int)sizeof(T) : 0), 16);
-  static constexpr int OFF_DY1T = rup(OFF_W2 + (HD ? 16 * W2P * (int)sizeof(T) : 0), 16);
-  static constexpr int OFF_M1 = rup(OFF_DY1T + (HD ? (D1PRE + 8 * D1P) * (int)sizeof(T) : 0), 16);  // [6][M1CP] u8 pool1 codes
-  static constexpr int TOTAL = rup(OFF_M1 + (HD ? M1IMG : 0), 16);
-  static constexpr int OFF_RED = OFF_XS;  // [4][256] f32 scratch after the image loop (dgrad side)
-  static_assert(!HD || 4 * 256 * 4 <= XS_N * (int)sizeof(T), "reduction scratch must fit in the aliased XS region");
+  static constexpr int OFF_W2 = rup(OFF_DYS + 18 * 18 * 16 * (int)sizeof(T), 16);
+  static constexpr int OFF_DY1T = rup(OFF_W2 + 16 * W2P * (int)sizeof(T), 16);
+  static constexpr int OFF_M1 = rup(OFF_DY1T + (D1PRE + 8 * D1P) * (int)sizeof(T), 16);  // [6][M1CP] u8 pool1 codes
+  static constexpr int TOTAL = rup(OFF_M1 + M1IMG, 16);
+  static constexpr int OFF_RED = OFF_XS;  // [NW][256] f32 scratch after the image loop
+  static_assert(8 * 256 * 4 <= XS_N * (int)sizeof(T), "reduction scratch must fit in the aliased XS region");
   static_assert(D1P >= 928 && 4 * XP + 4 * 32 + 928 <= ONES, "phase C reads stay inside zeroed rows");
 };
 
-template <typename T, int MODE>
-__global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
+// Per-image thread roles and the phase-B work split of conv_bwd_kernel, by workgroup size (NW waves).
+// NW = 4 (256 threads, the round-1..3 layout): every wave stages, every wave computes both GEMMs of phase B.
+// NW = 8 (512 threads, two workgroups = 16 waves per CU at the same LDS footprint): the staging roles and the
+// two phase-B GEMMs are on DIFFERENT waves -- waves 0-3 the conv2 dgrad (row pairs {2,2,2,1}), waves 4-7 the
+// conv2 wgrad (tiles {3,3,2,2}) -- so twice as many independent LDS / MFMA chains are in flight per CU and the
+// longest per-wave chain of a phase is 30 MFMAs instead of 45.
+template <typename T, int NW>
+struct BwdRoles {
+  static constexpr int NT = NW * 64;
+  static constexpr bool W8 = NW == 8;
+  // phase A staging roles (thread ranges)
+  static constexpr int XS_T0 = 0, XS_N = 112;                 // input row y, column chunk -> 5 XS planes
+  static constexpr int M1_T0 = W8 ? 128 : 112, M1_N = M1IMG / 16;  // 16-byte chunks of the pool1 codes
+  static constexpr int P1_T0 = W8 ? 256 : 128, P1_N = 84;     // pool1 row (c, y) -> 5 shifted P1T rows
+  static constexpr int DS_T0 = W8 ? 312 : 0, DS_N = 200;      // bf16 pool2 un-pooling: (channel pair, position)
+  static constexpr int F_T0 = W8 ? 112 : 0, F_ITEMS = W8 ? 1 : 2;  // f32 un-pooling: items per thread
+  // waves that load each role's next-image inputs (wave-uniform: a wave without the role issues none)
+  static DEV bool loads_px(int w) { return !W8 || w < 2; }
+  static DEV bool loads_m1(int w) { return !W8 || (w >= 2 && w < 4); }
+  static DEV bool loads_p1(int w) { return !W8 || (w >= 4 && w < 6); }
+  static DEV bool loads_p2(int w) { return !W8 || (sizeof(T) == 2 ? w >= 4 : w >= 1); }
+  // phase B: dgrad row pairs [q0, q0 + np) of 7 (np = 0: no dgrad on this wave); wgrad tiles [n0w, n0w + nw)
+  static DEV int dg_np(int w) { return W8 ? (w < 3 ? 2 : (w == 3 ? 1 : 0)) : (w < 3 ? 2 : 1); }
+  static DEV int dg_q0(int w) { return W8 ? (w < 4 ? 2 * w : 0) : 2 * w; }
+  static DEV int wg_nw(int w) {
+    if (W8) return w < 4 ? 0 : (w < 6 ? 3 : 2);
+    return w < 2 ? 2 : 3;
+  }
+  static DEV int wg_n0(int w) {
+    if (W8) return w < 4 ? 0 : (w < 6 ? 3 * (w - 4) : 6 + 2 * (w - 6));
+    return w < 2 ? 2 * w : 4 + 3 * (w - 2);
+  }
+};
+
+template <typename T, int NW>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 8 ? 4 : 1)))
+void conv_bwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
   using M = Mma<T>;
   using Frag = typename M::Frag;
-  using S = BwdSmem<T, MODE>;
-  constexpr bool HD = S::HD, HW = S::HW;
-  constexpr int KV = M::KV, KC = M::KC;
+  using S = BwdSmem<T>;
+  using R = BwdRoles<T, NW>;
+  constexpr int KV = M::KV, KC = M::KC, NT = R::NT;
   __shared__ __attribute__((aligned(16))) char smem[S::TOTAL];
   T* xs = reinterpret_cast<T*>(smem + S::OFF_XS);
   T* p1t = reinterpret_cast<T*>(smem + S::OFF_P1T);
@@ -862,59 +912,80 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   // optional wall-clock stamps (profiling): [0] start, [1] setup, 3 per image for images 0..3,
   // [14] loop end, [15] slab written
   auto stamp = [&](int k) {
-    if (cb.stamps && tid == 0 && blockIdx.x < 512) cb.stamps[(blockIdx.x + (MODE == 2 ? 512 : 0)) * 16 + k] = wall_clock64();
+    if (cb.stamps && tid == 0 && blockIdx.x < 512) cb.stamps[blockIdx.x * 16 + k] = wall_clock64();
   };
   stamp(0);
 
   // ---- software pipeline: every global input of image t+1 is loaded into registers while
   //      image t computes (phases B and C), so phase A only moves registers into LDS
-  // Phase-A thread roles (every LDS image is written with 16-byte stores, source rows prefetched):
-  //   tid [0, 112)   : input row y = tid/4, column chunk g = tid%4 -> its chunk of the 5 shifted XS planes
-  //   tid [112, 202) : 16-byte chunk tid-112 of the CHW16 pool1 codes -> M1
-  //   tid [128, 212) : pool1 channel c, row y ((tid-128) = c*14 + y) -> its row of the 5 shifted P1T planes
+  // Phase-A thread roles (BwdRoles; every LDS image is written with 16-byte stores, source rows prefetched):
+  //   XS : input row y = tid/4, column chunk g = tid%4 -> its chunk of the 5 shifted XS planes
+  //   M1 : 16-byte chunk of the CHW16 pool1 codes -> M1
+  //   P1 : pool1 channel c, row y (c*14 + y) -> its row of the 5 shifted P1T planes
+  //   DS : pool2 un-pooling scatter into DYS (/ DY2T)
   constexpr int PV = 16 * (int)sizeof(T) / 16;  // uint4 per CHW16 pool1 row (2 bf16 / 4 f32)
+  // Prefetch registers, one slot range per role: input pixels (4 dwords, image columns [8g-4, 8g+12) of row
+  // y-2), pool1 codes (one uint4), pool1 row (PV uint4), and the un-pooling items (codes c[2], raw grads g[2]).
+  // Where no thread has two of the XS / M1 / P1 roles (bf16, 8 waves) those share ONE slot range (a
+  // register union: 12 dwords instead of 20, so the 8-wave kernel fits 128 VGPRs).
+  constexpr bool UNION = NW == 8 && sizeof(T) == 2;
+  constexpr int O_PX = 0, O_M1 = UNION ? 0 : 4, O_P1 = UNION ? 0 : 8, O_DS = O_P1 + 4 * PV, NREG = O_DS + 4;
   struct Pre {
-    uint32_t u[4];    // input pixels, image columns [8g-4, 8g+12) of row y-2
-    uint4 p[PV];      // pool1 row (16 positions of one channel)
-    uint4 m;          // 16 pool1 codes
-    uint32_t c[2];    // pool2 codes for scatter items tid, tid + 256
-    T g[2];           // pool2 grads (raw; converted where used, so no load result is needed at issue)
+    uint32_t r[NREG];
+    DEV uint4 q(int o) const { return make_uint4(r[o], r[o + 1], r[o + 2], r[o + 3]); }
+    DEV void setq(int o, const uint4& v) { r[o] = v.x; r[o + 1] = v.y; r[o + 2] = v.z; r[o + 3] = v.w; }
+    DEV uint32_t code(int k) const { return r[O_DS + k]; }
+    DEV T grad(int k) const {
+      if constexpr (sizeof(T) == 2) return __builtin_bit_cast(T, (unsigned short)r[O_DS + 2 + k]);
+      else return __builtin_bit_cast(T, r[O_DS + 2 + k]);
+    }
   };
-  // Branch-free: every lane issues the same loads (addresses clamped into range, values of lanes
-  // without the role / of images past the batch zeroed at use), so vmcnt accounting stays exact.
+  // Branch-free inside a wave: every lane of a loading wave issues the same loads (addresses clamped into
+  // range, values of lanes without the role / of images past the batch zeroed at use), so vmcnt
+  // accounting stays exact; waves without a role (wave-uniform test) issue none of its loads.
   auto fetch = [&](int t) -> Pre {
     Pre f;
+#pragma unroll
+    for (int k = 0; k < NREG; ++k) f.r[k] = 0u;
     const bool live = t < ipb && unit * ipb + t < br.B;  // wave-uniform
     const int bb = min(unit * ipb + t, br.B - 1);
-    if constexpr (HD) {
-      const uint8_t* rowp = br.images + (size_t)bidx[live ? t : 0] * 784 + ((tid >> 2) % 28) * 28;
+    if (R::loads_px(w)) {
+      const int xt = min(tid - R::XS_T0, R::XS_N - 1);
+      const uint8_t* rowp = br.images + (size_t)bidx[live ? t : 0] * 784 + ((xt >> 2) % 28) * 28;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const int col = 8 * (tid & 3) - 4 + 4 * k;
-        f.u[k] = *reinterpret_cast<const uint32_t*>(rowp + min(max(col, 0), 24));
+        const int col = 8 * (xt & 3) - 4 + 4 * k;
+        f.r[O_PX + k] = *reinterpret_cast<const uint32_t*>(rowp + min(max(col, 0), 24));
       }
-      f.m = reinterpret_cast<const uint4*>(cb.m1 + (size_t)bb * M1IMG)[min(max(tid - 112, 0), M1IMG / 16 - 1)];
     }
-    if constexpr (HW) {
-      const int i = min(max(tid - 128, 0), 83), c = i / 14, y = i - 14 * c;
+    if (R::loads_m1(w))
+      f.setq(O_M1, reinterpret_cast<const uint4*>(cb.m1 + (size_t)bb * M1IMG)[min(max(tid - R::M1_T0, 0), R::M1_N - 1)]);
+    if (R::loads_p1(w)) {
+      const int i = min(max(tid - R::P1_T0, 0), R::P1_N - 1), c = i / 14, y = i - 14 * c;
       const uint4* ps = reinterpret_cast<const uint4*>(p1g + (size_t)bb * P1IMG + c * P1CP + y * 16);
 #pragma unroll
-      for (int k = 0; k < PV; ++k) f.p[k] = ps[k];
+      for (int k = 0; k < PV; ++k) f.setq(O_P1 + 4 * k, ps[k]);
     }
+    if (R::loads_p2(w)) {
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      int n, p;
-      if constexpr (sizeof(T) == 2) {  // bf16: thread j < 200 owns channels (2(j%8), 2(j%8)+1) at position j/8
-        const int j = min(tid, 199);
-        n = 2 * (j & 7) + r;
-        p = j >> 3;
-      } else {                          // f32: items tid, tid + 256 of (channel fastest, position)
-        const int e = min(tid + 256 * r, 399);
-        n = e & 15;
-        p = e >> 4;
+      for (int r = 0; r < 2; ++r) {
+        int n, p;
+        if constexpr (sizeof(T) == 2) {  // bf16: thread j < 200 owns channels (2(j%8), 2(j%8)+1) at position j/8
+          const int j = min(max(tid - R::DS_T0, 0), R::DS_N - 1);
+          n = 2 * (j & 7) + r;
+          p = j >> 3;
+        } else {                          // f32: items (channel fastest, position)
+          const int e = min(max(tid - R::F_T0 + NT * r, 0), 399);
+          n = e & 15;
+          p = e >> 4;
+        }
+        if (r < (sizeof(T) == 2 ? 2 : R::F_ITEMS)) {
+          f.r[O_DS + r] = cb.m2[(size_t)bb * 400 + n * 25 + p];
+          const T gv = dp2[(size_t)bb * K0P + n * 25 + p];
+          if constexpr (sizeof(T) == 2) f.r[O_DS + 2 + r] = __builtin_bit_cast(unsigned short, gv);
+          else f.r[O_DS + 2 + r] = __builtin_bit_cast(uint32_t, gv);
+        }
       }
-      f.c[r] = cb.m2[(size_t)bb * 400 + n * 25 + p];
-      f.g[r] = dp2[(size_t)bb * K0P + n * 25 + p];
     }
     return f;
   };
@@ -926,25 +997,21 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   //  shuttle accumulators VGPR<->AGPR around every MFMA -- the B operand is read from LDS)
 
   // ---- once per workgroup: zero every padded image, stage C2d
-  if constexpr (HD) {
-    zero_lds<T>(xs, S::ONES);
-    for (int e = tid; e < S::ONES_N; e += 256) xs[S::ONES + e] = to_t<T>(1.f);
-    zero_lds<T>(dy1t - S::D1PRE, S::D1PRE + 8 * S::D1P);
-    zero_lds<T>(dys, 18 * 18 * 16);
-  }
-  if constexpr (HW) {
-    zero_lds<T>(p1t, 31 * S::P1P);
-    for (int e = tid; e < S::P1P; e += 256) p1t[31 * S::P1P + e] = to_t<T>(1.f);
-    if constexpr (S::DY2) zero_lds<T>(dy2t, 16 * S::D2P);
-  }
+  zero_lds<T>(xs, S::ONES);
+  for (int e = tid; e < S::ONES_N; e += NT) xs[S::ONES + e] = to_t<T>(1.f);
+  zero_lds<T>(dy1t - S::D1PRE, S::D1PRE + 8 * S::D1P);
+  zero_lds<T>(dys, 18 * 18 * 16);
+  zero_lds<T>(p1t, 31 * S::P1P);
+  for (int e = tid; e < S::P1P; e += NT) p1t[31 * S::P1P + e] = to_t<T>(1.f);
+  if constexpr (S::DY2) zero_lds<T>(dy2t, 16 * S::D2P);
   // conv2 dgrad, two output rows per tile: out (Y = y + r, x, c) = sum over kh' in [-1, 4], kw, n of
   // dY2[y - kh'][x - kw][n] * W2[n][c][kh' + r][kw]  ->  B[(kh'+1)*5 + kw, n][(r, c)], zero where
   // kh' + r is outside 0..4.  N = (r, c) holds 12 live columns of 16 (was 6 with one row per tile).
   // Row (r, c) is C2D row c shifted by 5 taps: r = 0 -> [80 zeros | C2D[c][0..400)], r = 1 ->
   // [C2D[c][0..400) | 80 zeros]; copied as 16-byte vectors (rows c >= 6 are all zero).
-  if constexpr (HD) {
+  {
     constexpr int VE = 16 / (int)sizeof(T), RV = 480 / VE, SH = 80 / VE;
-    for (int e = tid; e < 16 * RV; e += 256) {
+    for (int e = tid; e < 16 * RV; e += NT) {
       const int nr = e / RV, v = e % RV, r = nr >> 3, c = nr & 7;
       const int src = r == 0 ? v - SH : v;  // source vector within C2D row c
       uint4 val = make_uint4(0, 0, 0, 0);
@@ -953,10 +1020,9 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
       *reinterpret_cast<uint4*>(w2 + nr * S::W2P + v * VE) = val;
     }
   }
-  // ---- static work split of phase B (dgrad row-pair tile = 15 K-chunks, wgrad tile = 5):
-  //      dgrad pairs {2,2,2,1}, wgrad tiles {2,2,3,3}  ->  40/40/45/30 MFMAs per wave
-  const int np = w < 3 ? 2 : 1, q0 = 2 * w;              // dgrad row pairs [q0, q0 + np)
-  const int nw = w < 2 ? 2 : 3, n0w = w < 2 ? 2 * w : 4 + 3 * (w - 2);
+  // ---- static work split of phase B (dgrad row-pair tile = 15 K-chunks, wgrad tile = 5): BwdRoles
+  const int np = R::dg_np(w), q0 = R::dg_q0(w);  // dgrad row pairs [q0, q0 + np)
+  const int nw = R::wg_nw(w), n0w = R::wg_n0(w);  // wgrad tiles [n0w, n0w + nw)
   constexpr int NWT = 3;  // wgrad accumulators per wave
   // ---- per-lane operand offsets (loop invariant)
   // conv2 wgrad B: DENSE columns kcol = tap*6 + c (150 weights) + 1 bias column = 10 tiles of 16
@@ -966,7 +1032,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   for (int i = 0; i < NWT; ++i) {
     const int kcol = (n0w + i) * 16 + row, tap = kcol / 6, c = kcol - 6 * tap;
     w2off[i] = kcol < 150 ? ((tap % 5) * 6 + c) * S::P1P + (tap / 5) * 16 : (kcol == 150 ? 31 : 30) * S::P1P;
-    if (i >= nw) w2off[i] = 30 * S::P1P;  // no third tile on this wave: zero plane
+    if (i >= nw) w2off[i] = 30 * S::P1P;  // no such tile on this wave: zero plane
   }
   // conv1 wgrad (phase C) as ONE 16x16 tile per image: M row m = (r, n) reads channel n of DY1T shifted
   // back r image rows, N column j = (kernel-row base khb in {0, 2, 4}, kw) reads XS plane kw at row khb,
@@ -978,16 +1044,17 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   constexpr uint8_t C_BMAP[16] = {8, 9, 12, 4, 5, 15, 10, 13, 2, 14, 6, 11, 1, 7, 3, 0};  // (khb / 2) * 5 + kw | 15
   const int c_aoff = (C_AMAP[row] & 7) * S::D1P - 32 * (C_AMAP[row] >> 3);
   const int c_boff = C_BMAP[row] < 15 ? (C_BMAP[row] % 5) * S::XP + 2 * (C_BMAP[row] / 5) * 32 : S::ONES;
-  const Frag ones = ones_frag<T>(), zf = M::zero();
-  int doff[D2CH];  // conv2 dgrad A: -(tap row, col) shift of the lane's K-chunk inside the padded DYS
-#pragma unroll
-  for (int kc = 0; kc < D2CH; ++kc) {
-    int tap, n0;
-    if constexpr (KV == 8) { tap = kc * 2 + (grp >> 1); n0 = (grp & 1) * 8; }
-    else { tap = kc; n0 = grp * 4; }
-    const int khp = tap / 5 - 1, kw = tap % 5;  // A row y - kh' (pair base y <= 12: DYS rows <= 17)
-    doff[kc] = (-khp * 18 - kw) * 16 + n0;
-  }
+  // conv2 dgrad A: the lane's K-chunk kc covers tap = 2kc + (grp >> 1) (bf16; f32: tap = kc), channels n0..; its
+  // fragment sits at -(tap row kh', col kw) positions from the tile's base in the padded DYS.  The
+  // lane-dependent part is folded into two base offsets -- the second tap of a bf16 chunk is one column
+  // left of the first (-16 elements) unless the first ends a kernel row (tap % 5 == 4: next row, kw = 0:
+  // -224) -- so every chunk's offset is a compile-time constant on one of them (no per-chunk VGPRs).
+  const int dl_n = (KV == 8 ? (grp & 1) * 8 - 16 * (grp >> 1) : grp * 4);
+  const int dl_s = (KV == 8 ? (grp & 1) * 8 - 224 * (grp >> 1) : grp * 4);
+  auto doff = [&](int kc) {
+    const int tap0 = KV == 8 ? 2 * kc : kc, khp = tap0 / 5 - 1, kw = tap0 % 5;  // pair base y <= 12: rows <= 17
+    return (-khp * 18 - kw) * 16 + ((KV == 8 && kw == 4) ? dl_s : dl_n);
+  };
 
   f32x4 accW2[NWT], accW1 = zero4();
 #pragma unroll
@@ -996,21 +1063,20 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   __syncthreads();
   stamp(1);
 
-
   for (int t = 0; t < ipb; ++t) {
     const int b = unit * ipb + t;
     const bool valid = b < br.B;
     const Pre cur = nxt;
     // ---- phase A: stage input (5 shifted copies), pool1 (5 shifted channel-major copies),
     //      pool1 codes, and the pool2 un-pooling scatter into DYS / DY2T
-    if (HD && tid < 112 && !ABLATED(cb.ablate, 8)) {
+    if (tid >= R::XS_T0 && tid < R::XS_T0 + R::XS_N && !ABLATED(cb.ablate, 8)) {
       // XS: planes kw = 0..4 of row y, columns [8g, 8g+8): xs[kw][y][x] = xpad[y][x + kw] = w[kw + 2 + j]
       // with w[i] = normalised pixel at image column 8g - 4 + i (0 outside the image)
-      const int y = 2 + (tid >> 2), g = tid & 3;
+      const int xt = tid - R::XS_T0, y = 2 + (xt >> 2), g = xt & 3;
       float wv[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const uint32_t byte = (cur.u[i >> 2] >> (8 * (i & 3))) & 255u;
+        const uint32_t byte = (cur.r[O_PX + (i >> 2)] >> (8 * (i & 3))) & 255u;
         const bool in = valid && (unsigned)(8 * g - 4 + i) < 28u;  // also masks the clamped (duplicate) words
         wv[i] = in ? mnist_norm(byte) : 0.f;
       }
@@ -1043,15 +1109,15 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
         }
       }
     }
-    if (HD && tid >= 112 && tid < 112 + M1IMG / 16 && !ABLATED(cb.ablate, 8))
-      reinterpret_cast<uint4*>(m1s)[tid - 112] = valid ? cur.m : make_uint4(0, 0, 0, 0);
-    if (HW && tid >= 128 && tid < 128 + 84 && !ABLATED(cb.ablate, 8)) {
+    if (tid >= R::M1_T0 && tid < R::M1_T0 + R::M1_N && !ABLATED(cb.ablate, 8))
+      reinterpret_cast<uint4*>(m1s)[tid - R::M1_T0] = valid ? cur.q(O_M1) : make_uint4(0, 0, 0, 0);
+    if (tid >= R::P1_T0 && tid < R::P1_T0 + R::P1_N && !ABLATED(cb.ablate, 8)) {
       // P1T: row y of planes (kw, c), kw = 0..4: p1t[kw*6+c][y][x] = pool1[y][x + kw][c], 0 for x + kw >= 14
-      const int i = tid - 128, c = i / 14, y = i - 14 * c;
+      const int i = tid - R::P1_T0, c = i / 14, y = i - 14 * c;
       T pv[16];
 #pragma unroll
       for (int k = 0; k < PV; ++k)
-        *reinterpret_cast<uint4*>(pv + k * (16 / (int)sizeof(T))) = valid ? cur.p[k] : make_uint4(0, 0, 0, 0);
+        *reinterpret_cast<uint4*>(pv + k * (16 / (int)sizeof(T))) = valid ? cur.q(O_P1 + 4 * k) : make_uint4(0, 0, 0, 0);
       T* dst = p1t + c * S::P1P + y * 16;
       if constexpr (sizeof(T) == 2) {
         uint32_t D[10];
@@ -1086,15 +1152,15 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
       }
     }
     if constexpr (sizeof(T) == 2) {
-      // pool2 un-pooling, two channels per thread: every DYS write is one 32-bit (channel pair) store and
-      // every DY2T write one 32-bit (column pair) store -- half the store instructions of 16-bit writes
-      if (tid < 200 && !ABLATED(cb.ablate, 32)) {
-        const int n0 = 2 * (tid & 7), p = tid >> 3, py = p / 5, px = p % 5;
+      // pool2 un-pooling, two channels per thread: every DYS write is one 32-bit (channel pair) store
+      if (tid >= R::DS_T0 && tid < R::DS_T0 + R::DS_N && !ABLATED(cb.ablate, 32)) {
+        const int j = tid - R::DS_T0;
+        const int n0 = 2 * (j & 7), p = j >> 3, py = p / 5, px = p % 5;
         float v[2][4];  // [channel][window]
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
-          const uint32_t code = valid ? cur.c[r] : 0u;  // code 0: ReLU blocked, every window gets 0
-          const float g = to_f(cur.g[r]);
+          const uint32_t code = valid ? cur.code(r) : 0u;  // code 0: ReLU blocked, every window gets 0
+          const float g = to_f(cur.grad(r));
 #pragma unroll
           for (int win = 0; win < 4; ++win) v[r][win] = ((code & 4) && (code & 3) == win) ? g : 0.f;
         }
@@ -1107,31 +1173,23 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
 #pragma unroll
         for (int win = 0; win < 4; ++win) {
           const int oh = 2 * py + (win >> 1), ow = 2 * px + (win & 1);
-          if constexpr (HD) *reinterpret_cast<uint32_t*>(dys + ((oh + 4) * 18 + ow + 4) * 16 + n0) = pack2(v[0][win], v[1][win]);
-        }
-        if constexpr (S::DY2) {
-#pragma unroll
-          for (int r = 0; r < 2; ++r)
-#pragma unroll
-            for (int dy = 0; dy < 2; ++dy)
-              *reinterpret_cast<uint32_t*>(dy2t + (n0 + r) * S::D2P + (2 * py + dy) * 16 + 2 * px) =
-                  pack2(v[r][2 * dy], v[r][2 * dy + 1]);
+          *reinterpret_cast<uint32_t*>(dys + ((oh + 4) * 18 + ow + 4) * 16 + n0) = pack2(v[0][win], v[1][win]);
         }
       }
     } else {
 #pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        const int e = tid + 256 * r;
-        if (e >= 400 || ABLATED(cb.ablate, 32)) break;
+      for (int r = 0; r < R::F_ITEMS; ++r) {
+        const int e = tid - R::F_T0 + NT * r;
+        if (e < 0 || e >= 400 || ABLATED(cb.ablate, 32)) break;
         const int n = e & 15, p = e >> 4, py = p / 5, px = p % 5;  // channel fastest: conflict-free DYS writes
-        const uint32_t code = valid ? cur.c[r] : 0u;  // code 0: ReLU blocked, every window gets 0
-        const float g = to_f(cur.g[r]);
+        const uint32_t code = valid ? cur.code(r) : 0u;  // code 0: ReLU blocked, every window gets 0
+        const float g = to_f(cur.grad(r));
 #pragma unroll
         for (int win = 0; win < 4; ++win) {
           const int oh = 2 * py + (win >> 1), ow = 2 * px + (win & 1);
           const T v = to_t<T>(((code & 4) && (code & 3) == win) ? g : 0.f);
-          if constexpr (HD) dys[((oh + 4) * 18 + ow + 4) * 16 + n] = v;
-          if constexpr (HW) dy2t[n * S::D2P + oh * 16 + ow] = v;
+          dys[((oh + 4) * 18 + ow + 4) * 16 + n] = v;
+          dy2t[n * S::D2P + oh * 16 + ow] = v;
         }
       }
     }
@@ -1142,10 +1200,9 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     nxt = fetch(t + 1);
 
     // ---- phase B1: conv2 wgrad  dW2[n][(tap, c)] += sum_pos dY2[pos][n] * pool1[pos + tap][c]
-    //      Straight-line (constant trip counts, the ablation test outside the loop) with the next
-    //      chunk's fragments loaded before this chunk's MFMAs: a runtime trip count kept the loop
-    //      rolled and every chunk waited for its own LDS reads.
-    if (HW && !ABLATED(cb.ablate, 64)) {
+    //      Straight-line (constant trip counts) with the next chunk's fragments loaded before this chunk's
+    //      MFMAs: a runtime trip count kept the loop rolled and every chunk waited for its own LDS reads.
+    if (nw > 0 && !ABLATED(cb.ablate, 64)) {
       auto ld_a = [&](int kc) -> Frag {
         if constexpr (S::TRA) {
           // positions p0 .. p0 + 7 (row y = p0 / 16, columns x0 .. x0 + 7; x >= 10 reads DYS's zero padding) of
@@ -1169,25 +1226,25 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
         const int p0 = kc * KC + grp * KV;
         return M::load(p1t + w2off[i] + (p0 >> 4) * 16 + (p0 & 15));
       };
-      // NT real tiles on this wave (2 on waves 0-1, 3 on waves 2-3): no zero-plane filler tile
+      // NT real tiles on this wave: no zero-plane filler tile
       auto wgrad2 = [&](auto ntc) {
-        constexpr int NT = decltype(ntc)::value;
-        Frag a = ld_a(0), b[NT];
+        constexpr int NTL = decltype(ntc)::value;
+        Frag a = ld_a(0), bb[NTL];
 #pragma unroll
-        for (int i = 0; i < NT; ++i) b[i] = ld_b(0, i);
+        for (int i = 0; i < NTL; ++i) bb[i] = ld_b(0, i);
 #pragma unroll
         for (int kc = 0; kc < W2CH; ++kc) {
-          Frag an = a, bn[NT];
+          Frag an = a, bn[NTL];
           if (kc + 1 < W2CH) {
             an = ld_a(kc + 1);
 #pragma unroll
-            for (int i = 0; i < NT; ++i) bn[i] = ld_b(kc + 1, i);
+            for (int i = 0; i < NTL; ++i) bn[i] = ld_b(kc + 1, i);
           }
 #pragma unroll
-          for (int i = 0; i < NT; ++i) M::mma(accW2[i], a, b[i]);
+          for (int i = 0; i < NTL; ++i) M::mma(accW2[i], a, bb[i]);
           a = an;
 #pragma unroll
-          for (int i = 0; i < NT; ++i) b[i] = bn[i];
+          for (int i = 0; i < NTL; ++i) bb[i] = bn[i];
         }
       };
       if (nw == 2) wgrad2(std::integral_constant<int, 2>{});
@@ -1199,7 +1256,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     //      Lane group g owns x = 4g..4g+3; the pool1 un-pooling epilogue (argmax + ReLU) writes the
     //      conv1 pre-activation grad rows 2Y and 2Y+1 (Y = y + r) as ONE 16-byte store each.
     //      A wave's (up to 2) tiles share every B fragment.
-    {
+    if (np > 0) {
       auto dgrad_tile_epi = [&](int y, const f32x4& acc) {
         const int c = row & 7, Y = y + (row >> 3);
         if (c < 6) {
@@ -1230,7 +1287,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
       };
       const int x = min(row, 13);
       const T* bq = w2 + row * S::W2P + grp * KV;
-      if (HD && !ABLATED(cb.ablate, 128)) {
+      if (!ABLATED(cb.ablate, 128)) {
         if (np == 2) {
           const int y0 = 2 * q0, y1 = y0 + 2;
           const T* a0 = dys + ((y0 + 4) * 18 + x + 4) * 16;
@@ -1242,15 +1299,15 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
           constexpr int SH = 160 / KC;  // chunks per two kernel rows (10 taps x 16 channels)
           static_assert(SH < D2CH, "row-pair A reuse needs more than two kernel rows of K");
           Frag A0[D2CH];
-          Frag fb = M::load(bq), fa1 = M::load(a1 + doff[0]);
-          A0[0] = M::load(a0 + doff[0]);
+          Frag fb = M::load(bq), fa1 = M::load(a1 + doff(0));
+          A0[0] = M::load(a0 + doff(0));
 #pragma unroll
           for (int kc = 0; kc < D2CH; ++kc) {  // next chunk's fragments in flight during this one's MFMAs
             Frag nb = fb, na1 = fa1;
             if (kc + 1 < D2CH) {
               nb = M::load(bq + (kc + 1) * KC);
-              A0[kc + 1] = M::load(a0 + doff[kc + 1]);
-              na1 = kc + 1 < SH ? M::load(a1 + doff[kc + 1]) : A0[kc + 1 - SH];
+              A0[kc + 1] = M::load(a0 + doff(kc + 1));
+              na1 = kc + 1 < SH ? M::load(a1 + doff(kc + 1)) : A0[kc + 1 - SH];
             }
             M::mma(acc0, A0[kc], fb);
             M::mma(acc1, fa1, fb);
@@ -1262,13 +1319,13 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
           const int y0 = 2 * q0;
           const T* a0 = dys + ((y0 + 4) * 18 + x + 4) * 16;
           f32x4 acc0 = zero4();
-          Frag fb = M::load(bq), fa0 = M::load(a0 + doff[0]);
+          Frag fb = M::load(bq), fa0 = M::load(a0 + doff(0));
 #pragma unroll
           for (int kc = 0; kc < D2CH; ++kc) {
             Frag nb = fb, na0 = fa0;
             if (kc + 1 < D2CH) {
               nb = M::load(bq + (kc + 1) * KC);
-              na0 = M::load(a0 + doff[kc + 1]);
+              na0 = M::load(a0 + doff(kc + 1));
             }
             M::mma(acc0, fa0, fb);
             fb = nb; fa0 = na0;
@@ -1281,25 +1338,26 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
     if (t < 4) stamp(3 + 3 * t);
 
     // ---- phase C: conv1 wgrad  dW1[n][kh][kw] += sum_pos dY1[pos][n] * xpad[pos + kh * 32 + kw]
-    //      K = positions 0..927 (28 image rows + the zero row 28 that row-shifted A rows need)
-    if constexpr (HD) {
-      constexpr int CCH = 928 / KC, CPW = CCH / 4;  // chunks per wave: CPW, + 1 on waves < CCH % 4
+    //      K = positions 0..927 (28 image rows + the zero row 28 that row-shifted A rows need), chunks split
+    //      round-robin over the NW waves (own accumulator each, summed in a fixed order after the loop)
+    {
+      constexpr int CCH = 928 / KC, CPW = CCH / NW;  // chunks per wave: CPW, + 1 on waves < CCH % NW
       if (!ABLATED(cb.ablate, 512)) {
         auto ld_a = [&](int kc) { return M::load(dy1t + c_aoff + kc * KC + grp * KV); };
         auto ld_b = [&](int kc) { return M::load(xs + c_boff + kc * KC + grp * KV); };
-        Frag a = ld_a(w), b = ld_b(w);
+        Frag a = ld_a(w), bx = ld_b(w);
 #pragma unroll
         for (int j = 0; j < CPW; ++j) {
-          Frag an = a, bn = b;
-          if (j + 1 < CPW || w < CCH % 4) {
-            const int kn = w + 4 * (j + 1);
+          Frag an = a, bn = bx;
+          if (j + 1 < CPW || w < CCH % NW) {
+            const int kn = w + NW * (j + 1);
             an = ld_a(kn);
             bn = ld_b(kn);
           }
-          M::mma(accW1, a, b);
-          a = an; b = bn;
+          M::mma(accW1, a, bx);
+          a = an; bx = bn;
         }
-        if (w < CCH % 4) M::mma(accW1, a, b);
+        if (w < CCH % NW) M::mma(accW1, a, bx);
       }
       __syncthreads();
       if (t < 4) stamp(4 + 3 * t);
@@ -1311,7 +1369,7 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
   float* out = cb.slab + (size_t)unit * L::CONV_PARAMS;
 #pragma unroll
   for (int i = 0; i < NWT; ++i) {
-    if (!HW || i >= nw) break;
+    if (i >= nw) break;
     const int kcol = (n0w + i) * 16 + row, tap = kcol / 6, c = kcol - 6 * tap;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -1320,27 +1378,30 @@ __global__ __launch_bounds__(256) void conv_bwd_kernel(BatchRef br, LenetConvBuf
       else if (kcol == 150) out[L::CB2 + n] = accW2[i][r];
     }
   }
-  if constexpr (HD) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) red[w * 256 + (grp * 4 + i) * 16 + row] = accW1[i];
-    __syncthreads();
-    {
-      const int m = tid >> 4, j = tid & 15;  // C row m = (r, n), column j = (khb, kw) | bias
-      const float v = (red[0 * 256 + tid] + red[1 * 256 + tid]) + (red[2 * 256 + tid] + red[3 * 256 + tid]);
-      const int r = C_AMAP[m] >> 3, n = C_AMAP[m] & 7, bj = C_BMAP[j];
-      if (n < 6) {
-        if (bj == 15) {
-          if (r == 0) out[L::CB1 + n] = v;
-        } else {
-          const int kh = 2 * (bj / 5) + r, kw = bj % 5;
-          if (kh <= 4) out[L::CW1 + n * 25 + kh * 5 + kw] = v;
-        }
+  for (int i = 0; i < 4; ++i) red[w * 256 + (grp * 4 + i) * 16 + row] = accW1[i];
+  __syncthreads();
+  if (tid < 256) {
+    const int m = tid >> 4, j = tid & 15;  // C row m = (r, n), column j = (khb, kw) | bias
+    float v;
+    if constexpr (NW == 8)
+      v = ((red[0 * 256 + tid] + red[1 * 256 + tid]) + (red[2 * 256 + tid] + red[3 * 256 + tid])) +
+          ((red[4 * 256 + tid] + red[5 * 256 + tid]) + (red[6 * 256 + tid] + red[7 * 256 + tid]));
+    else
+      v = (red[0 * 256 + tid] + red[1 * 256 + tid]) + (red[2 * 256 + tid] + red[3 * 256 + tid]);
+    const int r = C_AMAP[m] >> 3, n = C_AMAP[m] & 7, bj = C_BMAP[j];
+    if (n < 6) {
+      if (bj == 15) {
+        if (r == 0) out[L::CB1 + n] = v;
+      } else {
+        const int kh = 2 * (bj / 5) + r, kw = bj % 5;
+        if (kh <= 4) out[L::CW1 + n * 25 + kh * 5 + kw] = v;
       }
     }
   }
   stamp(15);
-  // (MODE 0 only: this block's hardware location, in its own row range; cb.stamps starts at STAMP_CONV_BWD)
-  if (MODE == 0 && cb.stamps && tid == 0 && blockIdx.x < 512)
+  // this block's hardware location, in its own row range (cb.stamps starts at STAMP_CONV_BWD)
+  if (cb.stamps && tid == 0 && blockIdx.x < 512)
     cb.stamps[(STAMP_BWD_HWLOC - STAMP_CONV_BWD + blockIdx.x) * 16] = hw_location();
 }
 
@@ -1404,6 +1465,9 @@ void launch_lenet_conv_bwd(DType t, const BatchRef& br, const LenetConvBuffers& 
   const int ipb = bwd_ipb(br.B, target_blocks), grid = (br.B + ipb - 1) / ipb;
   if (nslab_out) *nslab_out = grid;
   if (br.B <= 0) return;
-  if (t == DType::F32) hipLaunchKernelGGL((conv_bwd_kernel<float, 0>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
-  else hipLaunchKernelGGL((conv_bwd_kernel<bf16, 0>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
+  // Waves per workgroup (BwdRoles): fp32 -- 150 KB of LDS, one workgroup per CU -- runs 8 waves (0.440 vs
+  // 0.478 ms per LeNet fp32 B=8192 step, same box); bf16 keeps 4 (two workgroups per CU: 8 waves would take
+  // every VGPR of the SIMDs and starve the FC weight gradient that runs beside conv_bwd, 0.119-0.127 vs 0.103 ms)
+  if (t == DType::F32) hipLaunchKernelGGL((conv_bwd_kernel<float, 8>), dim3(grid), dim3(512), 0, s, br, cb, ipb);
+  else hipLaunchKernelGGL((conv_bwd_kernel<bf16, 4>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
 }

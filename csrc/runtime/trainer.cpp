@@ -126,6 +126,7 @@ void Trainer::release() {
     (void)hipStreamSynchronize(aux_stream_);
   }
   comm_.reset();
+  oneshot_.reset();
 }
 
 int Trainer::pack_size() const { return model_pack_size(model_); }
@@ -283,7 +284,11 @@ void Trainer::spin(double seconds, uintptr_t stream) {
 
 void Trainer::all_reduce(const std::vector<Bucket>& bs, int phase, hipStream_t s) {
   for (const Bucket& b : bs)
-    if (phase < 0 || b.phase == phase) comm_->all_reduce_sum_f32(ptr<float>(p_.grad) + b.p0, size_t(b.p1 - b.p0), s);
+    if (phase < 0 || b.phase == phase) {
+      float* g = ptr<float>(p_.grad) + b.p0;
+      if (oneshot_) oneshot_->all_reduce_sum_f32(g, size_t(b.p1 - b.p0), s);
+      else comm_->all_reduce_sum_f32(g, size_t(b.p1 - b.p0), s);
+    }
 }
 
 std::vector<Bucket> Trainer::issued_collectives() const {

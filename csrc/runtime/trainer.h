@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "../kernels/launch.h"
+#include "oneshot.h"
 #include "rccl_comm.h"
 
 struct TrainerPtrs {
@@ -48,6 +49,10 @@ class Trainer {
   ~Trainer();
 
   void set_comm(std::shared_ptr<RcclComm> c) { invalidate(); comm_ = std::move(c); }
+  // Gradient data plane of the step's collectives: the one-shot xGMI all-reduce instead of RCCL (null: RCCL).
+  // Works with or without an RCCL communicator attached (parameter broadcast then goes over the control plane).
+  void set_oneshot(std::shared_ptr<OneShotAllReduce> o) { invalidate(); oneshot_ = std::move(o); }
+  bool has_oneshot() const { return oneshot_ != nullptr; }
   // Timing only (exposed-communication measurement): with a communicator attached, run the local
   // single-GPU schedule without any collective.  Cached graphs are keyed by it.
   void set_comm_enabled(bool on) { comm_enabled_ = on; }
@@ -84,7 +89,7 @@ class Trainer {
   int bwd_grid() const;
   // The collectives one full-batch step issues under the current plan, in issue order.
   std::vector<Bucket> issued_collectives() const;
-  bool has_comm() const { return comm_ != nullptr; }
+  bool has_comm() const { return comm_ != nullptr || oneshot_ != nullptr; }
   int world() const { return world_; }
   // first parameter of backward phase 0 (see Plan): LeNet conv_params, MLP the layer-2 weight offset
   int phase_split() const;
@@ -139,7 +144,7 @@ class Trainer {
   void launch_mlp_comm_tail(int B, hipStream_t s, const HeadBuffers& hb, int hrows);
   // comm stream: wait for `ready`, all-reduce phase `phase`'s buckets, update its parameter range
   void comm_phase(int phase, hipEvent_t ready, bool bump);
-  bool use_comm() const { return comm_ && comm_enabled_; }
+  bool use_comm() const { return (comm_ || oneshot_) && comm_enabled_; }
   void sync_own_streams();
   struct GraphSlot {
     hipGraph_t graph = nullptr;
@@ -168,6 +173,7 @@ class Trainer {
   int bwd_blocks_ = 0;
   int max_conv_slabs_ = 0;  // rows of the conv slab (lenet_conv_bwd_max_blocks(batch) at the default target)
   std::shared_ptr<RcclComm> comm_;
+  std::shared_ptr<OneShotAllReduce> oneshot_;
   std::vector<Bucket> buckets_;
   hipStream_t comm_stream_ = nullptr;
   hipStream_t aux_stream_ = nullptr;  // concurrent FC wgrad branch (fork/join inside the step graph)

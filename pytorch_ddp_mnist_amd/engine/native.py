@@ -195,6 +195,7 @@ class NativeTrainer:
         self.stream = torch.cuda.Stream(device=dev)
         self.world = 1
         self.comm = None
+        self.oneshot = None         # one-shot xGMI all-reduce data plane (attach_oneshot)
         self.ext_allreduce = None   # external data plane (attach_external_allreduce)
         self.module_template = build_model(model)
         if init is not None:
@@ -237,6 +238,15 @@ class NativeTrainer:
         self.rt.set_world(world)
         self.set_plan(plan, bwd_blocks)
 
+    def attach_oneshot(self, oneshot, world: int, plan: str = "join") -> None:
+        """Use the one-shot xGMI all-reduce (parallel/oneshot.py) for the step's gradient collectives instead of
+        RCCL.  An RCCL communicator may stay attached (parameter broadcast, comm_profile comparison)."""
+        self.oneshot = oneshot
+        self.world = int(world)
+        self.rt.set_oneshot(oneshot)
+        self.rt.set_world(self.world)
+        self.set_plan(plan, 0)
+
     def set_plan(self, plan: str, bwd_blocks: int = 0) -> None:
         if plan not in PLANS:
             raise ValueError(f"unknown step plan {plan!r} (choices: {sorted(PLANS)})")
@@ -257,7 +267,9 @@ class NativeTrainer:
     def plan_info(self) -> dict:
         """What a full-batch step runs: plan, conv_bwd grid, and the collectives in issue order."""
         coll = [(b.p0, b.p1) for b in self.rt.issued_collectives()]
-        return {"plan": self.plan if self.comm is not None else ("local" if self.rt.concurrent else "local-serial"),
+        dp = self.comm is not None or self.oneshot is not None
+        return {"plan": self.plan if dp else ("local" if self.rt.concurrent else "local-serial"),
+                "allreduce": "oneshot" if self.oneshot is not None else ("rccl" if self.comm is not None else None),
                 "conv_bwd_grid": self.rt.bwd_grid if self.model_name == "lenet5" else None,
                 "collectives": [{"params": [a, b], "bytes": 4 * (b - a)} for a, b in coll]}
 
@@ -265,8 +277,14 @@ class NativeTrainer:
         self.rt.set_buckets([self.C.Bucket(int(a), int(b), int(ph)) for a, b, ph in ranges])
 
     def broadcast_params(self, root: int = 0) -> None:
-        """DDP construction semantics: every rank starts from rank 0's parameters."""
+        """DDP construction semantics: every rank starts from rank 0's parameters (over RCCL, or over the
+        c10d control plane when only the one-shot data plane is attached)."""
         if self.comm is None:
+            if self.oneshot is not None and self.world > 1:
+                import torch.distributed as dist
+                p = self.params.detach().cpu()
+                dist.broadcast(p, root)
+                self.load_flat(p)
             return
         self._sync_in()
         self.comm.broadcast_f32(self.params.data_ptr(), self.nparam, root, self.stream.cuda_stream)
@@ -304,7 +322,12 @@ class NativeTrainer:
         self.optimizer_step(1.0 / self.world)
 
     def check_comm(self) -> None:
-        """Non-blocking health poll (once per epoch): abort + raise on an asynchronous RCCL error."""
+        """Health poll (once per epoch): abort + raise on an asynchronous RCCL error; raise if a one-shot
+        all-reduce flag wait timed out."""
+        if self.oneshot is not None:
+            err = self.oneshot.check()
+            if err:
+                raise CollectiveError(err)
         if self.comm is None:
             return
         err = self.comm.async_error()
@@ -450,11 +473,12 @@ class NativeTrainer:
         from ..parallel.ddp import (choose_plan, default_plan_candidates, local_plan_candidates,
                                     mlp_plan_candidates)
         forced = forced_plan()
-        if self.comm is not None and forced:
+        dp = self.comm is not None or self.oneshot is not None  # a gradient data plane is attached
+        if dp and forced:
             self.set_plan(forced, 0)
             return {"chosen": forced, "timings_ms": {}, "forced": True}
         if candidates is None:
-            if self.comm is not None:
+            if dp:
                 if self.model_name == "lenet5":
                     ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
                     candidates = default_plan_candidates(self.C.conv_bwd_blocks(self.batch), ncu)
@@ -473,9 +497,9 @@ class NativeTrainer:
                 candidates = local_plan_candidates(fwd_head=self.fwd_head_applies())
             else:
                 return {"chosen": "local", "timings_ms": {}}
-        prefer = "join" if self.comm is not None else "concurrent"
+        prefer = "join" if dp else "concurrent"
         extra = {}
-        if self.comm is not None:
+        if dp:
             # the local step without collectives, in both single-GPU branch forms: exposed communication is
             # measured against the faster one (the concurrent branch is not the local best at every batch)
             for conc in (True, False):
@@ -508,23 +532,31 @@ class NativeTrainer:
           collectives vs the local single-GPU schedule without any, interleaved replays (taken from
           ``tune`` when the calibration already timed both).
         Collective: every rank calls it at the same point."""
-        if self.comm is None:
+        if self.comm is None and self.oneshot is None:
             return {"rccl_world": None}
         colls = []
         for c in self.plan_info()["collectives"]:
             a, b = c["params"]
-            buf = torch.zeros(b - a, dtype=torch.float32, device=self.device)
-            self._sync_in()
-            try:
-                ts = self.comm.time_all_reduce(buf.data_ptr(), b - a, warmup, iters, self.stream.cuda_stream,
-                                               comm_timeout())
-            except RuntimeError as e:
-                self.comm.abort()
-                raise CollectiveError(f"rank {self.comm.rank}: {e} (communicator aborted)") from e
-            ts = sorted(ts)
-            med = ts[len(ts) // 2]
-            med = reduce_max(med) if reduce_max is not None else med
-            colls.append({"params": [a, b], "bytes": 4 * (b - a), "allreduce_us": round(med * 1000.0, 2)})
+            row = {"params": [a, b], "bytes": 4 * (b - a)}
+            if self.comm is not None:
+                buf = torch.zeros(b - a, dtype=torch.float32, device=self.device)
+                self._sync_in()
+                try:
+                    ts = self.comm.time_all_reduce(buf.data_ptr(), b - a, warmup, iters, self.stream.cuda_stream,
+                                                   comm_timeout())
+                except RuntimeError as e:
+                    self.comm.abort()
+                    raise CollectiveError(f"rank {self.comm.rank}: {e} (communicator aborted)") from e
+                ts = sorted(ts)
+                med = ts[len(ts) // 2]
+                med = reduce_max(med) if reduce_max is not None else med
+                row["allreduce_us"] = round(med * 1000.0, 2)
+            if self.oneshot is not None:
+                from ..parallel.oneshot import time_oneshot
+                med = time_oneshot(self.oneshot, b - a, self.device, iters=iters, warmup=warmup)
+                med = reduce_max(med) if reduce_max is not None else med
+                row["oneshot_us"] = round(med * 1000.0, 2)
+            colls.append(row)
         tm = (tune or {}).get("timings_ms", {})
         chosen = (tune or {}).get("chosen")
         if chosen in tm and "nocomm_ms" in (tune or {}):
@@ -535,7 +567,8 @@ class NativeTrainer:
                    "nocomm_serial": {**cur, "comm": False, "concurrent": False}}
             t = self.time_schedules({"plan": cur, **loc}, iters=iters, warmup=warmup, reduce_max=reduce_max)
             plan_ms, local_ms = t["plan"], min(t["nocomm"], t["nocomm_serial"])
-        return {"rccl_world": int(self.comm.world), "collectives": colls,
+        return {"rccl_world": int(self.comm.world) if self.comm is not None else None,
+                "allreduce": "oneshot" if self.oneshot is not None else "rccl", "collectives": colls,
                 "step_plan_ms": round(plan_ms, 4), "step_local_ms": round(local_ms, 4),
                 "exposed_comm_us": round((plan_ms - local_ms) * 1000.0, 2)}
 
@@ -544,8 +577,11 @@ class NativeTrainer:
         they captured collectives -- and detach the communicator.  The trainer can still run local steps."""
         if self.comm is not None and not self.comm.aborted:
             self.synchronize()
+        else:
+            self.stream.synchronize()
         self.rt.release()
         self.comm = None
+        self.oneshot = None
 
     # ------------------------------------------------------------------ training
     def set_epoch_indices(self, indices: torch.Tensor) -> None:

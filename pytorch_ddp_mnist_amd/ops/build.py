@@ -67,22 +67,25 @@ def _compile(src: Path, headers: List[Path], cmd_prefix: List[str], force: bool)
     return obj
 
 
-def build_c(force: bool = False, jobs: int = 8) -> Path:
-    headers = list(CSRC.rglob("*.h"))
-    hip_srcs = sorted((CSRC / "kernels").glob("*.hip"))
-    cpp_srcs = sorted((CSRC / "runtime").glob("*.cpp")) + [CSRC / "bindings.cpp"]
+def build_c(force: bool = False, jobs: int = 8, csrc: Path = CSRC, out: Path = None) -> Path:
+    """``csrc`` / ``out``: build another source tree (e.g. a previous revision's ``csrc``, scripts/build_ab.sh)
+    into another file, for same-box A/B runs (ops/native.py ``MNIST_AMD_C_PATH``)."""
+    csrc = Path(csrc)
+    headers = list(csrc.rglob("*.h"))
+    hip_srcs = sorted((csrc / "kernels").glob("*.hip"))
+    cpp_srcs = sorted((csrc / "runtime").glob("*.cpp")) + [csrc / "bindings.cpp"]
     # MNIST_AMD_BUILD_DEFINES: extra -D flags of a diagnostic build (e.g. -DMNIST_AMD_ABLATION_BUILD for
     # scripts/ablate.sh); part of the object-cache key, so switching back rebuilds the normal objects
     defs = os.environ.get("MNIST_AMD_BUILD_DEFINES", "").split()
-    hip_cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", f"-I{CSRC}",
+    hip_cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", f"-I{csrc}",
                "-Wno-unused-result"] + defs
     cpp_cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}",
-               f"-I{CSRC}", "-fvisibility=hidden"] + defs + _pybind_includes()
+               f"-I{csrc}", "-fvisibility=hidden"] + defs + _pybind_includes()
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         futs = [ex.submit(_compile, s, headers, hip_cmd, force) for s in hip_srcs]
         futs += [ex.submit(_compile, s, headers, cpp_cmd, force) for s in cpp_srcs]
         objs = [f.result() for f in futs]
-    out = PKG / f"_C{EXT}"
+    out = Path(out) if out else PKG / f"_C{EXT}"
     tmp = out.with_name(out.name + ".tmp")
     _run([_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp)] + [str(o) for o in objs]
          + [f"-L{ROCM / 'lib'}", "-lamdhip64", "-lrccl"])
@@ -109,11 +112,13 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--only", choices=["_C", "_io"], default=None)
+    ap.add_argument("--csrc", default=str(CSRC), help="_C source tree (default: the repo's csrc)")
+    ap.add_argument("--out", default=None, help="_C output file (default: the in-tree package module)")
     a = ap.parse_args(argv)
     if a.only == "_io":
         print(build_io(a.force))
     elif a.only == "_C":
-        print(build_c(a.force))
+        print(build_c(a.force, csrc=Path(a.csrc), out=Path(a.out) if a.out else None))
     else:
         for p in build_all(a.force):
             print(p)

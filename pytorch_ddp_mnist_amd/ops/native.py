@@ -29,6 +29,18 @@ def load_c() -> ModuleType:
     global _C
     if _C is not None:
         return _C
+    alt = os.environ.get("MNIST_AMD_C_PATH")
+    if alt:
+        # same-box A/B of another build of the extension (scripts/build_ab.sh): the file's module init is
+        # PyInit__C, so it is loaded under the package module name from the given path
+        from importlib import util as _iu
+        spec = _iu.spec_from_file_location("pytorch_ddp_mnist_amd._C", alt)
+        if spec is None or spec.loader is None:
+            raise NativeExtensionError(f"MNIST_AMD_C_PATH={alt}: not a loadable extension")
+        mod = _iu.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        _C = mod
+        return _C
     try:
         _C = importlib.import_module("pytorch_ddp_mnist_amd._C")
     except ImportError as e:

@@ -1,0 +1,71 @@
+"""Bring-up of the one-shot xGMI all-reduce (csrc/runtime/oneshot.h, csrc/kernels/oneshot.hip).
+
+The alternative gradient data plane to RCCL's ring (survey §5.8-3): every rank exports one uncached device
+region over IPC (``hipIpcGetMemHandle``), the handles travel over the control-plane TCPStore, every rank maps
+its peers' regions, and a step's all-reduce becomes ONE kernel that pushes the local slice into every peer's
+slot over the point-to-point xGMI links and sums the W slots of its own region in a fixed rank order (bitwise
+identical replicas).  Reference call site it replaces: the DDP bucket all-reduce of
+``ddp_tutorial_multi_gpu.py:94`` (one NCCL all-reduce per step).  RCCL stays the default
+(``bench.py --allreduce rccl``); ``--allreduce oneshot`` selects this one.
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+KEY = "mnist_amd/oneshot/{gen}/{rank}"
+_GEN = [0]
+
+
+def oneshot_timeout() -> float:
+    """In-kernel bound of a flag wait (``MNIST_AMD_ONESHOT_TIMEOUT`` seconds, default 30): a rank whose peer
+    never arrives finishes the kernel with the error word set, reported by ``check()``."""
+    return float(os.environ.get("MNIST_AMD_ONESHOT_TIMEOUT", "30"))
+
+
+def make_oneshot(ctx, max_count: int, nblk: int = 64, timeout_s: Optional[float] = None, init_timeout_s: float = 180.0):
+    """Collective (every rank of ``ctx``): create this rank's region, exchange the IPC handles, map the peers.
+    World 1 needs no exchange."""
+    from ..ops.native import load_c
+    C = load_c()
+    dev = ctx.device.index if ctx.device.type == "cuda" and ctx.device.index is not None else torch.cuda.current_device()
+    o = C.OneShotAllReduce(ctx.rank, ctx.world, int(dev), int(max_count), int(nblk),
+                           oneshot_timeout() if timeout_s is None else float(timeout_s))
+    if ctx.world > 1:
+        _GEN[0] += 1
+        store = dist.distributed_c10d._get_default_store()
+        store.set(KEY.format(gen=_GEN[0], rank=ctx.rank), o.handle())
+        keys = [KEY.format(gen=_GEN[0], rank=r) for r in range(ctx.world)]
+        store.wait(keys, datetime.timedelta(seconds=init_timeout_s))
+        o.open_peers([bytes(store.get(k)) for k in keys])
+        ctx.barrier()  # every rank has mapped every region before the first call
+    return o
+
+
+def time_oneshot(o, count: int, device, iters: int = 48, warmup: int = 8):
+    """Latency (ms) of ONE one-shot all-reduce of ``count`` floats, as the step graph issues it: captured into a
+    graph and replayed back to back (median; collective -- every rank calls it)."""
+    buf = torch.zeros(count, dtype=torch.float32, device=device)
+    s = torch.cuda.Stream(device=device)
+    s.wait_stream(torch.cuda.current_stream(device))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        o.all_reduce_sum_f32(buf.data_ptr(), count, torch.cuda.current_stream(device).cuda_stream)
+    with torch.cuda.stream(s):
+        for _ in range(warmup):
+            g.replay()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(iters + 1)]
+        ev[0].record(s)
+        for i in range(iters):
+            g.replay()
+            ev[i + 1].record(s)
+    s.synchronize()
+    err = o.check()
+    if err:
+        raise RuntimeError(err)
+    ts = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(iters))
+    return ts[len(ts) // 2]
