@@ -260,13 +260,16 @@ def main(argv=None) -> int:
     tr.set_buckets(plan_buckets(model_phases(a.model)))
     tr.set_epoch_indices(idx_all)
     comm, rccl_version, tune, prof = None, None, None, None
-    oneshot = None
+    oneshot, probe, probe_err = None, None, None
     external = a.comm in ("torch", "gloo") and W > 1 and a.allreduce != "oneshot"
     if a.allreduce == "oneshot":
         if a.comm == "torch":
             raise SystemExit("--allreduce oneshot needs --comm rccl (RCCL kept for broadcast / comparison) or gloo")
-        from pytorch_ddp_mnist_amd.parallel.oneshot import make_oneshot
+        from pytorch_ddp_mnist_amd.parallel.oneshot import make_oneshot, validate_oneshot
         oneshot = make_oneshot(ctx, tr.nparam)
+        err = validate_oneshot(ctx, oneshot, tr.nparam)  # exact-sum check, agreed by every rank
+        if err:
+            raise SystemExit(f"[bench] one-shot all-reduce failed its check: {err}")
         tr.attach_oneshot(oneshot, W)
     if external:
         import torch.distributed as dist
@@ -290,6 +293,11 @@ def main(argv=None) -> int:
         tr.attach_comm(comm, W)
         if oneshot is not None:
             tr.attach_oneshot(oneshot, W)  # the step's collectives; RCCL broadcasts and is timed for comparison
+        elif W > 1 and os.environ.get("MNIST_AMD_PROBE_ONESHOT", "1") != "0":
+            # measure-only: the one-shot all-reduce is built, validated against the exact sum and timed in
+            # comm_profile next to RCCL's latency; the step keeps RCCL (never fatal)
+            from pytorch_ddp_mnist_amd.parallel.oneshot import probe_oneshot
+            probe, probe_err = probe_oneshot(ctx, tr.nparam)
         tr.broadcast_params(0)
         if pinned is not None:
             tr.set_plan(pinned)
@@ -311,7 +319,9 @@ def main(argv=None) -> int:
         # the captured schedules a calibration would time: nothing to choose
         tune = {"chosen": "eager-phases", "timings_ms": {}, "note": "external data plane: no graph schedules"}
     if (comm is not None or oneshot is not None) and use_graph:
-        prof = tr.comm_profile(reduce_max=ctx.all_reduce_max, tune=tune)
+        prof = tr.comm_profile(reduce_max=ctx.all_reduce_max, tune=tune, probe=probe)
+        if probe is not None or probe_err:
+            prof["oneshot_probe"] = "validated (measure-only)" if probe is not None else f"unavailable: {probe_err}"
 
     def run(n):
         tr.run_steps(n, use_graph=use_graph)  # k-step graphs (MNIST_AMD_GRAPH_STEPS), then single steps

@@ -23,8 +23,12 @@
 #include "common.h"
 #include "launch.h"
 #include "models.h"
+#include "wgrad.h"
 
 namespace {
+using wg::WgArgs;
+using wg::WgJob;
+using wg::wgrad_sgd_tile;
 
 template <typename T, class H, int MT, bool PRE = false>
 struct HeadSmem {
@@ -358,7 +362,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
             if (item) *reinterpret_cast<u32x4*>(sX + (r + q) * S::PX + c * 16 + h * 8) = pk[q][h];
           }
         }
-        if (TRAIN && item && !ABLATED(hb.ablate, 1)) {
+        if (TRAIN && item && !ABLATED(hb.ablate, 1) && hb.gx_images == nullptr) {
 #pragma unroll
           for (int j = 0; j < 16; ++j) {
             const int h = j >> 3, wd = (j & 7) >> 1, sh = 16 * (j & 1);
@@ -937,28 +941,6 @@ __global__ __launch_bounds__(256) void l1_split_kernel(BatchRef br, HeadBuffers 
 // one 16-byte load.  A 64x64 output block per workgroup (each wave 32x32 = 2x2 MFMA tiles);
 // the batch is split over gridDim.y, each split writes its own fp32 slab row (deterministic).
 // ====================================================================================
-template <typename T>
-struct WgJob {
-  const T* dyT;
-  const T* xT;
-  int N, K, NP, bias, out_off, nblk_k, blk_begin;
-};
-template <typename T>
-struct WgArgs {
-  WgJob<T> job[3];
-  int njobs, ldB, rlen, Bp, slab_ld;
-  // XCD-aware mode (xcd_ch > 0): 1-D grid; workgroup L runs on XCD L % 8 (round-robin dispatch) and
-  // reads only the batch rows the head kernel wrote from that XCD -- row chunks c = x, x+8, ... of
-  // xcd_ch rows (= head rows per workgroup) -- so its operands hit the XCD's own L2.
-  // contig: the head used the XCD-contiguous mapping (xcd_unit), so XCD x wrote chunks
-  // [x * nch / 8, (x + 1) * nch / 8) instead of x, x + 8, ...
-  int xcd_ch, nch, sx, contig;  // chunk rows, chunk count, splits per XCD
-  float* slab;
-  SgdFuse sgd;          // used when fuse != 0 (then splits == 1)
-  int fuse;
-  unsigned long long* stamps;  // optional phase stamps (MNIST_AMD_STAMPS): slots [STAMP_WGRAD + block][16]
-};
-
 template <typename T, int WD>
 __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
   using M = Mma<T>;
@@ -1076,21 +1058,23 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
 }
 
 // LDS-staged variant of wgrad_kernel (same tiles, splits, step order and slab layout; every output element
-// is the same MFMA chain, so the results are bitwise those of wgrad_kernel): per 32-row K-step the
-// workgroup stages the 64-row dY^T tile and the 64-row X^T tile ONCE (one 16-byte chunk of each per
-// thread, loaded a step ahead into registers), and each wave reads its 32x32 operands from LDS.  In
-// wgrad_kernel every fragment is fetched by two waves straight from L2 -- twice the L2 -> CU traffic,
-// which bounds that kernel (~37 GB/s per CU measured on the MLP at B=8192).  96-byte rows (64 data + 32
-// pad) make the fragment reads conflict-free for ds_read_b128's lane groups.  Needs 24 KB of LDS, so it
-// is for the schedules where nothing LDS-heavy runs beside it (the MLP; LeNet's FC wgrad shares the CUs
-// with conv_bwd and keeps the LDS-free kernel).
-template <typename T>
+// is the same MFMA chain, so the results are bitwise those of wgrad_kernel): the workgroup stages the 64-row
+// dY^T tile and the 64-row X^T tile of SUB consecutive 32-row K-steps ONCE per barrier interval (SUB 16-byte
+// chunks of each per thread, loaded an interval ahead into registers), and each wave reads its 32x32 operands
+// from LDS.  In wgrad_kernel every fragment is fetched by two waves straight from L2 -- twice the L2 -> CU
+// traffic, which bounds that kernel (~37 GB/s per CU measured on the MLP at B=8192).  SUB = 4 (128 batch rows
+// per barrier, 16 MFMAs per wave between barriers): with SUB = 1 every 4-MFMA step paid a barrier and an
+// L2 round trip of exposed latency.  Rows padded by 32 B (conflict-free fragment reads for ds_read_b128's
+// lane groups).  Needs 16 KB x SUB + padding of LDS, so it is for the schedules where nothing LDS-heavy
+// runs beside it (the MLP; LeNet's FC wgrad shares the CUs with conv_bwd and keeps the LDS-free kernel).
+template <typename T, int SUB>
 __global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
   using M = Mma<T>;
   using Frag = typename M::Frag;
   constexpr int KV = M::KV, KC = M::KC;
-  constexpr int PE = 96 / (int)sizeof(T);    // row pitch (elements): 64 B of data + 32 B of padding
-  constexpr int TILE = 64 * PE;              // one [64 rows][KC] tile
+  constexpr int ROWB = SUB * 64 + 32;                 // bytes per tile row: SUB steps x 64 B of data + 32 B pad
+  constexpr int PE = ROWB / (int)sizeof(T);           // row pitch (elements)
+  constexpr int TILE = 64 * PE;                       // one [64 rows][SUB * KC] tile
   __shared__ __attribute__((aligned(16))) T lds[2][2][TILE];  // [buffer][A = dY^T, B = X^T]
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
   const int lin = blockIdx.y * gridDim.x + blockIdx.x;
@@ -1119,6 +1103,7 @@ __global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
     return (a.contig ? x * (a.nch / 8) + m : x + 8 * m) * a.xcd_ch + (st % spc) * KC;
   };
   while (nsteps > 0 && step_row(nsteps - 1) >= a.Bp) --nsteps;  // steps past the (padded) batch
+  const int nint = (nsteps + SUB - 1) / SUB;                      // barrier intervals
   int j = 0;
   while (j + 1 < a.njobs && tile >= a.job[j + 1].blk_begin) ++j;
   const WgJob<T>& J = a.job[j];
@@ -1129,21 +1114,88 @@ __global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
   const int Kb = J.K + (J.bias ? 1 : 0);
   const bool wave_live = n0 < J.N && k0 < Kb;         // waves without outputs still stage and sync
 
-  // staging role: tile row r = tid / 4, 16-byte chunk c = tid % 4 of the step's KC elements
+  // staging role: tile row r = tid / 4, 16-byte chunk c = tid % 4 of each step's KC elements
   const int sr = tid >> 2, sc = tid & 3;
   const bool a_ok = nb0 + sr < J.NP, b_ok = kb0 + sr < J.K;
   const T* asrc = J.dyT + (size_t)min(nb0 + sr, J.NP - 1) * a.ldB + sc * KV;
   const T* bsrc = J.xT + (size_t)min(kb0 + sr, J.K > 0 ? J.K - 1 : 0) * a.ldB + sc * KV;
   const u32x4 z4 = u32x4{0u, 0u, 0u, 0u};
-  u32x4 ra, rb;
-  auto fetch = [&](int st) {
-    const int rc = step_row(st);
-    ra = *reinterpret_cast<const u32x4*>(asrc + rc);
-    rb = *reinterpret_cast<const u32x4*>(bsrc + rc);
+  u32x4 ra[SUB], rb[SUB];
+  // Gather job (GX, bf16, block-uniform): the B tile is [SUB * KC batch rows][64 pixels] (row pitch PG), built
+  // from the rows' uint8 pixels: item c = tid + 256 j (j < GJ) = tile row c / 4, 16-pixel chunk c % 4 (one
+  // 16-byte load); the row's sample index is loaded an interval earlier (gi), so each interval's pixel loads
+  // wait on no index load.  The MFMA B fragments are read with transposing ds_read_b64_tr_b16.
+  constexpr bool GXT = sizeof(T) == 2;
+  constexpr int PG = 64 + 8, GJ = SUB * KC * 4 / 256;
+  static_assert(!GXT || (GJ >= 1 && GJ <= SUB && SUB * KC * PG <= TILE), "gather tile");
+  const bool gx = GXT && J.gather;
+  const int32_t* gidx_base = gx ? a.gx_idx + (size_t)a.gx_step[0] * a.gx_stride : nullptr;
+  // sample indices (-1: row past the batch): gnx = the next interval to fetch, gtmp = the one after it
+  constexpr int GN = GXT ? GJ : 1;
+  int gnx[GN], gtmp[GN];
+  auto fetch_idx = [&](int it, int (&g)[GN]) {
+#pragma unroll
+    for (int j = 0; j < GN; ++j) {
+      const int c = tid + 256 * j, q = c / (4 * KC), rr = (c >> 2) % KC;
+      const int rg = step_row(min(it * SUB + q, nsteps - 1)) + rr;
+      g[j] = rg < a.gx_B ? gidx_base[rg] : -1;
+    }
   };
-  auto stage = [&](int buf) {
-    *reinterpret_cast<u32x4*>(&lds[buf][0][sr * PE + sc * KV]) = a_ok ? ra : z4;
-    *reinterpret_cast<u32x4*>(&lds[buf][1][sr * PE + sc * KV]) = b_ok ? rb : z4;
+  auto fetch = [&](int it, const int (&g)[GN]) {  // branch-free: steps past nsteps re-read the last step
+#pragma unroll
+    for (int q = 0; q < SUB; ++q) {
+      const int rc = step_row(min(it * SUB + q, nsteps - 1));
+      ra[q] = *reinterpret_cast<const u32x4*>(asrc + rc);
+      if (!gx) rb[q] = *reinterpret_cast<const u32x4*>(bsrc + rc);
+    }
+    if (gx) {
+#pragma unroll
+      for (int j = 0; j < GN; ++j) {
+        const int c = tid + 256 * j;
+        const int px = min(kb0 + (c & 3) * 16, 784 - 16);  // chunks past the image: any in-row address (k >= K unused)
+        rb[j] = *reinterpret_cast<const u32x4*>(a.gx_images + (size_t)max(g[j], 0) * 784 + px);
+      }
+    }
+  };
+  auto stage = [&](int buf, const int (&g)[GN]) {
+#pragma unroll
+    for (int q = 0; q < SUB; ++q) {
+      *reinterpret_cast<u32x4*>(&lds[buf][0][sr * PE + q * KC + sc * KV]) = a_ok ? ra[q] : z4;
+      if (!gx) *reinterpret_cast<u32x4*>(&lds[buf][1][sr * PE + q * KC + sc * KV]) = b_ok ? rb[q] : z4;
+    }
+    if constexpr (GXT) {
+      if (gx) {
+#pragma unroll
+        for (int j = 0; j < GJ; ++j) {
+          const int c = tid + 256 * j;
+          const bool live = g[j] >= 0;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            bf16x8 f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+              f[e] = (bf16)(live ? mnist_norm((rb[j][2 * h + (e >> 2)] >> (8 * (e & 3))) & 255u) : 0.f);
+            *reinterpret_cast<bf16x8*>(&lds[buf][1][(c >> 2) * PG + (c & 3) * 16 + h * 8]) = f;
+          }
+        }
+      }
+    }
+  };
+  // B fragment of gather job: pixel column kl (tile-local) of batch rows q * KC + grp * KV .. + 7 (the lane's k
+  // run of the MFMA), as two 4-row x 16-column blocks transposed by the read (lane 4 i + p of a 16-lane group
+  // addresses row i, columns 4 p .. 4 p + 3; lane l receives column l)
+  auto load_gx = [&](int buf, int q, int kl) -> Frag {
+    Frag f;
+    if constexpr (GXT) {
+      typedef short v4s __attribute__((ext_vector_type(4)));
+      const T* p = &lds[buf][1][(q * KC + grp * KV + ((lane & 15) >> 2)) * PG + kl + 4 * (lane & 3)];
+      const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(const_cast<T*>(p)));
+      const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(const_cast<T*>(p + 4 * PG)));
+      f.v = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    } else {
+      f = M::zero();
+    }
+    return f;
   };
 
   f32x4 acc[2][2];
@@ -1161,23 +1213,40 @@ __global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
   const int ao0 = (n0 - nb0 + row) * PE + grp * KV, ao1 = ao0 + 16 * PE;
   const int bo0 = (k0 - kb0 + row) * PE + grp * KV, bo1 = bo0 + 16 * PE;
 
-  if (nsteps > 0) {
-    fetch(0);
-    stage(0);
+  if (nint > 0) {
+    if (gx) {
+      fetch_idx(0, gtmp);
+      fetch_idx(1, gnx);  // (clamped to the last step when nint == 1; unused then)
+    }
+    fetch(0, gtmp);
+    stage(0, gtmp);
   }
   __syncthreads();
-  for (int st = 0; st < nsteps; ++st) {
-    const int buf = st & 1;
-    if (st + 1 < nsteps) fetch(st + 1);  // next step's chunks in flight during this step's MFMAs
-    const Frag a0 = M::load(&lds[buf][0][ao0]), a1 = M::load(&lds[buf][0][ao1]);
-    const Frag f0 = M::load(&lds[buf][1][bo0]), f1 = M::load(&lds[buf][1][bo1]);
-    const Frag b0 = sel0 == 0 ? f0 : (sel0 == 1 ? ones : zf);
-    const Frag b1 = sel1 == 0 ? f1 : (sel1 == 1 ? ones : zf);
-    M::mma(acc[0][0], a0, b0);
-    M::mma(acc[0][1], a0, b1);
-    M::mma(acc[1][0], a1, b0);
-    M::mma(acc[1][1], a1, b1);
-    if (st + 1 < nsteps) stage(buf ^ 1);  // that buffer was last read in step st - 1, before the barrier
+  const int gk0 = (k0 - kb0), gk1 = gk0 + 16;  // gather job: tile-local pixel columns of this wave's fragments
+  for (int it = 0; it < nint; ++it) {
+    const int buf = it & 1;
+    if (it + 1 < nint) fetch(it + 1, gnx);  // next interval's chunks in flight during this interval's MFMAs
+    if (gx && it + 2 < nint) fetch_idx(it + 2, gtmp);  // gather: the indices of the interval after next
+    const int nq = min(SUB, nsteps - it * SUB);  // live steps of this interval (block-uniform)
+#pragma unroll
+    for (int q = 0; q < SUB; ++q) {
+      if (q < nq) {
+        const Frag a0 = M::load(&lds[buf][0][ao0 + q * KC]), a1 = M::load(&lds[buf][0][ao1 + q * KC]);
+        const Frag f0 = gx ? load_gx(buf, q, gk0) : M::load(&lds[buf][1][bo0 + q * KC]);
+        const Frag f1 = gx ? load_gx(buf, q, gk1) : M::load(&lds[buf][1][bo1 + q * KC]);
+        const Frag b0 = sel0 == 0 ? f0 : (sel0 == 1 ? ones : zf);
+        const Frag b1 = sel1 == 0 ? f1 : (sel1 == 1 ? ones : zf);
+        M::mma(acc[0][0], a0, b0);
+        M::mma(acc[0][1], a0, b1);
+        M::mma(acc[1][0], a1, b0);
+        M::mma(acc[1][1], a1, b1);
+      }
+    }
+    if (it + 1 < nint) stage(buf ^ 1, gnx);  // that buffer was last read in interval it - 1, before the barrier
+    if (gx) {
+#pragma unroll
+      for (int j = 0; j < GN; ++j) gnx[j] = gtmp[j];
+    }
     __syncthreads();
   }
   if (!wave_live) return;
@@ -1198,91 +1267,9 @@ __global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
   if (a.stamps && threadIdx.x == 0 && lin < 512) a.stamps[(STAMP_WGRAD + lin) * 16 + 1] = wall_clock64();
 }
 
-// Weight-gradient GEMM + SGD update for one GPU and ONE batch split (small batches): every output
-// element is the whole gradient, so the update is the epilogue -- g = scale * dW, momentum, parameter,
-// packed operand images, device step counters -- and the separate reduce + SGD kernel disappears
-// (bitwise equal to wgrad -> reduce_sgd: a one-slab reduce is (0 + dW) * scale).  One 16x16 output tile
-// per wave and a 32x32 tile per block: few MFMAs and few memory operations per wave, so the whole K
-// range is prefetched at once and the epilogue's stores stay within one wave's outstanding-operation
-// budget (the 32x32-per-wave variant stalled on it).
 template <typename T, class Model>
 __global__ __launch_bounds__(256) void wgrad_sgd_kernel(WgArgs<T> a) {
-  using M = Mma<T>;
-  using Frag = typename M::Frag;
-  constexpr int KV = M::KV, KC = M::KC, FPS = 8;
-  const int lane = threadIdx.x & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
-  auto stamp = [&](int k) {
-    if (a.stamps && threadIdx.x == 0 && blockIdx.x < 512) a.stamps[(STAMP_WGRAD + blockIdx.x) * 16 + k] = wall_clock64();
-  };
-  stamp(0);
-  const int tile = blockIdx.x;
-  if (a.sgd.step_ptr && tile == 0 && threadIdx.x == 0) {
-    a.sgd.step_ptr[0] += 1;  // nothing after the head reads the batch counter in this step
-    a.sgd.step_ptr[1] += 1;
-  }
-  int j = 0;
-  while (j + 1 < a.njobs && tile >= a.job[j + 1].blk_begin) ++j;
-  const WgJob<T>& J = a.job[j];
-  const int lb = tile - J.blk_begin;
-  const int bn = lb / J.nblk_k, bk = lb % J.nblk_k;
-  const int n0 = bn * 32 + (w >> 1) * 16, k0 = bk * 32 + (w & 1) * 16;
-  const int Kb = J.K + (J.bias ? 1 : 0);
-  if (n0 >= J.N || k0 >= Kb) return;  // wave-uniform
-  const int nsteps = a.Bp / KC;
-
-  const T* ap = J.dyT + (size_t)(n0 + row) * a.ldB + grp * KV;  // rows < NP (zero padded)
-  const int kk = k0 + row;
-  const T* bp = J.xT + (size_t)min(kk, J.K > 0 ? J.K - 1 : 0) * a.ldB + grp * KV;
-  const int sel = kk < J.K ? 0 : (kk == J.K && J.bias ? 1 : 2);
-  Frag ones;
-#pragma unroll
-  for (int q = 0; q < KV; ++q) M::set(ones, q, 1.f);
-  const Frag zf = M::zero();
-
-  // the first FPS K-steps' fragments, then the SGD operands (the MFMAs wait only for the former)
-  Frag fa[FPS], fb[FPS];
-#pragma unroll
-  for (int st = 0; st < FPS; ++st) {
-    const int rc = min(st, nsteps - 1) * KC;
-    fa[st] = M::load(ap + rc);
-    fb[st] = M::load(bp + rc);
-  }
-  int pidx[4];
-  float pv[4], mv[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int n = n0 + grp * 4 + i;
-    const int q = n >= J.N ? -1 : (kk < J.K ? n * J.K + kk : (kk == J.K && J.bias ? J.N * J.K + n : -1));
-    pidx[i] = q < 0 ? -1 : J.out_off + q;
-    const int p = max(pidx[i], 0);
-    pv[i] = a.sgd.params[p];
-    mv[i] = a.sgd.mom ? a.sgd.mom[p] : 0.f;
-  }
-  f32x4 acc = zero4();
-#pragma unroll
-  for (int st = 0; st < FPS; ++st)
-    if (st < nsteps) M::mma(acc, fa[st], sel == 0 ? fb[st] : (sel == 1 ? ones : zf));
-  for (int st = FPS; st < nsteps; ++st) {  // longer batches: the rest, one step at a time
-    const Frag x = M::load(ap + st * KC), y = M::load(bp + st * KC);
-    M::mma(acc, x, sel == 0 ? y : (sel == 1 ? ones : zf));
-  }
-  stamp(1);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    if (pidx[i] < 0) continue;
-    const int p = pidx[i];
-    float g = (0.f + acc[i]) * a.sgd.scale;  // = reduce_sgd over one slab
-    a.sgd.grad[p] = g;
-    if (a.sgd.mom) {
-      const float b = a.sgd.momentum * mv[i] + g;
-      a.sgd.mom[p] = b;
-      g = b;
-    }
-    const float nv = pv[i] - a.sgd.lr * g;
-    a.sgd.params[p] = nv;
-    Packer<Model, T>::pack(p, nv, reinterpret_cast<T*>(a.sgd.pack));
-  }
-  stamp(2);
+  wgrad_sgd_tile<T, Model>(a, blockIdx.x);
 }
 
 // wgrad_kernel keeps ONE ring slot of K-step fragments per wave (the next step's fragments fetched while this
@@ -1290,44 +1277,14 @@ __global__ __launch_bounds__(256) void wgrad_sgd_kernel(WgArgs<T> a) {
 // LDS-staged weight gradient (wgrad_lds_kernel) is used for the MLP, whose wgrad runs alone on the chip; the
 // LeNet wgrad runs beside conv_bwd, which holds the LDS.
 constexpr int WGRAD_DEPTH = 1;
+constexpr int WGRAD_SUB = 4;  // wgrad_lds_kernel: 32-row K-steps staged per barrier interval
 
 template <typename T, class H, class Model>
 int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab_ld, int xcd_ch, hipStream_t s,
                  const SgdFuse* fuse, int job_mask) {
-  WgArgs<T> a{};
-  const int BT = fuse ? 32 : 64;  // output tile per block (wgrad_sgd_kernel: 32, wgrad_kernel: 64)
-  int nj = 0;
-  auto mk = [&](int layer, const void* dy, const void* x, int N, int K, int NP, bool bias, int off, int& blk) {
-    if (!(job_mask >> layer & 1)) return;
-    WgJob<T>& J = a.job[nj++];
-    J.dyT = reinterpret_cast<const T*>(dy);
-    J.xT = reinterpret_cast<const T*>(x);
-    J.N = N; J.K = K; J.NP = NP; J.bias = bias ? 1 : 0; J.out_off = off;
-    J.nblk_k = (K + (bias ? 1 : 0) + BT - 1) / BT;
-    J.blk_begin = blk;
-    blk += ((N + BT - 1) / BT) * J.nblk_k;
-  };
   int blk = 0;
-  mk(0, hb.dy1T, hb.xT, H::N1, H::K0, H::N1P, true, H::W1, blk);
-  mk(1, hb.dy2T, hb.h1T, H::N2, H::N1, H::N2P, true, H::W2, blk);
-  mk(2, hb.dy3T, hb.h2T, H::NC, H::N2, H::NCP, H::BIAS3, H::W3, blk);
-  if (nj == 0) throw std::invalid_argument("wgrad: empty job mask");
-  a.njobs = nj;
-  a.ldB = hb.ldB;
+  WgArgs<T> a = wg::make_args<T, H, Model>(hb, B, splits, slab, slab_ld, fuse, job_mask, &blk);
   constexpr int KC = Mma<T>::KC;
-  a.Bp = rup(B, KC);
-  splits = std::max(1, std::min(splits, a.Bp / KC));
-  a.rlen = rup((a.Bp + splits - 1) / splits, KC);
-  splits = (a.Bp + a.rlen - 1) / a.rlen;
-  if (fuse) {
-    if (splits != 1) throw std::invalid_argument("wgrad with the SGD epilogue needs one batch split");
-    a.sgd = *fuse;
-    a.fuse = 1;
-  }
-  a.slab = slab;
-  a.slab_ld = slab_ld;
-  a.stamps = hb.stamps;
-  a.xcd_ch = 0;
   const bool lds_stage = std::is_same<Model, MlpModel>::value;
   // XCD-aware mapping when the head's row tiling is known and the split count divides over 8 XCDs
   if (!fuse && xcd_ch > 0 && xcd_ch % KC == 0 && splits % 8 == 0) {
@@ -1336,12 +1293,12 @@ int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab
     a.sx = splits / 8;
     const int head_grid = (rup(B, 32) + xcd_ch - 1) / xcd_ch;  // head_launch_mtw's grid
     a.contig = hb.xcd && head_grid % 8 == 0 && a.nch == head_grid;
-    if (lds_stage) hipLaunchKernelGGL(wgrad_lds_kernel<T>, dim3(blk * splits), dim3(256), 0, s, a);
+    if (lds_stage) hipLaunchKernelGGL((wgrad_lds_kernel<T, WGRAD_SUB>), dim3(blk * splits), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((wgrad_kernel<T, WGRAD_DEPTH>), dim3(blk * splits), dim3(256), 0, s, a);
   } else if (a.fuse) {
     hipLaunchKernelGGL((wgrad_sgd_kernel<T, Model>), dim3(blk), dim3(256), 0, s, a);
   } else {
-    if (lds_stage) hipLaunchKernelGGL(wgrad_lds_kernel<T>, dim3(blk, splits), dim3(256), 0, s, a);
+    if (lds_stage) hipLaunchKernelGGL((wgrad_lds_kernel<T, WGRAD_SUB>), dim3(blk, splits), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((wgrad_kernel<T, WGRAD_DEPTH>), dim3(blk, splits), dim3(256), 0, s, a);
   }
   return splits;

@@ -51,6 +51,14 @@ struct HeadBuffers {
   float drop_p;
   int32_t xcd = 0;       // the head kernel used the XCD-contiguous row mapping (BatchRef::xcd)
   int32_t ablate = 0;    // diagnostics only (MNIST_AMD_HEAD_ABLATE): bit 0 = skip the X^T stores (wrong wgrad)
+  // X^T re-gather (MLP bf16, LDS-staged weight gradient): when gx_images is set, the head does NOT write X^T
+  // and the layer-1 weight gradient gathers the batch rows' uint8 pixels itself (idx_epoch[step * stride + r],
+  // normalised in registers, transposed by its LDS reads) -- bitwise the operand the head would have stored
+  const uint8_t* gx_images = nullptr;
+  const int32_t* gx_idx = nullptr;
+  const int32_t* gx_step = nullptr;
+  int32_t gx_stride = 0;
+  int32_t gx_B = 0;      // rows of the batch (rows past it are zero)
 };
 
 struct LenetConvBuffers {
@@ -137,6 +145,10 @@ int launch_lenet_head16(DType t, const BatchRef& br, const HeadBuffers& hb, hipS
 // block walks ceil(B / target) images, so a smaller target leaves whole CUs free (for RCCL kernels).
 void launch_lenet_conv_bwd(DType t, const BatchRef& br, const LenetConvBuffers& cb, int* nslab_out,
                            hipStream_t s, int target_blocks = 0);
+// Small batches (one GPU, one FC batch split): conv_bwd + the FC weight gradient with its SGD update (as
+// launch_head_wgrad with `fuse`) in ONE kernel; returns the conv slab count (the conv update follows).
+int launch_lenet_conv_bwd_fc(DType t, const BatchRef& br, const LenetConvBuffers& cb, const HeadBuffers& hb,
+                             const SgdFuse& fuse, hipStream_t s, int target_blocks = 0);
 int lenet_conv_bwd_blocks(int B, int target_blocks = 0);
 int lenet_conv_bwd_max_blocks(int B, int target_blocks = 0);  // slab rows needed for any batch <= B
 

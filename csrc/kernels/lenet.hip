@@ -25,6 +25,7 @@
 #include "common.h"
 #include "launch.h"
 #include "models.h"
+#include "wgrad.h"
 
 namespace {
 
@@ -886,9 +887,9 @@ struct BwdRoles {
   }
 };
 
+// One conv_bwd workgroup: block `blk` of `nblk` (the conv_bwd part of the grid).
 template <typename T, int NW>
-__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 8 ? 4 : 1)))
-void conv_bwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
+DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int ipb, const int blk, const int nblk) {
   using M = Mma<T>;
   using Frag = typename M::Frag;
   using S = BwdSmem<T>;
@@ -904,7 +905,7 @@ void conv_bwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
   uint8_t* m1s = reinterpret_cast<uint8_t*>(smem + S::OFF_M1);
   float* red = reinterpret_cast<float*>(smem + S::OFF_RED);
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
-  const int unit = xcd_unit(blockIdx.x, gridDim.x, br.xcd);  // images [unit * ipb, +ipb), slab row unit
+  const int unit = xcd_unit(blk, nblk, br.xcd);  // images [unit * ipb, +ipb), slab row unit
   const BlockIdx bidx(br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride, unit * ipb, ipb, br.B);
   const T* pack = reinterpret_cast<const T*>(cb.pack);
   const T* dp2 = reinterpret_cast<const T*>(cb.dp2);
@@ -912,7 +913,7 @@ void conv_bwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
   // optional wall-clock stamps (profiling): [0] start, [1] setup, 3 per image for images 0..3,
   // [14] loop end, [15] slab written
   auto stamp = [&](int k) {
-    if (cb.stamps && tid == 0 && blockIdx.x < 512) cb.stamps[blockIdx.x * 16 + k] = wall_clock64();
+    if (cb.stamps && tid == 0 && blk < 512) cb.stamps[blk * 16 + k] = wall_clock64();
   };
   stamp(0);
 
@@ -1401,8 +1402,30 @@ void conv_bwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
   }
   stamp(15);
   // this block's hardware location, in its own row range (cb.stamps starts at STAMP_CONV_BWD)
-  if (cb.stamps && tid == 0 && blockIdx.x < 512)
-    cb.stamps[(STAMP_BWD_HWLOC - STAMP_CONV_BWD + blockIdx.x) * 16] = hw_location();
+  if (cb.stamps && tid == 0 && blk < 512)
+    cb.stamps[(STAMP_BWD_HWLOC - STAMP_CONV_BWD + blk) * 16] = hw_location();
+}
+
+template <typename T, int NW>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 8 ? 4 : 1)))
+void conv_bwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
+  conv_bwd_block<T, NW>(br, cb, ipb, blockIdx.x, gridDim.x);
+}
+
+// Small batches, one GPU, one FC batch split: conv_bwd and the FC weight gradient + SGD update (wg::
+// wgrad_sgd_tile, the wgrad_sgd_kernel body) in ONE launch -- workgroups [0, nconv) are conv_bwd's, the rest
+// one 32x32 FC output tile each (waves 4.. of a wider workgroup idle).  The two touch disjoint data (FC
+// operands and FC parameters / images vs the conv ones), as in the concurrent two-stream schedule, so this is
+// that schedule without the fork / join: the serial small-batch chain loses a kernel boundary and the FC
+// update runs in conv_bwd's shadow.  The step counters are bumped by the conv update that follows.
+template <typename T, int NW>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 8 ? 4 : 1)))
+void conv_bwd_fc_kernel(BatchRef br, LenetConvBuffers cb, int ipb, int nconv, wg::WgArgs<T> fa) {
+  if ((int)blockIdx.x < nconv) {
+    conv_bwd_block<T, NW>(br, cb, ipb, blockIdx.x, nconv);
+  } else if (threadIdx.x < 256) {
+    wg::wgrad_sgd_tile<T, LenetModel>(fa, (int)blockIdx.x - nconv);
+  }
 }
 
 }  // namespace
@@ -1470,4 +1493,19 @@ void launch_lenet_conv_bwd(DType t, const BatchRef& br, const LenetConvBuffers& 
   // every VGPR of the SIMDs and starve the FC weight gradient that runs beside conv_bwd, 0.119-0.127 vs 0.103 ms)
   if (t == DType::F32) hipLaunchKernelGGL((conv_bwd_kernel<float, 8>), dim3(grid), dim3(512), 0, s, br, cb, ipb);
   else hipLaunchKernelGGL((conv_bwd_kernel<bf16, 4>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
+}
+
+int launch_lenet_conv_bwd_fc(DType t, const BatchRef& br, const LenetConvBuffers& cb, const HeadBuffers& hb,
+                             const SgdFuse& fuse, hipStream_t s, int target_blocks) {
+  const int ipb = bwd_ipb(br.B, target_blocks), nconv = (br.B + ipb - 1) / ipb;
+  if (br.B <= 0) return nconv;
+  int splits = 1, nfc = 0;
+  if (t == DType::F32) {
+    const auto fa = wg::make_args<float, LenetModel::Head, LenetModel>(hb, br.B, splits, nullptr, 0, &fuse, 7, &nfc);
+    hipLaunchKernelGGL((conv_bwd_fc_kernel<float, 8>), dim3(nconv + nfc), dim3(512), 0, s, br, cb, ipb, nconv, fa);
+  } else {
+    const auto fa = wg::make_args<bf16, LenetModel::Head, LenetModel>(hb, br.B, splits, nullptr, 0, &fuse, 7, &nfc);
+    hipLaunchKernelGGL((conv_bwd_fc_kernel<bf16, 4>), dim3(nconv + nfc), dim3(256), 0, s, br, cb, ipb, nconv, fa);
+  }
+  return nconv;
 }

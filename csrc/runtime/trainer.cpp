@@ -202,6 +202,19 @@ HeadBuffers Trainer::head_buffers(float* metrics) const {
   return hb;
 }
 
+void Trainer::set_regather(HeadBuffers& hb, const BatchRef& br, bool fused_wgrad) const {
+#ifndef MNIST_AMD_NO_REGATHER  // (A/B builds only: X^T written by the head and read back by the wgrad)
+  if (model_ != ModelKind::MLP || dtype_ != DType::BF16 || fused_wgrad) return;
+  hb.gx_images = br.images;
+  hb.gx_idx = br.idx_epoch;
+  hb.gx_step = br.step_ptr;
+  hb.gx_stride = br.batch_stride;
+  hb.gx_B = br.B;
+#else
+  (void)hb; (void)br; (void)fused_wgrad;
+#endif
+}
+
 LenetConvBuffers Trainer::conv_buffers() const {
   LenetConvBuffers cb;
   cb.params = ptr<const float>(p_.params);
@@ -227,7 +240,8 @@ void Trainer::forward_backward(int B, uintptr_t stream) {
   hipStream_t s = S(stream);
   if (B <= 0 || B > batch_) throw std::invalid_argument("forward_backward: bad batch size");
   const BatchRef br = batch_ref(B);
-  const HeadBuffers hb = head_buffers(ptr<float>(p_.metrics));
+  HeadBuffers hb = head_buffers(ptr<float>(p_.metrics));
+  set_regather(hb, br, false);
   int hrows = 0;
   if (model_ == ModelKind::LENET) {
     if (fwd_head_active(B)) hrows = launch_lenet_fwd_head(dtype_, br, conv_buffers(), hb, s);
@@ -305,10 +319,11 @@ std::vector<Bucket> Trainer::issued_collectives() const {
 void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
   if (B <= 0 || B > batch_) throw std::invalid_argument("train_step: bad batch size");
   const BatchRef br = batch_ref(B);
-  const HeadBuffers hb = head_buffers(ptr<float>(p_.metrics));
+  HeadBuffers hb = head_buffers(ptr<float>(p_.metrics));
   const float scale = 1.0f / float(B);
   const int cp = model_conv_params(model_);
   const bool comm = use_comm();
+  set_regather(hb, br, model_ == ModelKind::MLP && !comm && fc_splits_ == 1 && fuse_wgrad_sgd_);
   last_stream_ = s;
   // deferred join of the previous step's aux branch: the head overwrites the activations its FC wgrad
   // read and reads the FC weights its FC update wrote (conv_fwd touches neither, so with separate
@@ -393,6 +408,29 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
                     momentum_ != 0.f ? ptr<float>(p_.mom) : nullptr,  // as launch_reduce_sgd
                     ptr<void>(p_.pack), ptr<int32_t>(p_.step)};
     launch_head_wgrad(model_, dtype_, hb, B, 1, ptr<float>(p_.slab_fc), nparam_, s, hrows, &f);
+    post_launch(s);
+    return;
+  }
+  if (model_ == ModelKind::LENET && fc_splits_ == 1 && fuse_wgrad_sgd_) {
+    // serial single-GPU schedule, one FC batch split (small batches): the FC update is the wgrad kernel's
+    // epilogue (it touches only FC parameters / operand images, which conv_bwd does not read), and the closing
+    // reduce + SGD covers the conv parameters only (bitwise equal to wgrad -> reduce_sgd over all of them)
+    const SgdFuse f{scale, lr_, momentum_, ptr<float>(p_.params), ptr<float>(p_.grad),
+                    momentum_ != 0.f ? ptr<float>(p_.mom) : nullptr, ptr<void>(p_.pack), nullptr};
+#ifndef MNIST_AMD_NO_BWD_FC  // (A/B builds only: the FC wgrad + update as its own kernel before conv_bwd)
+    // ... as extra workgroups of the conv_bwd launch (one kernel instead of two)
+    const int nslab = launch_lenet_conv_bwd_fc(dtype_, br, conv_buffers(), hb, f, s, bwd_blocks_);
+    post_launch(s);
+#else
+    launch_head_wgrad(model_, dtype_, hb, B, 1, ptr<float>(p_.slab_fc), nparam_, s, hrows, &f);
+    post_launch(s);
+    int nslab = 0;
+    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s, bwd_blocks_);
+    post_launch(s);
+#endif
+    launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
+                      nparam_, 1, cp, 0, cp, scale, ptr<float>(p_.params), ptr<float>(p_.grad), ptr<float>(p_.mom),
+                      ptr<void>(p_.pack), lr_, momentum_, ptr<int32_t>(p_.step), s);
     post_launch(s);
     return;
   }

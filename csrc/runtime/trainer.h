@@ -136,6 +136,9 @@ class Trainer {
  private:
   BatchRef batch_ref(int B) const;
   HeadBuffers head_buffers(float* metrics) const;
+  // MLP bf16 training: the layer-1 weight gradient re-gathers the batch's uint8 rows (the head skips its X^T
+  // stores), unless the step's wgrad is the SGD-fused one (no LDS staging)
+  void set_regather(HeadBuffers& hb, const BatchRef& br, bool fused_wgrad) const;
   LenetConvBuffers conv_buffers() const;
   // defer_join: (single GPU, concurrent schedule, inside a multi-step graph) leave the aux branch (FC
   // wgrad + FC update) un-joined at the end of the step; the NEXT step's head waits for it instead.

@@ -522,7 +522,8 @@ class NativeTrainer:
             log(out)
         return out
 
-    def comm_profile(self, reduce_max=None, iters: int = 48, warmup: int = 8, tune: Optional[dict] = None) -> dict:
+    def comm_profile(self, reduce_max=None, iters: int = 48, warmup: int = 8, tune: Optional[dict] = None,
+                     probe=None) -> dict:
         """Attributable communication figures of the installed plan (bench JSON ``comm_profile``).
 
         * ``rccl_world`` -- ranks of the RCCL communicator;
@@ -530,7 +531,9 @@ class NativeTrainer:
           size, captured in its own graph and replayed back to back (median of ``iters``, rank-max);
         * ``step_plan_ms`` / ``step_local_ms`` / ``exposed_comm_us`` -- the captured step with the plan's
           collectives vs the local single-GPU schedule without any, interleaved replays (taken from
-          ``tune`` when the calibration already timed both).
+          ``tune`` when the calibration already timed both);
+        * ``probe``: a validated one-shot all-reduce that the step does NOT use (measure-only): its standalone
+          latency per collective is reported next to RCCL's (``oneshot_us``).
         Collective: every rank calls it at the same point."""
         if self.comm is None and self.oneshot is None:
             return {"rccl_world": None}
@@ -551,9 +554,10 @@ class NativeTrainer:
                 med = ts[len(ts) // 2]
                 med = reduce_max(med) if reduce_max is not None else med
                 row["allreduce_us"] = round(med * 1000.0, 2)
-            if self.oneshot is not None:
+            os_ = self.oneshot if self.oneshot is not None else probe
+            if os_ is not None:
                 from ..parallel.oneshot import time_oneshot
-                med = time_oneshot(self.oneshot, b - a, self.device, iters=iters, warmup=warmup)
+                med = time_oneshot(os_, b - a, self.device, iters=iters, warmup=warmup)
                 med = reduce_max(med) if reduce_max is not None else med
                 row["oneshot_us"] = round(med * 1000.0, 2)
             colls.append(row)

@@ -33,16 +33,27 @@ def make_oneshot(ctx, max_count: int, nblk: int = 64, timeout_s: Optional[float]
     from ..ops.native import load_c
     C = load_c()
     dev = ctx.device.index if ctx.device.type == "cuda" and ctx.device.index is not None else torch.cuda.current_device()
-    o = C.OneShotAllReduce(ctx.rank, ctx.world, int(dev), int(max_count), int(nblk),
-                           oneshot_timeout() if timeout_s is None else float(timeout_s))
-    if ctx.world > 1:
-        _GEN[0] += 1
-        store = dist.distributed_c10d._get_default_store()
-        store.set(KEY.format(gen=_GEN[0], rank=ctx.rank), o.handle())
-        keys = [KEY.format(gen=_GEN[0], rank=r) for r in range(ctx.world)]
-        store.wait(keys, datetime.timedelta(seconds=init_timeout_s))
-        o.open_peers([bytes(store.get(k)) for k in keys])
-        ctx.barrier()  # every rank has mapped every region before the first call
+    if ctx.world == 1:
+        return C.OneShotAllReduce(ctx.rank, ctx.world, int(dev), int(max_count), int(nblk),
+                                  oneshot_timeout() if timeout_s is None else float(timeout_s))
+    _GEN[0] += 1
+    store = dist.distributed_c10d._get_default_store()
+    mine = KEY.format(gen=_GEN[0], rank=ctx.rank)
+    try:
+        o = C.OneShotAllReduce(ctx.rank, ctx.world, int(dev), int(max_count), int(nblk),
+                               oneshot_timeout() if timeout_s is None else float(timeout_s))
+        h = o.handle()
+    except Exception:
+        store.set(mine, b"")  # tell the peers at once instead of letting them wait out the deadline
+        raise
+    store.set(mine, h)
+    keys = [KEY.format(gen=_GEN[0], rank=r) for r in range(ctx.world)]
+    store.wait(keys, datetime.timedelta(seconds=init_timeout_s))
+    handles = [bytes(store.get(k)) for k in keys]
+    if any(not x for x in handles):
+        raise RuntimeError(f"rank {ctx.rank}: a peer failed to create its one-shot region")
+    o.open_peers(handles)
+    ctx.barrier()  # every rank has mapped every region before the first call
     return o
 
 
@@ -69,3 +80,43 @@ def time_oneshot(o, count: int, device, iters: int = 48, warmup: int = 8):
         raise RuntimeError(err)
     ts = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(iters))
     return ts[len(ts) // 2]
+
+
+def validate_oneshot(ctx, o, count: int) -> str:
+    """Collective correctness check of a freshly built one-shot all-reduce against the exact host sum: rank r
+    contributes (r + 1) * (i % 97 + 1) / 8 at element i (exact in fp32 for W <= 8, any summation order), two
+    calls (both buffer parities).  Returns "" on every rank if every rank matched, else the failures.  The
+    verdict is agreed over the control plane, so all ranks take the same decision."""
+    try:
+        i = torch.arange(count, dtype=torch.float32, device=ctx.device) % 97 + 1
+        expect = i * (ctx.world * (ctx.world + 1) / 2) / 8
+        ok = True
+        for _ in range(2):
+            x = i * (ctx.rank + 1) / 8
+            s = torch.cuda.current_stream(ctx.device)
+            o.all_reduce_sum_f32(x.data_ptr(), count, s.cuda_stream)
+            s.synchronize()
+            ok = ok and bool(torch.equal(x, expect)) and o.check() == ""
+        err = "" if ok else f"rank {ctx.rank}: one-shot all-reduce result differs from the exact sum"
+    except Exception as e:  # noqa: BLE001 -- any failure disqualifies the probe
+        err = f"rank {ctx.rank}: {e}"
+    bad = ctx.all_reduce_sum([0.0 if not err else 1.0])[0] if ctx.world > 1 else (1.0 if err else 0.0)
+    if bad:
+        return err or f"{int(bad)} rank(s) failed the one-shot check"
+    return ""
+
+
+def probe_oneshot(ctx, max_count: int):
+    """Measure-only one-shot all-reduce next to RCCL (bench.py at world > 1 with ``--allreduce rccl``): built,
+    exchanged and validated, or None with the reason -- never fatal, and agreed by every rank."""
+    err = ""
+    o = None
+    try:
+        o = make_oneshot(ctx, max_count)
+    except Exception as e:  # noqa: BLE001
+        err = f"rank {ctx.rank}: {e}"
+    failed = ctx.all_reduce_sum([1.0 if err else 0.0])[0] if ctx.world > 1 else (1.0 if err else 0.0)
+    if failed:
+        return None, err or "one-shot bring-up failed on another rank"
+    err = validate_oneshot(ctx, o, max_count)
+    return (None, err) if err else (o, "")

@@ -26,6 +26,8 @@ def cycles(kind, addrs):
         groups, nb, width, ideal = B128_GROUPS, 64, 4, 4
     elif kind in ("r32", "w8", "w16", "w32"):
         groups, nb, width, ideal = [list(range(32)), list(range(32, 64))], 32, 1, 2
+    elif kind == "r64tr":  # ds_read_b64_tr_b16: 2 x 32 lanes, bank = dword % 64, 2 dwords per lane
+        groups, nb, width, ideal = [list(range(32)), list(range(32, 64))], 64, 2, 2
     elif kind == "w128":
         groups, nb, width, ideal = [list(range(8 * i, 8 * i + 8)) for i in range(8)], 32, 4, 8
     else:
@@ -51,7 +53,7 @@ def model(P):
     OFF_XS = 0
     OFF_P1T = rup(OFF_XS + XPL * XP * T, 16)
     OFF_DY2T = rup(OFF_P1T + PPL * P1P * T, 16)
-    OFF_DYS = rup(OFF_DY2T + 16 * D2P * T, 16)
+    OFF_DYS = rup(OFF_DY2T + (0 if P.get("TRA") else 16 * D2P * T), 16)
     OFF_W2 = rup(OFF_DYS + P["DYS_N"] * T, 16)
     OFF_DY1T = rup(OFF_W2 + 16 * W2P * T, 16)
     OFF_M1 = rup(OFF_DY1T + 8 * D1P * T, 16)
@@ -113,7 +115,17 @@ def model(P):
                             if px - kw >= 0:
                                 ad[l] = OFF_P1T + T * ((kw * 6 + c) * P1P + py * P1R + px - kw)
                     add("A.p1t", "w16", ad)
-        for r in range(2):
+        if P.get("TRA"):  # bf16: two channels per thread, one 32-bit DYS store per window, no DY2T image
+            for win in range(4):
+                ad = {}
+                for tid, l in lanes:
+                    if tid < 200:
+                        n0, p = 2 * (tid & 7), tid >> 3
+                        py, px = p // 5, p % 5
+                        oh, ow = 2 * py + (win >> 1), 2 * px + (win & 1)
+                        ad[l] = OFF_DYS + T * dys_idx(oh, ow, n0)
+                add("A.dys", "w32", ad)
+        for r in range(0 if P.get("TRA") else 2):
             for win in range(4):
                 a1, a2 = {}, {}
                 for tid, l in lanes:
@@ -154,12 +166,22 @@ def model(P):
                 offs[l] = o
             w2off.append(offs)
         for kc in range(5):
-            ad = {}
-            for l in range(64):
-                row, grp = l & 15, l >> 4
-                p0 = kc * 32 + grp * 8
-                ad[l] = OFF_DY2T + T * (row * D2P + (p0 >> 4) * D2R + (p0 & 15))
-            add("B1.dy2t", "r128", ad)
+            if P.get("TRA"):  # A fragment = two transposing 4-position x 16-channel reads of DYS
+                for half in range(2):
+                    ad = {}
+                    for l in range(64):
+                        grp = l >> 4
+                        p0 = kc * 32 + grp * 8
+                        y, x0 = p0 >> 4, p0 & 15
+                        ad[l] = OFF_DYS + T * (((y + 4) * 18 + x0 + ((l & 15) >> 2) + 4 + 4 * half) * 16 + 4 * (l & 3))
+                    add("B1.dys_tr", "r64tr", ad)
+            else:
+                ad = {}
+                for l in range(64):
+                    row, grp = l & 15, l >> 4
+                    p0 = kc * 32 + grp * 8
+                    ad[l] = OFF_DY2T + T * (row * D2P + (p0 >> 4) * D2R + (p0 & 15))
+                add("B1.dy2t", "r128", ad)
             for i in range(len(w2off)):
                 ad = {}
                 for l in range(64):
@@ -243,6 +265,9 @@ AMAP_CODES = [8, 11, 0, 10, 4, 12, 5, 13, 15, 3, 2, 14, 9, 7, 6, 1]  # r * 8 + n
 CUR = dict(PREV, XP=1048, D1P=944, C2=1, PRE=32, ONES=5 * 1048 + 120,
            AMAP=[(c >> 3, c & 7) for c in AMAP_CODES],
            BMAP=[8, 9, 12, 4, 5, 15, 10, 13, 2, 14, 6, 11, 1, 7, 3, 0])
+R3C = CUR
+# round 3 final / round 4: the conv2 wgrad A operand read from DYS with ds_read_b64_tr_b16 (no DY2T image)
+CUR = dict(R3C, TRA=1)
 
 
 def report(P, title=""):
@@ -262,6 +287,9 @@ if __name__ == "__main__":
     if "r1" in sys.argv[1:]:
         report(R1, "round-1 conv_bwd bf16")
         sys.argv.remove("r1")
+    if "r3c" in sys.argv[1:]:
+        report(R3C, "round-3 session-3 conv_bwd bf16 (channel-major DY2T copy)")
+        sys.argv.remove("r3c")
     if "prev" in sys.argv[1:]:
         report(PREV, "round-2 conv_bwd bf16")
         sys.argv.remove("prev")

@@ -9,7 +9,7 @@ rank's "all-reduced" gradient is its own): they must equal a local run at half t
 (x0.5 is exact in binary floating point).
 ``_k<k>`` variants run the steps as ONE k-step graph (run_steps), whose steps may leave the aux
 branch join to the next step's head; they must equal the same number of single-step graphs.
-Usage: python scripts/sched_equiv.py [--model mlp|lenet5] VARIANT [VARIANT ...]
+Usage: python scripts/sched_equiv.py [--model mlp|lenet5] [--dtype bf16|fp32] [--batch B] VARIANT [VARIANT ...]
   VARIANT = {local,local_halflr,join,split}[_b<blocks>][_w2][_k<k>]
 """
 import argparse
@@ -32,6 +32,7 @@ ap.add_argument("variants", nargs="+")
 ap.add_argument("--batch", type=int, default=512)
 ap.add_argument("--steps", type=int, default=4)
 ap.add_argument("--model", default="lenet5", choices=["lenet5", "mlp"])
+ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
 a = ap.parse_args()
 x, y = make_split(4096, seed=7)
 C = load_c()
@@ -44,7 +45,7 @@ for v in a.variants:
     kind, blocks, w2, k = m.group(1), int(m.group(2) or 0), bool(m.group(3)), int(m.group(4) or 0)
     lr = 0.025 if kind == "local_halflr" else 0.05
     torch.manual_seed(0)
-    tr = NativeTrainer(a.model, "bf16", a.batch, torch.from_numpy(x.reshape(-1, 784)), torch.from_numpy(y),
+    tr = NativeTrainer(a.model, a.dtype, a.batch, torch.from_numpy(x.reshape(-1, 784)), torch.from_numpy(y),
                        lr=lr, momentum=0.9, dropout=0.0, init=build_model(a.model))
     if kind in ("join", "split"):
         tr.attach_comm(C.RcclComm(C.RcclComm.make_unique_id(), 0, 1, 0), 2 if w2 else 1, plan=kind,

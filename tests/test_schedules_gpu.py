@@ -21,9 +21,9 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _digests(env_extra, variants, model="lenet5"):
+def _digests(env_extra, variants, model="lenet5", extra=()):
     env = dict(os.environ, PYTHONPATH=ROOT, **env_extra)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "sched_equiv.py"), "--model", model] + variants,
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "sched_equiv.py"), "--model", model, *extra] + variants,
                        env=env,
                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:]
@@ -41,6 +41,17 @@ def test_schedules_bitwise_equal(native):
         assert d[k] == ref, k
     assert d["join_w2"] == serial["local_halflr"] and d["split_w2"] == serial["local_halflr"]
     assert d["join_b480"] == d["local_b480"] and d["split_b480"] == d["local_b480"]
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("dtype,batch", [("fp32", 128), ("bf16", 128)])
+def test_small_batch_serial_equals_concurrent(native, dtype, batch):
+    """Small batches (one FC batch split): the serial schedule runs conv_bwd and the SGD-fused FC weight
+    gradient as ONE kernel (launch_lenet_conv_bwd_fc); the concurrent one runs them on two streams."""
+    extra = ("--dtype", dtype, "--batch", str(batch))
+    serial = _digests({"MNIST_AMD_CONCURRENT": "0"}, ["local", "local_k4"], extra=extra)
+    conc = _digests({"MNIST_AMD_CONCURRENT": "1"}, ["local"], extra=extra)
+    assert serial["local"] == conc["local"] and serial["local_k4"] == conc["local"]
 
 
 @pytest.mark.timeout(300)

@@ -2,7 +2,7 @@
 
 RCCL refuses two ranks on one device, but nothing else in the multi-GPU chain needs two GPUs:
 ``bench.py --gpus 2 --comm gloo`` self-launches two rank processes that share the GPU, rendezvous over
-the TCPStore, broadcast rank 0's parameters, run the rank-max start-up calibration and train on their
+the TCPStore, broadcast rank 0's parameters and train on their
 DistributedSampler shards with the gradient slab summed by c10d gloo through pinned host memory.
 Both replicas must end bitwise identical, and equal to the same two shards trained by two trainers in
 ONE process whose gradients are summed on the host (the DDP arithmetic, reference
@@ -68,8 +68,8 @@ def test_two_ranks_share_one_gpu(native, tmp_path, model, dtype, batch):
                        "--dump-params", str(tmp_path / "p")])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["value"] > 0
     assert "gloo" in out["config"]["comm"]
-    if model == "lenet5":   # the rank-max calibration ran across the two processes
-        assert set(out["config"]["plan_autotune"]["timings_ms"]) == {"concurrent", "serial"}
+    # the host (gloo) data plane runs the eager phase API, not the captured schedules: nothing is calibrated
+    assert out["config"]["plan_autotune"]["chosen"] == "eager-phases"
     # (the two ranks share stderr: their lines can interleave without a newline between them)
     digests = dict(re.findall(r"digest rank=(\d) ([0-9a-f]{64})", err))
     assert set(digests) == {"0", "1"} and digests["0"] == digests["1"], err[-2000:]
