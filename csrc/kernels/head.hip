@@ -1120,19 +1120,24 @@ __global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
   const T* asrc = J.dyT + (size_t)min(nb0 + sr, J.NP - 1) * a.ldB + sc * KV;
   const T* bsrc = J.xT + (size_t)min(kb0 + sr, J.K > 0 ? J.K - 1 : 0) * a.ldB + sc * KV;
   const u32x4 z4 = u32x4{0u, 0u, 0u, 0u};
-  u32x4 ra[SUB], rb[SUB];
   // Gather job (GX, bf16, block-uniform): the B tile is [SUB * KC batch rows][64 pixels] (row pitch PG), built
   // from the rows' uint8 pixels: item c = tid + 256 j (j < GJ) = tile row c / 4, 16-pixel chunk c % 4 (one
-  // 16-byte load); the row's sample index is loaded an interval earlier (gi), so each interval's pixel loads
-  // wait on no index load.  The MFMA B fragments are read with transposing ds_read_b64_tr_b16.
+  // 16-byte load); the rows' sample indices are loaded an interval before their pixels, so no pixel load waits
+  // on an index load.  The MFMA B fragments are read with transposing ds_read_b64_tr_b16.
   constexpr bool GXT = sizeof(T) == 2;
   constexpr int PG = 64 + 8, GJ = SUB * KC * 4 / 256;
   static_assert(!GXT || (GJ >= 1 && GJ <= SUB && SUB * KC * PG <= TILE), "gather tile");
   const bool gx = GXT && J.gather;
   const int32_t* gidx_base = gx ? a.gx_idx + (size_t)a.gx_step[0] * a.gx_stride : nullptr;
-  // sample indices (-1: row past the batch): gnx = the next interval to fetch, gtmp = the one after it
   constexpr int GN = GXT ? GJ : 1;
-  int gnx[GN], gtmp[GN];
+  // One interval's staging data in registers.  Two slots: interval i lives in slot i & 1, and it is fetched two
+  // intervals ahead (issued at the start of interval i - 2, staged at the end of interval i - 1), so two
+  // intervals of loads are in flight behind the MFMAs (one ahead: the K loop waited ~ one L2 round trip per
+  // interval).  Indices (gather) live in slot i & 1 too, loaded one interval before their pixel fetch.
+  struct Slot {
+    u32x4 ra[SUB], rb[SUB];
+    bool live[GN];
+  };
   auto fetch_idx = [&](int it, int (&g)[GN]) {
 #pragma unroll
     for (int j = 0; j < GN; ++j) {
@@ -1141,40 +1146,40 @@ __global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
       g[j] = rg < a.gx_B ? gidx_base[rg] : -1;
     }
   };
-  auto fetch = [&](int it, const int (&g)[GN]) {  // branch-free: steps past nsteps re-read the last step
+  auto fetch = [&](int it, Slot& d, const int (&g)[GN]) {  // branch-free: steps past nsteps re-read the last step
 #pragma unroll
     for (int q = 0; q < SUB; ++q) {
       const int rc = step_row(min(it * SUB + q, nsteps - 1));
-      ra[q] = *reinterpret_cast<const u32x4*>(asrc + rc);
-      if (!gx) rb[q] = *reinterpret_cast<const u32x4*>(bsrc + rc);
+      d.ra[q] = *reinterpret_cast<const u32x4*>(asrc + rc);
+      if (!gx) d.rb[q] = *reinterpret_cast<const u32x4*>(bsrc + rc);
     }
     if (gx) {
 #pragma unroll
       for (int j = 0; j < GN; ++j) {
         const int c = tid + 256 * j;
         const int px = min(kb0 + (c & 3) * 16, 784 - 16);  // chunks past the image: any in-row address (k >= K unused)
-        rb[j] = *reinterpret_cast<const u32x4*>(a.gx_images + (size_t)max(g[j], 0) * 784 + px);
+        d.rb[j] = *reinterpret_cast<const u32x4*>(a.gx_images + (size_t)max(g[j], 0) * 784 + px);
+        d.live[j] = g[j] >= 0;
       }
     }
   };
-  auto stage = [&](int buf, const int (&g)[GN]) {
+  auto stage = [&](int buf, const Slot& d) {
 #pragma unroll
     for (int q = 0; q < SUB; ++q) {
-      *reinterpret_cast<u32x4*>(&lds[buf][0][sr * PE + q * KC + sc * KV]) = a_ok ? ra[q] : z4;
-      if (!gx) *reinterpret_cast<u32x4*>(&lds[buf][1][sr * PE + q * KC + sc * KV]) = b_ok ? rb[q] : z4;
+      *reinterpret_cast<u32x4*>(&lds[buf][0][sr * PE + q * KC + sc * KV]) = a_ok ? d.ra[q] : z4;
+      if (!gx) *reinterpret_cast<u32x4*>(&lds[buf][1][sr * PE + q * KC + sc * KV]) = b_ok ? d.rb[q] : z4;
     }
     if constexpr (GXT) {
       if (gx) {
 #pragma unroll
         for (int j = 0; j < GJ; ++j) {
           const int c = tid + 256 * j;
-          const bool live = g[j] >= 0;
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             bf16x8 f;
 #pragma unroll
             for (int e = 0; e < 8; ++e)
-              f[e] = (bf16)(live ? mnist_norm((rb[j][2 * h + (e >> 2)] >> (8 * (e & 3))) & 255u) : 0.f);
+              f[e] = (bf16)(d.live[j] ? mnist_norm((d.rb[j][2 * h + (e >> 2)] >> (8 * (e & 3))) & 255u) : 0.f);
             *reinterpret_cast<bf16x8*>(&lds[buf][1][(c >> 2) * PG + (c & 3) * 16 + h * 8]) = f;
           }
         }
@@ -1213,20 +1218,9 @@ __global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
   const int ao0 = (n0 - nb0 + row) * PE + grp * KV, ao1 = ao0 + 16 * PE;
   const int bo0 = (k0 - kb0 + row) * PE + grp * KV, bo1 = bo0 + 16 * PE;
 
-  if (nint > 0) {
-    if (gx) {
-      fetch_idx(0, gtmp);
-      fetch_idx(1, gnx);  // (clamped to the last step when nint == 1; unused then)
-    }
-    fetch(0, gtmp);
-    stage(0, gtmp);
-  }
-  __syncthreads();
   const int gk0 = (k0 - kb0), gk1 = gk0 + 16;  // gather job: tile-local pixel columns of this wave's fragments
-  for (int it = 0; it < nint; ++it) {
+  auto compute = [&](int it) {
     const int buf = it & 1;
-    if (it + 1 < nint) fetch(it + 1, gnx);  // next interval's chunks in flight during this interval's MFMAs
-    if (gx && it + 2 < nint) fetch_idx(it + 2, gtmp);  // gather: the indices of the interval after next
     const int nq = min(SUB, nsteps - it * SUB);  // live steps of this interval (block-uniform)
 #pragma unroll
     for (int q = 0; q < SUB; ++q) {
@@ -1242,12 +1236,33 @@ __global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
         M::mma(acc[1][1], a1, b1);
       }
     }
-    if (it + 1 < nint) stage(buf ^ 1, gnx);  // that buffer was last read in interval it - 1, before the barrier
+  };
+  Slot s0, s1;
+  int i0[GN], i1[GN];
+  if (nint > 0) {
     if (gx) {
-#pragma unroll
-      for (int j = 0; j < GN; ++j) gnx[j] = gtmp[j];
+      fetch_idx(0, i0);
+      fetch_idx(1, i1);  // (clamped to the last step when nint == 1; unused then)
     }
+    fetch(0, s0, i0);
+    if (nint > 1) fetch(1, s1, i1);
+    if (gx && nint > 2) fetch_idx(2, i0);
+    stage(0, s0);
+  }
+  __syncthreads();
+  // interval it: slot `cur` (= it & 1) was staged before the barrier, so it takes interval it + 2's loads (its
+  // indices are in `icur`); `inxt` is free too (interval it + 1's pixels are in flight) and takes interval
+  // it + 3's indices; then the MFMAs of interval it; then interval it + 1 (slot `nxt`) is staged.
+  auto body = [&](int it, Slot& cur, Slot& nxt, int (&icur)[GN], int (&inxt)[GN]) {
+    if (it + 2 < nint) fetch(it + 2, cur, icur);
+    if (gx && it + 3 < nint) fetch_idx(it + 3, inxt);
+    compute(it);
+    if (it + 1 < nint) stage((it + 1) & 1, nxt);  // that buffer was last read in interval it - 1, before the barrier
     __syncthreads();
+  };
+  for (int it = 0; it < nint; it += 2) {  // unrolled by two: the slots alternate statically (no register copies)
+    body(it, s0, s1, i0, i1);
+    if (it + 1 < nint) body(it + 1, s1, s0, i1, i0);
   }
   if (!wave_live) return;
 
