@@ -18,6 +18,9 @@ B128_GROUPS = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
 B128_GROUPS += [[l + 32 for l in g] for g in B128_GROUPS]
 
 
+BYTES = {"r128": 16, "w128": 16, "r64tr": 8, "r32": 4, "w32": 4, "w16": 2, "w8": 1}
+
+
 def cycles(kind, addrs):
     """addrs: {lane: byte address} of ONE wave-instruction (inactive lanes absent)."""
     if not addrs:
@@ -59,7 +62,7 @@ def model(P):
     OFF_M1 = rup(OFF_DY1T + 8 * D1P * T, 16)
     total_lds = rup(OFF_M1 + (6 * P["M1CP"] if P.get("NEWA") else 6 * 14 * 16), 16)
     dys_idx = P["dys_idx"]
-    acc = collections.defaultdict(lambda: [0, 0, 0])  # name -> [instrs, cycles, ideal]
+    acc = collections.defaultdict(lambda: [0, 0, 0, 0])  # name -> [instrs, cycles, ideal, bytes]
 
     def add(name, kind, addrs):
         c, i = cycles(kind, addrs)
@@ -68,6 +71,7 @@ def model(P):
             a[0] += 1
             a[1] += c
             a[2] += i
+            a[3] += len(addrs) * BYTES[kind]
 
     for w in range(4):
         lanes = [(w * 64 + l, l) for l in range(64)]
@@ -272,14 +276,15 @@ CUR = dict(R3C, TRA=1)
 
 def report(P, title=""):
     acc, lds = model(P)
-    tc = ti = 0
+    tc = ti = tb = 0
     print(f"== {title} (LDS {lds} B/workgroup)")
     for k in sorted(acc):
-        n, c, i = acc[k]
+        n, c, i, b = acc[k]
         tc += c
         ti += i
-        print(f"  {k:10s} instrs {n:4d}  cycles {c:5d}  ideal {i:5d}  x{c / max(i, 1):.2f}")
-    print(f"  total cycles/image {tc}  ideal {ti}  conflict share {100 * (tc - ti) / tc:.1f}%")
+        tb += b
+        print(f"  {k:10s} instrs {n:4d}  cycles {c:5d}  ideal {i:5d}  x{c / max(i, 1):.2f}  bytes {b:6d}")
+    print(f"  total cycles/image {tc}  ideal {ti}  conflict share {100 * (tc - ti) / tc:.1f}%  bytes/image {tb}")
     return tc
 
 

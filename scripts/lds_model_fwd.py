@@ -10,7 +10,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from lds_model import cycles  # noqa: E402
+from lds_model import BYTES, cycles  # noqa: E402
 
 
 C1Q = (0, 1, 2, 3)  # conv1 M-row block -> pooled column (lenet.hip conv_fwd_kernel: identity)
@@ -28,7 +28,7 @@ def model(P):
     OFF_M1 = rup(OFF_P1C + 6 * P1CP * T, 16)
     OFF_P2 = rup(OFF_M1 + 6 * M1CP, 16)
     OFF_M2 = rup(OFF_P2 + 400 * T, 16)
-    acc = collections.defaultdict(lambda: [0, 0, 0])
+    acc = collections.defaultdict(lambda: [0, 0, 0, 0])
 
     def add(name, kind, addrs):
         c, ideal = cycles(kind, addrs)
@@ -36,6 +36,7 @@ def model(P):
         a[0] += 1
         a[1] += c
         a[2] += ideal
+        a[3] += len(addrs) * BYTES[kind]
 
     # stage: 4 waves, tid < 224, 4 x ds_write_b128
     for w in range(4):
@@ -111,13 +112,14 @@ def model(P):
 
 def report(P):
     acc = model(P)
-    tot_c = tot_i = 0
-    print(f"{'access':24s} {'instr':>6s} {'cycles':>7s} {'ideal':>6s} {'conflict':>8s}")
-    for name, (n, c, i) in acc.items():
+    tot_c = tot_i = tot_b = 0
+    print(f"{'access':24s} {'instr':>6s} {'cycles':>7s} {'ideal':>6s} {'conflict':>8s} {'bytes':>7s}")
+    for name, (n, c, i, b) in acc.items():
         tot_c += c
         tot_i += i
-        print(f"{name:24s} {n:6d} {c:7d} {i:6d} {100 * (c - i) / max(c, 1):7.1f}%")
-    print(f"{'total':24s} {'':6s} {tot_c:7d} {tot_i:6d} {100 * (tot_c - tot_i) / max(tot_c, 1):7.1f}%")
+        tot_b += b
+        print(f"{name:24s} {n:6d} {c:7d} {i:6d} {100 * (c - i) / max(c, 1):7.1f}% {b:7d}")
+    print(f"{'total':24s} {'':6s} {tot_c:7d} {tot_i:6d} {100 * (tot_c - tot_i) / max(tot_c, 1):7.1f}% {tot_b:7d}")
 
 
 def search():
@@ -128,7 +130,7 @@ def search():
             for P1CP in (232, 240, 248, 256):
                 for M1CP in (240, 256, 272, 288):
                     acc = model({"XP": XP, "P1CP": P1CP, "M1CP": M1CP, "RP": RP})
-                    res.append((sum(c for _, c, _ in acc.values()), XP, RP, P1CP, M1CP))
+                    res.append((sum(v[1] for v in acc.values()), XP, RP, P1CP, M1CP))
     res.sort()
     for r in res[:8]:
         print("cycles %d  XP=%d RP=%d P1CP=%d M1CP=%d" % r)

@@ -57,13 +57,16 @@ def test_conv_bwd_phase_c_layout():
     """conv1 wgrad as one packed tile (lenet.hip C_AMAP / C_BMAP, XP 1048, D1P 944): conflict-free
     DY1T reads, at most 1.5-way XS reads, and fewer LDS cycles per image than the two-tile layout."""
     acc, _ = lds_model.model(lds_model.CUR)
-    n, c, i = acc["C.dy1t"]
+    n, c, i, _ = acc["C.dy1t"]
     assert (n, c) == (29, i)
-    n, c, i = acc["C.xs"]
+    n, c, i, _ = acc["C.xs"]
     assert n == 29 and c <= 1.5 * i
     prev, _ = lds_model.model(lds_model.PREV)
     tot = lambda a: sum(v[1] for v in a.values())  # noqa: E731
     assert tot(acc) < tot(prev) - 150
+    # round 3 final: the conv2 wgrad A operand read from DYS with transposing reads (no DY2T copy) is cheaper
+    r3c, _ = lds_model.model(lds_model.R3C)
+    assert "B1.dys_tr" in acc and "B1.dy2t" not in acc and tot(acc) < tot(r3c)
     # the (r, n) map covers every (row shift, channel) once; the column map every (khb, kw) + the bias
     assert sorted(lds_model.CUR["AMAP"]) == [(r, n) for r in range(2) for n in range(8)]
     assert sorted(lds_model.CUR["BMAP"]) == list(range(16))
