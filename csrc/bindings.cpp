@@ -46,7 +46,12 @@ PYBIND11_MODULE(_C, m) {
   m.attr("L1_KSPLIT") = L1_KSPLIT;
   m.def("metric_rows", [](int B) { return metric_rows(B); });
   m.attr("L1_SPLIT_MAX_B") = L1_SPLIT_MAX_B;
-  m.attr("STAMP_ROWS") = STAMP_ROWS;  // rows of the MNIST_AMD_STAMPS buffer (launch.h)
+  m.attr("STAMP_ROWS") = STAMP_ROWS;
+#ifdef MNIST_AMD_RAW_ROWS
+  m.attr("RAW_ROWS") = true;
+#else
+  m.attr("RAW_ROWS") = false;
+#endif  // rows of the MNIST_AMD_STAMPS buffer (launch.h)
   m.def("device_count", [] {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -75,7 +80,7 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init<>())
 #define RW(f) .def_readwrite(#f, &TrainerPtrs::f)
       RW(images) RW(labels) RW(idx) RW(step) RW(params) RW(grad) RW(mom) RW(pack) RW(slab_fc) RW(slab_conv)
-      RW(metrics) RW(xT) RW(h1T) RW(h2T) RW(dy1T) RW(dy2T) RW(dy3T) RW(p1) RW(m1) RW(p2) RW(m2) RW(dp2) RW(z1p) RW(stamps) RW(xnext) RW(ynext);
+      RW(metrics) RW(xT) RW(h1T) RW(h2T) RW(dy1T) RW(dy2T) RW(dy3T) RW(p1) RW(m1) RW(p2) RW(m2) RW(dp2) RW(z1p) RW(stamps) RW(xnext) RW(ynext) RW(xrows);
 #undef RW
 
   py::class_<Bucket>(m, "Bucket")

@@ -343,6 +343,12 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       // around the loads' consumers
       const int eu = tid + i * NTH, e = min(eu, NGI - 1), r = (e % (R / 4)) * 4, c = e / (R / 4);
       const bool item = eu < NGI;
+      if (TRAIN && hb.xrows != nullptr && item && c < H::K0 / 16) {
+        // raw-row hand-off to the layer-1 weight gradient: the 16 pixels of each of the 4 rows, as loaded
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (r0 + r + q < B) *reinterpret_cast<u32x4*>(hb.xrows + (size_t)(r0 + r + q) * 784 + c * 16) = px[i][q];
+      }
       if constexpr (sizeof(T) == 2) {
         // each row's 16 pixels -> 16 bf16 packed in 8 registers (two 16-byte LDS stores); the xT store of
         // pixel j takes halfword j of the four rows (as the pool2-row path below)
@@ -362,7 +368,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
             if (item) *reinterpret_cast<u32x4*>(sX + (r + q) * S::PX + c * 16 + h * 8) = pk[q][h];
           }
         }
-        if (TRAIN && item && !ABLATED(hb.ablate, 1) && hb.gx_images == nullptr) {
+        if (TRAIN && item && !ABLATED(hb.ablate, 1) && hb.xrows == nullptr) {
 #pragma unroll
           for (int j = 0; j < 16; ++j) {
             const int h = j >> 3, wd = (j & 7) >> 1, sh = 16 * (j & 1);
@@ -1057,143 +1063,110 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
   if (a.stamps && threadIdx.x == 0 && lin < 512) a.stamps[(STAMP_WGRAD + lin) * 16 + 1] = wall_clock64();
 }
 
+// Batch rows of a wgrad workgroup's K-steps (wgrad_kernel's split / XCD-aware mapping, see WgArgs).
+struct WgRows {
+  int xcd_ch, rs, m0, spc, x, contig, nch;
+  DEV int operator()(int st, int KC) const {  // first batch row of step st (monotonic in st)
+    if (xcd_ch == 0) return rs + st * KC;
+    const int m = m0 + st / spc;
+    return (contig ? x * (nch / 8) + m : x + 8 * m) * xcd_ch + (st % spc) * KC;
+  }
+};
+
 // LDS-staged variant of wgrad_kernel (same tiles, splits, step order and slab layout; every output element
 // is the same MFMA chain, so the results are bitwise those of wgrad_kernel): the workgroup stages the 64-row
-// dY^T tile and the 64-row X^T tile of SUB consecutive 32-row K-steps ONCE per barrier interval (SUB 16-byte
-// chunks of each per thread, loaded an interval ahead into registers), and each wave reads its 32x32 operands
-// from LDS.  In wgrad_kernel every fragment is fetched by two waves straight from L2 -- twice the L2 -> CU
-// traffic, which bounds that kernel (~37 GB/s per CU measured on the MLP at B=8192).  SUB = 4 (128 batch rows
-// per barrier, 16 MFMAs per wave between barriers): with SUB = 1 every 4-MFMA step paid a barrier and an
-// L2 round trip of exposed latency.  Rows padded by 32 B (conflict-free fragment reads for ds_read_b128's
-// lane groups).  Needs 16 KB x SUB + padding of LDS, so it is for the schedules where nothing LDS-heavy
-// runs beside it (the MLP; LeNet's FC wgrad shares the CUs with conv_bwd and keeps the LDS-free kernel).
-template <typename T, int SUB>
-__global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
+// dY^T tile and the 64-row X^T tile of SUB (2) consecutive 32-row K-steps per interval, and each wave reads its
+// 32x32 operands from LDS (in wgrad_kernel every fragment is fetched by two waves straight from L2).
+//  * loads: interval i's 16-byte chunks are issued two intervals ahead into one of two register slots (slot
+//    i & 1, statically alternated by a two-way unrolled loop), so two intervals of loads are in flight behind
+//    the MFMAs; ONE LDS buffer (20 KB at SUB 2), written between two barriers (a double-buffered SUB-4
+//    version -- 72 KB, two workgroups per CU -- ran the MLP's 560-workgroup grid in two rounds);
+//  * GX (gather job, bf16; builds with MNIST_AMD_RAW_ROWS only): the layer-1 input comes from the raw uint8
+//    batch rows the head wrote (HeadBuffers::xrows, half the bytes of a bf16 X^T): the B tile is [SUB * 32
+//    batch rows][64 pixels] (row pitch PG), filled from 16-pixel chunks normalised in registers, read with
+//    transposing ds_read_b64_tr_b16.  Measured slower than the bf16 X^T it replaces (35.5 vs 33.2 us per MLP
+//    step at SUB 2, same box): the head's row stores cost what its X^T stores cost (~1.1 us of the staging
+//    phase) and the in-register normalise + 8-byte transposing reads cost more than 16-byte X^T fragment
+//    reads; re-gathering through the epoch's sample indices instead put an index round trip in front of every
+//    interval's pixel loads.  Every load sits in straight-line code or behind a block-uniform branch.
+// Rows padded by 32 B (conflict-free ds_read_b128 fragment reads).  LDS use keeps it to the schedules where
+// nothing LDS-heavy runs beside it (the MLP; LeNet's FC wgrad runs beside conv_bwd on the LDS-free kernel).
+template <typename T, int SUB, bool GX>
+DEV void wgrad_lds_body(const WgArgs<T>& a, const int j, const WgRows rows, const int nsteps, const int tile,
+                        const int split, T* sa, T* sb) {
+  const WgJob<T>& J = a.job[j];
   using M = Mma<T>;
   using Frag = typename M::Frag;
   constexpr int KV = M::KV, KC = M::KC;
-  constexpr int ROWB = SUB * 64 + 32;                 // bytes per tile row: SUB steps x 64 B of data + 32 B pad
-  constexpr int PE = ROWB / (int)sizeof(T);           // row pitch (elements)
-  constexpr int TILE = 64 * PE;                       // one [64 rows][SUB * KC] tile
-  __shared__ __attribute__((aligned(16))) T lds[2][2][TILE];  // [buffer][A = dY^T, B = X^T]
+  constexpr int PE = (SUB * 64 + 32) / (int)sizeof(T);  // row pitch (elements): SUB steps x 64 B + 32 B pad
+  constexpr int PG = 64 + 8, GJ = SUB * KC * 4 / 256, GN = GX ? GJ : 1;
+  static_assert(!GX || (sizeof(T) == 2 && GJ >= 1 && SUB * KC * PG <= 64 * PE), "gather tile");
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
-  const int lin = blockIdx.y * gridDim.x + blockIdx.x;
-  if (a.stamps && threadIdx.x == 0 && lin < 512) a.stamps[(STAMP_WGRAD + lin) * 16] = wall_clock64();
-  int tile, split, nsteps, x = 0, m0 = 0, spc = 1, rs = 0;
-  if (a.xcd_ch == 0) {
-    tile = blockIdx.x;
-    split = blockIdx.y;
-    rs = split * a.rlen;
-    nsteps = (min(rs + a.rlen, a.Bp) - rs + KC - 1) / KC;
-  } else {
-    const int L = blockIdx.x, q = L >> 3;
-    x = L & 7;
-    tile = q / a.sx;
-    const int sub = q % a.sx;
-    split = x * a.sx + sub;
-    const int mx = a.contig ? a.nch / 8 : (x < a.nch ? (a.nch - x + 7) / 8 : 0);
-    m0 = sub * mx / a.sx;
-    const int m1 = (sub + 1) * mx / a.sx;
-    spc = a.xcd_ch / KC;
-    nsteps = (m1 - m0) * spc;
-  }
-  auto step_row = [&](int st) -> int {  // first batch row of step st (monotonic in st)
-    if (a.xcd_ch == 0) return rs + st * KC;
-    const int m = m0 + st / spc;
-    return (a.contig ? x * (a.nch / 8) + m : x + 8 * m) * a.xcd_ch + (st % spc) * KC;
-  };
-  while (nsteps > 0 && step_row(nsteps - 1) >= a.Bp) --nsteps;  // steps past the (padded) batch
-  const int nint = (nsteps + SUB - 1) / SUB;                      // barrier intervals
-  int j = 0;
-  while (j + 1 < a.njobs && tile >= a.job[j + 1].blk_begin) ++j;
-  const WgJob<T>& J = a.job[j];
+  const int nint = (nsteps + SUB - 1) / SUB;  // barrier intervals (block-uniform)
   const int lb = tile - J.blk_begin;
   const int bn = lb / J.nblk_k, bk = lb % J.nblk_k;
-  const int nb0 = bn * 64, kb0 = bk * 64;              // block origin (block-uniform)
+  const int nb0 = bn * 64, kb0 = bk * 64;
   const int n0 = nb0 + (w >> 1) * 32, k0 = kb0 + (w & 1) * 32;
   const int Kb = J.K + (J.bias ? 1 : 0);
-  const bool wave_live = n0 < J.N && k0 < Kb;         // waves without outputs still stage and sync
+  const bool wave_live = n0 < J.N && k0 < Kb;  // waves without outputs still stage and sync
 
-  // staging role: tile row r = tid / 4, 16-byte chunk c = tid % 4 of each step's KC elements
+  // staging role: tile row sr = tid / 4, 16-byte chunk sc = tid % 4 of each step's KC elements
   const int sr = tid >> 2, sc = tid & 3;
   const bool a_ok = nb0 + sr < J.NP, b_ok = kb0 + sr < J.K;
   const T* asrc = J.dyT + (size_t)min(nb0 + sr, J.NP - 1) * a.ldB + sc * KV;
   const T* bsrc = J.xT + (size_t)min(kb0 + sr, J.K > 0 ? J.K - 1 : 0) * a.ldB + sc * KV;
   const u32x4 z4 = u32x4{0u, 0u, 0u, 0u};
-  // Gather job (GX, bf16, block-uniform): the B tile is [SUB * KC batch rows][64 pixels] (row pitch PG), built
-  // from the rows' uint8 pixels: item c = tid + 256 j (j < GJ) = tile row c / 4, 16-pixel chunk c % 4 (one
-  // 16-byte load); the rows' sample indices are loaded an interval before their pixels, so no pixel load waits
-  // on an index load.  The MFMA B fragments are read with transposing ds_read_b64_tr_b16.
-  constexpr bool GXT = sizeof(T) == 2;
-  constexpr int PG = 64 + 8, GJ = SUB * KC * 4 / 256;
-  static_assert(!GXT || (GJ >= 1 && GJ <= SUB && SUB * KC * PG <= TILE), "gather tile");
-  const bool gx = GXT && J.gather;
-  const int32_t* gidx_base = gx ? a.gx_idx + (size_t)a.gx_step[0] * a.gx_stride : nullptr;
-  constexpr int GN = GXT ? GJ : 1;
-  // One interval's staging data in registers.  Two slots: interval i lives in slot i & 1, and it is fetched two
-  // intervals ahead (issued at the start of interval i - 2, staged at the end of interval i - 1), so two
-  // intervals of loads are in flight behind the MFMAs (one ahead: the K loop waited ~ one L2 round trip per
-  // interval).  Indices (gather) live in slot i & 1 too, loaded one interval before their pixel fetch.
   struct Slot {
-    u32x4 ra[SUB], rb[SUB];
+    u32x4 ra[SUB], rb[GX ? GJ : SUB];
     bool live[GN];
   };
-  auto fetch_idx = [&](int it, int (&g)[GN]) {
-#pragma unroll
-    for (int j = 0; j < GN; ++j) {
-      const int c = tid + 256 * j, q = c / (4 * KC), rr = (c >> 2) % KC;
-      const int rg = step_row(min(it * SUB + q, nsteps - 1)) + rr;
-      g[j] = rg < a.gx_B ? gidx_base[rg] : -1;
-    }
-  };
-  auto fetch = [&](int it, Slot& d, const int (&g)[GN]) {  // branch-free: steps past nsteps re-read the last step
+  auto fetch = [&](int it, Slot& d) {  // straight-line loads of interval it (steps past nsteps re-read the last)
 #pragma unroll
     for (int q = 0; q < SUB; ++q) {
-      const int rc = step_row(min(it * SUB + q, nsteps - 1));
+      const int rc = rows(min(it * SUB + q, nsteps - 1), KC);
       d.ra[q] = *reinterpret_cast<const u32x4*>(asrc + rc);
-      if (!gx) d.rb[q] = *reinterpret_cast<const u32x4*>(bsrc + rc);
+      if constexpr (!GX) d.rb[q] = *reinterpret_cast<const u32x4*>(bsrc + rc);
     }
-    if (gx) {
+    if constexpr (GX) {
 #pragma unroll
-      for (int j = 0; j < GN; ++j) {
-        const int c = tid + 256 * j;
+      for (int j = 0; j < GJ; ++j) {
+        const int c = tid + 256 * j, q = c / (4 * KC), rr = (c >> 2) % KC;
+        const int rg = rows(min(it * SUB + q, nsteps - 1), KC) + rr;
         const int px = min(kb0 + (c & 3) * 16, 784 - 16);  // chunks past the image: any in-row address (k >= K unused)
-        d.rb[j] = *reinterpret_cast<const u32x4*>(a.gx_images + (size_t)max(g[j], 0) * 784 + px);
-        d.live[j] = g[j] >= 0;
+        d.rb[j] = *reinterpret_cast<const u32x4*>(a.gx_rows + (size_t)min(rg, a.gx_B - 1) * 784 + px);
+        d.live[j] = rg < a.gx_B;
       }
     }
   };
-  auto stage = [&](int buf, const Slot& d) {
+  auto stage = [&](const Slot& d) {
 #pragma unroll
     for (int q = 0; q < SUB; ++q) {
-      *reinterpret_cast<u32x4*>(&lds[buf][0][sr * PE + q * KC + sc * KV]) = a_ok ? d.ra[q] : z4;
-      if (!gx) *reinterpret_cast<u32x4*>(&lds[buf][1][sr * PE + q * KC + sc * KV]) = b_ok ? d.rb[q] : z4;
+      *reinterpret_cast<u32x4*>(&sa[sr * PE + q * KC + sc * KV]) = a_ok ? d.ra[q] : z4;
+      if constexpr (!GX) *reinterpret_cast<u32x4*>(&sb[sr * PE + q * KC + sc * KV]) = b_ok ? d.rb[q] : z4;
     }
-    if constexpr (GXT) {
-      if (gx) {
+    if constexpr (GX) {
 #pragma unroll
-        for (int j = 0; j < GJ; ++j) {
-          const int c = tid + 256 * j;
+      for (int j = 0; j < GJ; ++j) {
+        const int c = tid + 256 * j;
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            bf16x8 f;
+        for (int h = 0; h < 2; ++h) {
+          bf16x8 f;
 #pragma unroll
-            for (int e = 0; e < 8; ++e)
-              f[e] = (bf16)(d.live[j] ? mnist_norm((d.rb[j][2 * h + (e >> 2)] >> (8 * (e & 3))) & 255u) : 0.f);
-            *reinterpret_cast<bf16x8*>(&lds[buf][1][(c >> 2) * PG + (c & 3) * 16 + h * 8]) = f;
-          }
+          for (int e = 0; e < 8; ++e)
+            f[e] = (bf16)(d.live[j] ? mnist_norm((d.rb[j][2 * h + (e >> 2)] >> (8 * (e & 3))) & 255u) : 0.f);
+          *reinterpret_cast<bf16x8*>(&sb[(c >> 2) * PG + (c & 3) * 16 + h * 8]) = f;
         }
       }
     }
   };
-  // B fragment of gather job: pixel column kl (tile-local) of batch rows q * KC + grp * KV .. + 7 (the lane's k
-  // run of the MFMA), as two 4-row x 16-column blocks transposed by the read (lane 4 i + p of a 16-lane group
-  // addresses row i, columns 4 p .. 4 p + 3; lane l receives column l)
-  auto load_gx = [&](int buf, int q, int kl) -> Frag {
+  // gather B fragment: pixel column kl (tile-local) of batch rows q * KC + grp * KV .. + 7 (the lane's k run of
+  // the MFMA), two 4-row x 16-column blocks transposed by the read (lane 4 i + p of a 16-lane group addresses
+  // row i, columns 4 p .. 4 p + 3; lane l receives column l)
+  auto load_gx = [&](int q, int kl) -> Frag {
     Frag f;
-    if constexpr (GXT) {
+    if constexpr (GX) {
       typedef short v4s __attribute__((ext_vector_type(4)));
-      const T* p = &lds[buf][1][(q * KC + grp * KV + ((lane & 15) >> 2)) * PG + kl + 4 * (lane & 3)];
+      const T* p = &sb[(q * KC + grp * KV + ((lane & 15) >> 2)) * PG + kl + 4 * (lane & 3)];
       const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(const_cast<T*>(p)));
       const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(const_cast<T*>(p + 4 * PG)));
       f.v = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
@@ -1217,19 +1190,28 @@ __global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
   const int sel1 = kk1 < J.K ? 0 : (kk1 == J.K && J.bias ? 1 : 2);
   const int ao0 = (n0 - nb0 + row) * PE + grp * KV, ao1 = ao0 + 16 * PE;
   const int bo0 = (k0 - kb0 + row) * PE + grp * KV, bo1 = bo0 + 16 * PE;
-
-  const int gk0 = (k0 - kb0), gk1 = gk0 + 16;  // gather job: tile-local pixel columns of this wave's fragments
+  const int gk0 = k0 - kb0, gk1 = gk0 + 16;  // gather: tile-local pixel columns of this wave's fragments
+  // B columns past K: the bias column reads ones, the padding zeros -- loop-invariant per lane, applied as a
+  // vector select (a select between whole fragments was lowered to an indexed scratch array)
+  const bool use0 = sel0 == 0, use1 = sel1 == 0;
+  const Frag alt0 = sel0 == 1 ? ones : zf, alt1 = sel1 == 1 ? ones : zf;
   auto compute = [&](int it) {
-    const int buf = it & 1;
     const int nq = min(SUB, nsteps - it * SUB);  // live steps of this interval (block-uniform)
 #pragma unroll
     for (int q = 0; q < SUB; ++q) {
       if (q < nq) {
-        const Frag a0 = M::load(&lds[buf][0][ao0 + q * KC]), a1 = M::load(&lds[buf][0][ao1 + q * KC]);
-        const Frag f0 = gx ? load_gx(buf, q, gk0) : M::load(&lds[buf][1][bo0 + q * KC]);
-        const Frag f1 = gx ? load_gx(buf, q, gk1) : M::load(&lds[buf][1][bo1 + q * KC]);
-        const Frag b0 = sel0 == 0 ? f0 : (sel0 == 1 ? ones : zf);
-        const Frag b1 = sel1 == 0 ? f1 : (sel1 == 1 ? ones : zf);
+        const Frag a0 = M::load(&sa[ao0 + q * KC]), a1 = M::load(&sa[ao1 + q * KC]);
+        Frag f0, f1;
+        if constexpr (GX) {
+          f0 = load_gx(q, gk0);
+          f1 = load_gx(q, gk1);
+        } else {
+          f0 = M::load(&sb[bo0 + q * KC]);
+          f1 = M::load(&sb[bo1 + q * KC]);
+        }
+        Frag b0, b1;
+        b0.v = use0 ? f0.v : alt0.v;
+        b1.v = use1 ? f1.v : alt1.v;
         M::mma(acc[0][0], a0, b0);
         M::mma(acc[0][1], a0, b1);
         M::mma(acc[1][0], a1, b0);
@@ -1237,32 +1219,28 @@ __global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
       }
     }
   };
+
   Slot s0, s1;
-  int i0[GN], i1[GN];
   if (nint > 0) {
-    if (gx) {
-      fetch_idx(0, i0);
-      fetch_idx(1, i1);  // (clamped to the last step when nint == 1; unused then)
-    }
-    fetch(0, s0, i0);
-    if (nint > 1) fetch(1, s1, i1);
-    if (gx && nint > 2) fetch_idx(2, i0);
-    stage(0, s0);
+    fetch(0, s0);
+    if (nint > 1) fetch(1, s1);
+    stage(s0);
   }
   __syncthreads();
-  // interval it: slot `cur` (= it & 1) was staged before the barrier, so it takes interval it + 2's loads (its
-  // indices are in `icur`); `inxt` is free too (interval it + 1's pixels are in flight) and takes interval
-  // it + 3's indices; then the MFMAs of interval it; then interval it + 1 (slot `nxt`) is staged.
-  auto body = [&](int it, Slot& cur, Slot& nxt, int (&icur)[GN], int (&inxt)[GN]) {
-    if (it + 2 < nint) fetch(it + 2, cur, icur);
-    if (gx && it + 3 < nint) fetch_idx(it + 3, inxt);
+  // interval it: slot `cur` (interval it, staged before the barrier) takes interval it + 2's loads; then interval
+  // it's MFMAs; then, between two barriers, interval it + 1 (slot `nxt`) is staged
+  auto body = [&](int it, Slot& cur, Slot& nxt) {
+    if (it + 2 < nint) fetch(it + 2, cur);
     compute(it);
-    if (it + 1 < nint) stage((it + 1) & 1, nxt);  // that buffer was last read in interval it - 1, before the barrier
-    __syncthreads();
+    if (it + 1 < nint) {
+      __syncthreads();  // every wave has read interval it from the buffer
+      stage(nxt);
+      __syncthreads();
+    }
   };
   for (int it = 0; it < nint; it += 2) {  // unrolled by two: the slots alternate statically (no register copies)
-    body(it, s0, s1, i0, i1);
-    if (it + 1 < nint) body(it + 1, s1, s0, i1, i0);
+    body(it, s0, s1);
+    if (it + 1 < nint) body(it + 1, s1, s0);
   }
   if (!wave_live) return;
 
@@ -1279,6 +1257,47 @@ __global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
         if (q >= 0) out[q] = acc[mi][ni][i];
       }
     }
+}
+
+template <typename T, int SUB>
+__global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
+  constexpr int KC = Mma<T>::KC;
+  constexpr int TILE = 64 * ((SUB * 64 + 32) / (int)sizeof(T));
+  __shared__ __attribute__((aligned(16))) T lds[2][TILE];  // [A = dY^T, B = X^T / gathered rows]
+  const int lin = blockIdx.y * gridDim.x + blockIdx.x;
+  if (a.stamps && threadIdx.x == 0 && lin < 512) a.stamps[(STAMP_WGRAD + lin) * 16] = wall_clock64();
+  int tile, split, nsteps;
+  WgRows rows{a.xcd_ch, 0, 0, 1, 0, a.contig, a.nch};
+  if (a.xcd_ch == 0) {
+    tile = blockIdx.x;
+    split = blockIdx.y;
+    rows.rs = split * a.rlen;
+    nsteps = (min(rows.rs + a.rlen, a.Bp) - rows.rs + KC - 1) / KC;
+  } else {
+    const int L = blockIdx.x, q = L >> 3;
+    rows.x = L & 7;
+    tile = q / a.sx;
+    const int sub = q % a.sx;
+    split = rows.x * a.sx + sub;
+    const int mx = a.contig ? a.nch / 8 : (rows.x < a.nch ? (a.nch - rows.x + 7) / 8 : 0);
+    rows.m0 = sub * mx / a.sx;
+    const int m1 = (sub + 1) * mx / a.sx;
+    rows.spc = a.xcd_ch / KC;
+    nsteps = (m1 - rows.m0) * rows.spc;
+  }
+  while (nsteps > 0 && rows(nsteps - 1, KC) >= a.Bp) --nsteps;  // steps past the (padded) batch
+  nsteps = __builtin_amdgcn_readfirstlane(nsteps);
+  int j = 0;
+  while (j + 1 < a.njobs && tile >= a.job[j + 1].blk_begin) ++j;
+  if constexpr (sizeof(T) == 2 && SUB >= 2) {
+    if (a.job[j].gather) {
+      wgrad_lds_body<T, SUB, true>(a, j, rows, nsteps, tile, split, lds[0], lds[1]);
+    } else {
+      wgrad_lds_body<T, SUB, false>(a, j, rows, nsteps, tile, split, lds[0], lds[1]);
+    }
+  } else {
+    wgrad_lds_body<T, SUB, false>(a, j, rows, nsteps, tile, split, lds[0], lds[1]);
+  }
   if (a.stamps && threadIdx.x == 0 && lin < 512) a.stamps[(STAMP_WGRAD + lin) * 16 + 1] = wall_clock64();
 }
 
@@ -1292,7 +1311,13 @@ __global__ __launch_bounds__(256) void wgrad_sgd_kernel(WgArgs<T> a) {
 // LDS-staged weight gradient (wgrad_lds_kernel) is used for the MLP, whose wgrad runs alone on the chip; the
 // LeNet wgrad runs beside conv_bwd, which holds the LDS.
 constexpr int WGRAD_DEPTH = 1;
-constexpr int WGRAD_SUB = 4;  // wgrad_lds_kernel: 32-row K-steps staged per barrier interval
+// 32-row K-steps per LDS interval, measured on the MLP at B = 8192 (1000 steps, same box, bitwise-equal
+// parameters; profiles/r4_session2/ab_mlp8k_wgrad_sub.txt): SUB 1 / 2 / 3 / 4 = 34.9 / 33.2 / 34.1 / 34.9 us
+// per step (the round-3 kernel -- one step per barrier, 6 workgroups per CU -- 34.1-34.6)
+#ifndef MNIST_AMD_WGRAD_SUB
+#define MNIST_AMD_WGRAD_SUB 2
+#endif
+constexpr int WGRAD_SUB = MNIST_AMD_WGRAD_SUB;  // wgrad_lds_kernel: 32-row K-steps staged per barrier interval
 
 template <typename T, class H, class Model>
 int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab_ld, int xcd_ch, hipStream_t s,
@@ -1366,6 +1391,8 @@ int head_launch_t(bool train, const BatchRef& br, const HeadBuffers& hb, int row
   // runs inside the head (B=128: 38.2 vs 39.9 us per step with the split)
   constexpr bool split_l1 = H::K0 >= 512;
   if (hb.z1p && br.B <= L1_SPLIT_MAX_B && split_l1) {
+    // (l1_split_kernel, not the head, reads the pixels there: it writes X^T, never the raw rows)
+    if (train && hb.xrows) throw std::logic_error("head: the raw-row hand-off needs the head's own gather");
     head_launch_split<T, H>(train, br, hb, s);
     return 16;
   }

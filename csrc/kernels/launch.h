@@ -51,14 +51,11 @@ struct HeadBuffers {
   float drop_p;
   int32_t xcd = 0;       // the head kernel used the XCD-contiguous row mapping (BatchRef::xcd)
   int32_t ablate = 0;    // diagnostics only (MNIST_AMD_HEAD_ABLATE): bit 0 = skip the X^T stores (wrong wgrad)
-  // X^T re-gather (MLP bf16, LDS-staged weight gradient): when gx_images is set, the head does NOT write X^T
-  // and the layer-1 weight gradient gathers the batch rows' uint8 pixels itself (idx_epoch[step * stride + r],
-  // normalised in registers, transposed by its LDS reads) -- bitwise the operand the head would have stored
-  const uint8_t* gx_images = nullptr;
-  const int32_t* gx_idx = nullptr;
-  const int32_t* gx_step = nullptr;
-  int32_t gx_stride = 0;
-  int32_t gx_B = 0;      // rows of the batch (rows past it are zero)
+  // Raw-row hand-off (MLP bf16, LDS-staged weight gradient): when xrows is set, the head writes its gathered
+  // uint8 pixels in batch-row order ([B][784], 6.4 MB at B = 8192) instead of the bf16 X^T (12.8 MB), and the
+  // layer-1 weight gradient normalises them in registers -- bitwise the operand X^T would have held
+  uint8_t* xrows = nullptr;
+  int32_t gx_B = 0;      // rows of the batch (rows past it read as zero)
 };
 
 struct LenetConvBuffers {

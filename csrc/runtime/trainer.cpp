@@ -203,12 +203,10 @@ HeadBuffers Trainer::head_buffers(float* metrics) const {
 }
 
 void Trainer::set_regather(HeadBuffers& hb, const BatchRef& br, bool fused_wgrad) const {
-#ifndef MNIST_AMD_NO_REGATHER  // (A/B builds only: X^T written by the head and read back by the wgrad)
-  if (model_ != ModelKind::MLP || dtype_ != DType::BF16 || fused_wgrad) return;
-  hb.gx_images = br.images;
-  hb.gx_idx = br.idx_epoch;
-  hb.gx_step = br.step_ptr;
-  hb.gx_stride = br.batch_stride;
+#ifdef MNIST_AMD_RAW_ROWS  // opt-in build: measured slower than the bf16 X^T (head.hip wgrad_lds_body, GX)
+  // (not with the small-batch layer-1 split path: there l1_split_kernel, not the head, reads the pixels)
+  if (model_ != ModelKind::MLP || dtype_ != DType::BF16 || fused_wgrad || !p_.xrows || p_.z1p) return;
+  hb.xrows = ptr<uint8_t>(p_.xrows);
   hb.gx_B = br.B;
 #else
   (void)hb; (void)br; (void)fused_wgrad;

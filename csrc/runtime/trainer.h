@@ -24,6 +24,7 @@ struct TrainerPtrs {
   uintptr_t z1p = 0;  // optional: enables the small-batch layer-1 split path
   uintptr_t stamps = 0;  // optional: per-block phase timestamps of the head kernel (profiling)
   uintptr_t xnext = 0, ynext = 0;  // optional: small-batch MLP look-ahead gather buffers (BatchRef)
+  uintptr_t xrows = 0;  // optional: MLP bf16 raw-row hand-off head -> layer-1 wgrad ([batch][784] uint8)
 };
 
 // A gradient bucket = contiguous range of the flat grad slab, all-reduced as one RCCL call as
@@ -136,8 +137,8 @@ class Trainer {
  private:
   BatchRef batch_ref(int B) const;
   HeadBuffers head_buffers(float* metrics) const;
-  // MLP bf16 training: the layer-1 weight gradient re-gathers the batch's uint8 rows (the head skips its X^T
-  // stores), unless the step's wgrad is the SGD-fused one (no LDS staging)
+  // MLP bf16 training: the head hands the batch's raw uint8 rows to the layer-1 weight gradient instead of a
+  // bf16 X^T, unless the step's wgrad is the SGD-fused one (no LDS staging) or no row buffer was given
   void set_regather(HeadBuffers& hb, const BatchRef& br, bool fused_wgrad) const;
   LenetConvBuffers conv_buffers() const;
   // defer_join: (single GPU, concurrent schedule, inside a multi-step graph) leave the aux branch (FC

@@ -173,6 +173,10 @@ class NativeTrainer:
         look = model == "mlp" and self.z1p is not None and not os.environ.get("MNIST_AMD_NO_LOOKAHEAD")
         self.xnext = z(_rup(self.batch, 64) * 784, dt=torch.uint8) if look else None
         self.ynext = z(_rup(self.batch, 64), dt=torch.uint8) if look else None
+        # MLP bf16, builds with MNIST_AMD_RAW_ROWS: the head hands its raw uint8 rows to the layer-1 weight
+        # gradient instead of a bf16 X^T (measured slower; csrc/kernels/head.hip wgrad_lds_body)
+        raw = getattr(C, "RAW_ROWS", False) and model == "mlp" and dtype == "bf16"
+        self.xrows = z(self.batch, 784, dt=torch.uint8) if raw else None
 
         P = C.TrainerPtrs()
         ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
@@ -184,6 +188,8 @@ class NativeTrainer:
         P.p1, P.m1, P.p2, P.m2, P.dp2 = ptr(self.p1), ptr(self.m1), ptr(self.p2), ptr(self.m2), ptr(self.dp2)
         P.z1p = ptr(self.z1p)
         P.xnext, P.ynext = ptr(self.xnext), ptr(self.ynext)
+        if hasattr(P, "xrows"):  # (A/B runs load older builds through MNIST_AMD_C_PATH)
+            P.xrows = ptr(self.xrows)
         # MNIST_AMD_STAMPS=1: per-workgroup phase timestamps (wall clock, 100 MHz), 16 slots per workgroup,
         # one row range per kernel (csrc/kernels/launch.h STAMP_*; later workgroups skip)
         self.stamps = z(C.STAMP_ROWS * 16, dt=torch.int64) if os.environ.get("MNIST_AMD_STAMPS") else None
