@@ -33,12 +33,44 @@ template <> struct Mma<float> {
   static constexpr int KV = 4;    // contiguous k per lane per chunk
   static constexpr int KC = 16;   // k per chunk
   struct Frag { f32x4 v; };
+#ifndef MNIST_AMD_F32_SPLIT
   static DEV void mma(f32x4& acc, const Frag& a, const Frag& b) {
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[0], b.v[0], acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[1], b.v[1], acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[2], b.v[2], acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[3], b.v[3], acc, 0, 0, 0);
   }
+#else
+  // Opt-in build (MNIST_AMD_F32_SPLIT): fp32 operands as hi + lo bf16 pairs (hi = the upper 16 bits, exact
+  // remainder rounded to bf16), product = lo*hi + hi*lo + hi*hi on v_mfma_f32_16x16x16_bf16, whose lane layout
+  // (4 contiguous k per lane, K = 16) is this chunk's: three bf16 MFMAs instead of four f32 ones at 1/16 of the
+  // bf16 rate.  Relative error per product <= ~2^-16 (the dropped lo*lo and the rounding of lo).
+  typedef __attribute__((ext_vector_type(4))) short s16x4;
+  static DEV void split(const f32x4& x, s16x4& hi, s16x4& lo) {
+    unsigned u[4];
+    f32x4 r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      u[j] = __builtin_bit_cast(unsigned, x[j]);
+      r[j] = x[j] - __builtin_bit_cast(float, u[j] & 0xFFFF0000u);
+    }
+    const unsigned h01 = __builtin_amdgcn_perm(u[1], u[0], 0x07060302u);
+    const unsigned h23 = __builtin_amdgcn_perm(u[3], u[2], 0x07060302u);
+    hi = __builtin_bit_cast(s16x4, (unsigned __attribute__((ext_vector_type(2)))){h01, h23});
+    bf16x4 l;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) l[j] = (bf16)r[j];
+    lo = __builtin_bit_cast(s16x4, l);
+  }
+  static DEV void mma(f32x4& acc, const Frag& a, const Frag& b) {
+    s16x4 ah, al, bh, bl;
+    split(a.v, ah, al);
+    split(b.v, bh, bl);
+    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, bh, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, bl, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, bh, acc, 0, 0, 0);
+  }
+#endif
   static DEV Frag load(const float* p) { Frag f; f.v = *reinterpret_cast<const f32x4*>(p); return f; }
   static DEV Frag zero() { Frag f; f.v = f32x4{0.f, 0.f, 0.f, 0.f}; return f; }
   static DEV void set(Frag& f, int j, float x) { f.v[j] = x; }
