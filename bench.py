@@ -358,6 +358,8 @@ def main(argv=None) -> int:
         comm_desc = "none (single process, no gradient exchange)"
     ms = elapsed / a.steps * 1e3
     value = n_gpus * a.batch * a.steps / elapsed
+    from pytorch_ddp_mnist_amd.ops.native import load_c as _load_c
+    split = getattr(_load_c(), "F32_SPLIT", 0) if a.dtype == "fp32" else 0
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -369,7 +371,8 @@ def main(argv=None) -> int:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": a.dtype,
+        # an opt-in split build (MNIST_AMD_F32_SPLIT) computes fp32 products as bf16-part MFMAs: say so
+        "dtype": a.dtype + (f" (products as {split}-part bf16 MFMAs)" if split else ""),
         "data": f"synthetic (MNIST-shaped 28x28 uint8, class-template + noise, mode={a.synthetic_mode}; "
                 "random-init weights)" + ("; loaded from a CDF-5 netCDF file" if load else ""),
         "config": {

@@ -47,6 +47,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("metric_rows", [](int B) { return metric_rows(B); });
   m.attr("L1_SPLIT_MAX_B") = L1_SPLIT_MAX_B;
   m.attr("STAMP_ROWS") = STAMP_ROWS;
+#ifdef MNIST_AMD_F32_SPLIT
+  m.attr("F32_SPLIT") = (int)MNIST_AMD_F32_SPLIT;  // fp32 products as bf16-part MFMAs (common.h Mma<float>)
+#else
+  m.attr("F32_SPLIT") = 0;
+#endif
 #ifdef MNIST_AMD_RAW_ROWS
   m.attr("RAW_ROWS") = true;
 #else

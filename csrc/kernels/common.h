@@ -41,34 +41,49 @@ template <> struct Mma<float> {
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[3], b.v[3], acc, 0, 0, 0);
   }
 #else
-  // Opt-in build (MNIST_AMD_F32_SPLIT): fp32 operands as hi + lo bf16 pairs (hi = the upper 16 bits, exact
-  // remainder rounded to bf16), product = lo*hi + hi*lo + hi*hi on v_mfma_f32_16x16x16_bf16, whose lane layout
-  // (4 contiguous k per lane, K = 16) is this chunk's: three bf16 MFMAs instead of four f32 ones at 1/16 of the
-  // bf16 rate.  Relative error per product <= ~2^-16 (the dropped lo*lo and the rounding of lo).
+  // Opt-in build (MNIST_AMD_F32_SPLIT=2 or 3): fp32 operands as 2 or 3 bf16 parts (hi = x rounded to bf16, then
+  // each exact remainder rounded to bf16), products on v_mfma_f32_16x16x16_bf16, whose lane layout (4
+  // contiguous k per lane, K = 16) is this chunk's.  =2: lo*lo + lo*hi + hi*lo + hi*hi, 4 bf16 MFMAs instead of
+  // 4 f32 ones (at 1/16 of the bf16 rate), ~2^-16 relative error per product (the rounding of lo).  =3: the six
+  // terms of weight >= 2^-16 of (hi + mid + lo)^2, ~2^-24 (fp32-like).
   typedef __attribute__((ext_vector_type(4))) short s16x4;
-  static DEV void split(const f32x4& x, s16x4& hi, s16x4& lo) {
-    unsigned u[4];
-    f32x4 r;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      u[j] = __builtin_bit_cast(unsigned, x[j]);
-      r[j] = x[j] - __builtin_bit_cast(float, u[j] & 0xFFFF0000u);
-    }
-    const unsigned h01 = __builtin_amdgcn_perm(u[1], u[0], 0x07060302u);
-    const unsigned h23 = __builtin_amdgcn_perm(u[3], u[2], 0x07060302u);
-    hi = __builtin_bit_cast(s16x4, (unsigned __attribute__((ext_vector_type(2)))){h01, h23});
-    bf16x4 l;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) l[j] = (bf16)r[j];
-    lo = __builtin_bit_cast(s16x4, l);
+  // (whole vectors are bit-cast: hipcc (ROCm 7.2) lowered __builtin_bit_cast of an ext-vector ELEMENT --
+  // x.y, x[j] -- to a read of element 0)
+  static DEV s16x4 part(const f32x4 x, f32x4& rem) {  // x rounded to bf16; rem = x - that (exact)
+    typedef __attribute__((ext_vector_type(4))) unsigned u4;
+    typedef __attribute__((ext_vector_type(4))) unsigned short us4;
+    bf16x4 h;
+    h.x = (bf16)x.x;
+    h.y = (bf16)x.y;
+    h.z = (bf16)x.z;
+    h.w = (bf16)x.w;
+    const u4 hw = __builtin_convertvector(__builtin_bit_cast(us4, h), u4) << 16;  // h as fp32 bits
+    rem = x - __builtin_bit_cast(f32x4, hw);
+    return __builtin_bit_cast(s16x4, h);
+  }
+  static DEV f32x4 mf(const s16x4 a, const s16x4 b, f32x4 acc) {
+    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, acc, 0, 0, 0);
   }
   static DEV void mma(f32x4& acc, const Frag& a, const Frag& b) {
-    s16x4 ah, al, bh, bl;
-    split(a.v, ah, al);
-    split(b.v, bh, bl);
-    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, bh, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, bl, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, bh, acc, 0, 0, 0);
+    f32x4 ra, rb;
+    const s16x4 ah = part(a.v, ra), bh = part(b.v, rb);
+#if MNIST_AMD_F32_SPLIT >= 3
+    f32x4 ra2, rb2;
+    const s16x4 am = part(ra, ra2), bm = part(rb, rb2);
+    const s16x4 al = part(ra2, ra), bl = part(rb2, rb);
+    acc = mf(al, bh, acc);
+    acc = mf(ah, bl, acc);
+    acc = mf(am, bm, acc);
+    acc = mf(am, bh, acc);
+    acc = mf(ah, bm, acc);
+    acc = mf(ah, bh, acc);
+#else
+    const s16x4 al = part(ra, ra), bl = part(rb, rb);
+    acc = mf(al, bl, acc);
+    acc = mf(al, bh, acc);
+    acc = mf(ah, bl, acc);
+    acc = mf(ah, bh, acc);
+#endif
   }
 #endif
   static DEV Frag load(const float* p) { Frag f; f.v = *reinterpret_cast<const f32x4*>(p); return f; }
