@@ -34,3 +34,5 @@ int main() {
   printf("max abs err %.3e  (max |ref| %.3f)  C[0][0]=%f\n", maxerr, maxref, hC[0]);
   return maxerr < 1e-3 * maxref ? 0 : 1;
 }
+// Build and run (one GPU):  hipcc --offload-arch=gfx950 -O3 -std=c++17 -DMNIST_AMD_F32_SPLIT=2 \
+//   scripts/diag/mfma_split_check.hip -o /tmp/split_check && /tmp/split_check
