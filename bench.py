@@ -394,6 +394,11 @@ def main(argv=None) -> int:
         "input": load or {"source": "in-memory synthetic split -> HBM (one copy)"},
         "comm_profile": prof,
         "top1": None if top1 is None else round(top1, 4),
+        # what the top-1 above measures: the 10000-image synthetic test split after warm-up + timed steps
+        "top1_eval": None if top1 is None else {
+            "split": f"synthetic test (10000, mode={a.synthetic_mode})",
+            "steps_trained": a.warmup + a.steps,
+            "epochs_trained": round((a.warmup + a.steps) * a.batch * n_gpus / 60000, 2)},
         "train_loss_mean": round(train.mean_loss, 4),
     }
     if a.digest or a.dump_params:
