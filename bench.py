@@ -68,10 +68,11 @@ def parse(argv=None):
                     help="gradient data plane of the captured step: RCCL (default) or the one-shot xGMI all-reduce "
                          "(every rank pushes its slice into every peer's IPC-mapped slot, then sums its own slots in "
                          "rank order; parallel/oneshot.py).  With --comm gloo the ranks may share one GPU")
-    ap.add_argument("--plan", default="auto", choices=["auto", "join", "split", "fixed"],
+    ap.add_argument("--plan", default="auto", choices=["auto", "join", "split", "overlap", "fixed"],
                     help="step plan: auto = time the candidates at start-up and keep the fastest "
                          "(multi-GPU plans, or the single-GPU schedules); join/split = that multi-GPU plan; "
-                         "fixed = no calibration, defaults")
+                         "overlap = LeNet, one-shot all-reduces inside the concurrent schedule's branches "
+                         "(needs a validated one-shot data plane); fixed = no calibration, defaults")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--comm-world1", action="store_true",
                     help="attach a world-1 RCCL communicator (runs the multi-GPU step schedule on one GPU)")
@@ -157,6 +158,21 @@ def bench_data(world: int, rank: int, batch: int, total_steps: int, mode: str = 
                          for e in range(n_epochs)]).to(torch.int32)
     test_x, test_y = make_split(10000, seed=2, mode=mode)
     return torch.from_numpy(images), torch.from_numpy(labels), idx_all, test_x, test_y
+
+
+def attach_overlap_plan(ctx, tr, fc_inst, world: int) -> str:
+    """LeNet: make the one-shot OVERLAP plan available (csrc/runtime/trainer.h Plan::OVERLAP) -- ``fc_inst`` (a
+    validated one-shot instance, >= the FC range) carries the FC range on the aux stream, a second instance,
+    built and validated here, the conv range on the main stream.  Collective; never fatal: returns "" or why
+    the plan is unavailable (agreed by every rank)."""
+    if tr.model_name != "lenet5":
+        return "LeNet-only plan"
+    from pytorch_ddp_mnist_amd.parallel.oneshot import probe_oneshot
+    conv, err = probe_oneshot(ctx, int(tr.rt.conv_params))
+    if conv is None:
+        return err
+    tr.attach_overlap(fc_inst, conv, world)
+    return ""
 
 
 def netcdf_data(ctx, images, labels, data_dir, mode: str):
@@ -271,6 +287,9 @@ def main(argv=None) -> int:
         if err:
             raise SystemExit(f"[bench] one-shot all-reduce failed its check: {err}")
         tr.attach_oneshot(oneshot, W)
+        ov_err = attach_overlap_plan(ctx, tr, oneshot, W)
+        if ov_err and pinned == "overlap":
+            raise SystemExit(f"[bench] --plan overlap: {ov_err}")
     if external:
         import torch.distributed as dist
         if a.comm == "gloo":
@@ -298,6 +317,11 @@ def main(argv=None) -> int:
             # comm_profile next to RCCL's latency; the step keeps RCCL (never fatal)
             from pytorch_ddp_mnist_amd.parallel.oneshot import probe_oneshot
             probe, probe_err = probe_oneshot(ctx, tr.nparam)
+            if probe is not None:
+                # the validated instance also carries the OVERLAP plan's FC range (a calibration candidate)
+                ov_err = attach_overlap_plan(ctx, tr, probe, W)
+                if ov_err:
+                    probe_err = f"overlap plan unavailable: {ov_err}"
         tr.broadcast_params(0)
         if pinned is not None:
             tr.set_plan(pinned)
@@ -345,9 +369,11 @@ def main(argv=None) -> int:
 
     n_gpus = comm.world if comm is not None else W
     info = tr.plan_info()
-    if oneshot is not None:
+    if oneshot is not None or info["plan"] == "overlap":
         colls = " + ".join(f"{c['bytes'] // 1024} KiB" for c in info["collectives"])
-        comm_desc = f"one-shot xGMI all-reduce (IPC peer slots, fixed rank order), plan={info['plan']}: {colls} per step"
+        where = " inside the backward branches" if info["plan"] == "overlap" else ""
+        comm_desc = (f"one-shot xGMI all-reduce (IPC peer slots, fixed rank order){where}, plan={info['plan']}: "
+                     f"{colls} per step" + (f" (RCCL {rccl_version} attached: broadcast, comparison)" if comm else ""))
     elif comm is not None:
         colls = " + ".join(f"{c['bytes'] // 1024} KiB" for c in info["collectives"])
         comm_desc = f"native RCCL {rccl_version}, plan={info['plan']}: all-reduce {colls} per step"

@@ -188,6 +188,8 @@ PYBIND11_MODULE(_C, m) {
            py::arg("batch"), py::arg("ld_b"), py::arg("fc_splits"), py::arg("ptrs"))
       .def("set_comm", &Trainer::set_comm)
       .def("set_oneshot", &Trainer::set_oneshot)
+      .def("set_overlap", &Trainer::set_overlap, py::arg("fc"), py::arg("conv"))
+      .def_property_readonly("has_overlap", &Trainer::has_overlap)
       .def_property_readonly("has_oneshot", &Trainer::has_oneshot)
       .def("set_world", &Trainer::set_world)
       .def("set_optimizer", &Trainer::set_optimizer)

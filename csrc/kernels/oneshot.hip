@@ -30,6 +30,21 @@ struct OneShotArgs {
 
 constexpr int OS_THREADS = 256;
 
+// Ordering without cache-maintenance fences (a system-scope release / acquire pair wrote back and invalidated
+// the whole L2 in every block: ~14 us per call at world 1, whatever the size): every payload byte moves with
+// system-coherent write-through / cache-bypassing 16-byte buffer accesses (sc0 sc1), so (a) a storing wave's
+// s_waitcnt vmcnt(0) means its pushes are performed at the destination before its block raises a flag
+// (relaxed system-scope atomic store, also sc0 sc1), and (b) the receive slots are read with sc0 sc1 loads after
+// the flag poll, which no cache line can serve stale -- the LLVM AMDGPU memory model's release / acquire minus
+// the L2 write-back / invalidate that only non-coherent accesses need (MI355X_MICROARCH.md, visibility: "sc1
+// stores and loads in place of the release and the acquire").  MNIST_AMD_ONESHOT_FENCES builds the fenced form.
+constexpr int SYS = 17;  // buffer-instruction cache policy: sc0 | sc1 (system coherent)
+typedef __attribute__((address_space(1))) uint32_t gu32;  // flags: global (not flat) accesses
+constexpr int RSRC3 = 0x00020000;  // raw buffer descriptor word 3 (32-bit data, untyped)
+DEV __amdgpu_buffer_rsrc_t rsrc(const void* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes, RSRC3);
+}
+
 __global__ __launch_bounds__(OS_THREADS) void oneshot_allreduce_kernel(OneShotArgs a) {
   const int b = blockIdx.x, nblk = gridDim.x, tid = threadIdx.x;
   const int nv = a.count >> 2;                       // float4 elements
@@ -40,29 +55,37 @@ __global__ __launch_bounds__(OS_THREADS) void oneshot_allreduce_kernel(OneShotAr
   __syncthreads();
   const uint32_t s = s_seq;
   const int par = s & 1;
+  const int slot_bytes = a.max_count * 4;
   // 1. push this block's slice into slot [rank] of every rank's receive buffer
-  for (int v = v0 + tid; v < v1; v += OS_THREADS) {
-    const f32x4 x = reinterpret_cast<const f32x4*>(a.buf)[v];
-    for (int q = 0; q < a.world; ++q) {
-      f32x4* dst = reinterpret_cast<f32x4*>(a.peer_data[q] + ((size_t)par * a.world + a.rank) * a.max_count);
-      dst[v] = x;
+  for (int q = 0; q < a.world; ++q) {
+    const float* slot = a.peer_data[q] + ((size_t)par * a.world + a.rank) * a.max_count;
+#ifdef MNIST_AMD_ONESHOT_FENCES
+    for (int v = v0 + tid; v < v1; v += OS_THREADS)
+      reinterpret_cast<f32x4*>(const_cast<float*>(slot))[v] = reinterpret_cast<const f32x4*>(a.buf)[v];
+    if (b == 0 && tid < (a.count & 3)) const_cast<float*>(slot)[(nv << 2) + tid] = a.buf[(nv << 2) + tid];
+#else
+    const __amdgpu_buffer_rsrc_t r = rsrc(slot, slot_bytes);
+    for (int v = v0 + tid; v < v1; v += OS_THREADS)
+      __builtin_amdgcn_raw_buffer_store_b128(reinterpret_cast<const u32x4*>(a.buf)[v], r, v * 16, 0, SYS);
+    if (b == 0 && tid < (a.count & 3)) {  // tail (count % 4) by block 0
+      const int e = (nv << 2) + tid;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, a.buf[e]), r, e * 4, 0, SYS);
     }
+#endif
   }
-  // tail (count % 4) by block 0
-  if (b == 0 && tid < (a.count & 3)) {
-    const int e = (nv << 2) + tid;
-    for (int q = 0; q < a.world; ++q) a.peer_data[q][((size_t)par * a.world + a.rank) * a.max_count + e] = a.buf[e];
-  }
-  // every storing wave's stores are complete (system scope) before the block's flags are raised
+#ifdef MNIST_AMD_ONESHOT_FENCES
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+#endif
+  // every storing wave's pushes are performed before the block's flags are raised
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid < a.world) {
-    __hip_atomic_store(a.peer_flags[tid] + (size_t)a.rank * nblk + b, s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store((gu32*)(a.peer_flags[tid] + (size_t)a.rank * nblk + b), s, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
   }
   // 2. wait for every rank's flag of this block (lane r polls source rank r), bounded
   if (tid < a.world) {
-    const uint32_t* f = a.peer_flags[a.rank] + (size_t)tid * nblk + b;
+    gu32* f = (gu32*)(a.peer_flags[a.rank] + (size_t)tid * nblk + b);
     const unsigned long long t0 = wall_clock64();
     while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < s) {
       if (wall_clock64() - t0 > a.timeout_ticks) {
@@ -72,10 +95,13 @@ __global__ __launch_bounds__(OS_THREADS) void oneshot_allreduce_kernel(OneShotAr
       __builtin_amdgcn_s_sleep(2);
     }
   }
+#ifdef MNIST_AMD_ONESHOT_FENCES
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#endif
   __syncthreads();
   // 3. sum the W slots of the own receive buffer in rank order
   const float* rb = a.peer_data[a.rank] + (size_t)par * a.world * a.max_count;
+#ifdef MNIST_AMD_ONESHOT_FENCES
   for (int v = v0 + tid; v < v1; v += OS_THREADS) {
     f32x4 acc = reinterpret_cast<const f32x4*>(rb)[v];
     for (int r = 1; r < a.world; ++r) acc += reinterpret_cast<const f32x4*>(rb + (size_t)r * a.max_count)[v];
@@ -87,6 +113,22 @@ __global__ __launch_bounds__(OS_THREADS) void oneshot_allreduce_kernel(OneShotAr
     for (int r = 1; r < a.world; ++r) acc += rb[(size_t)r * a.max_count + e];
     a.buf[e] = acc;
   }
+#else
+  const __amdgpu_buffer_rsrc_t rr = rsrc(rb, a.world * slot_bytes);
+  for (int v = v0 + tid; v < v1; v += OS_THREADS) {
+    f32x4 acc = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, v * 16, 0, SYS));
+    for (int r = 1; r < a.world; ++r)
+      acc += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rr, r * slot_bytes + v * 16, 0, SYS));
+    reinterpret_cast<f32x4*>(a.buf)[v] = acc;
+  }
+  if (b == 0 && tid < (a.count & 3)) {
+    const int e = (nv << 2) + tid;
+    float acc = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, e * 4, 0, SYS));
+    for (int r = 1; r < a.world; ++r)
+      acc += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rr, r * slot_bytes + e * 4, 0, SYS));
+    a.buf[e] = acc;
+  }
+#endif
   if (tid == 0) a.seq[b] = s;
 }
 

@@ -5,6 +5,7 @@
 //                    -> reduce+sgd(conv) + step bump (fused reduce/SGD/pack kernels)
 //   LeNet, comm    : conv_fwd -> head -> { conv_bwd -> reduce(conv)  ||  wgrad(FC) -> reduce(FC) on aux }
 //                    then Plan::JOIN  : ONE all-reduce of the coalesced slab -> sgd_pack
+//                      or Plan::OVERLAP: one-shot AR + update inside each branch (aux: FC, main: conv)
 //                      or Plan::SPLIT : comm stream: AR(FC buckets) as soon as reduce(FC) is done (beside
 //                                       conv_bwd) -> update(FC range); then AR(conv buckets) after
 //                                       reduce(conv) -> update(conv range) + step bump
@@ -127,6 +128,9 @@ void Trainer::release() {
   }
   comm_.reset();
   oneshot_.reset();
+  ov_fc_.reset();
+  ov_conv_.reset();
+  if (plan_ == Plan::OVERLAP) plan_ = Plan::JOIN;
 }
 
 int Trainer::pack_size() const { return model_pack_size(model_); }
@@ -299,13 +303,18 @@ void Trainer::all_reduce(const std::vector<Bucket>& bs, int phase, hipStream_t s
     if (phase < 0 || b.phase == phase) {
       float* g = ptr<float>(p_.grad) + b.p0;
       if (oneshot_) oneshot_->all_reduce_sum_f32(g, size_t(b.p1 - b.p0), s);
-      else comm_->all_reduce_sum_f32(g, size_t(b.p1 - b.p0), s);
+      else if (comm_) comm_->all_reduce_sum_f32(g, size_t(b.p1 - b.p0), s);
+      else throw std::logic_error("all_reduce: no RCCL communicator or one-shot instance for this plan");
     }
 }
 
 std::vector<Bucket> Trainer::issued_collectives() const {
   std::vector<Bucket> out;
   if (!use_comm()) return out;
+  if (plan_ == Plan::OVERLAP) {  // aux stream's FC range, main stream's conv range
+    const int cp = model_conv_params(model_);
+    return {{cp, nparam_, 0}, {0, cp, 1}};
+  }
   if (plan_ == Plan::SPLIT) {
     for (const Bucket& b : buckets_) if (b.phase == 0) out.push_back(b);
     for (const Bucket& b : buckets_) if (b.phase != 0) out.push_back(b);
@@ -359,6 +368,13 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     int nslab = 0;
     launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s, bwd_blocks_);
     post_launch(s);
+    if (comm && plan_ == Plan::OVERLAP) {
+      launch_lenet_overlap(B, nslab, s, hb, hrows);
+      // like the local schedule: the FC branch is joined by the next step's head inside a multi-step graph
+      if (defer_join) aux_pending_ = true;
+      else HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));
+      return;
+    }
     if (comm) {
       const int splits =
           launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, aux_stream_, hrows);
@@ -531,6 +547,31 @@ void Trainer::launch_lenet_comm_tail(int B, int nslab, int splits, hipStream_t s
   HIP_CHECK(hipEventRecord(events_[0], comm_stream_));
   HIP_CHECK(hipStreamWaitEvent(s, events_[0], 0));
   trace("split: done");
+}
+
+// Plan::OVERLAP (see trainer.h): each branch reduces its slab, all-reduces its range with its own one-shot
+// instance and updates it (1/W folded into the update).  Same reduce trees and update kernels as JOIN, so at
+// world 1 it is bitwise the local step.
+void Trainer::launch_lenet_overlap(int B, int nslab, hipStream_t s, const HeadBuffers& hb, int hrows) {
+  const float scale = 1.0f / float(B), gs = 1.0f / float(world_);
+  const int cp = model_conv_params(model_);
+  float* g = ptr<float>(p_.grad);
+  const int splits =
+      launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, aux_stream_, hrows);
+  post_launch(aux_stream_);
+  launch_reduce(ptr<const float>(p_.slab_fc), nparam_, splits, cp, nparam_, scale, g, aux_stream_);
+  post_launch(aux_stream_);
+  ov_fc_->all_reduce_sum_f32(g + cp, size_t(nparam_ - cp), aux_stream_);
+  launch_sgd_pack_range(model_, dtype_, ptr<float>(p_.params), g, ptr<float>(p_.mom), ptr<void>(p_.pack), cp, nparam_,
+                        lr_, momentum_, gs, nullptr, aux_stream_);
+  post_launch(aux_stream_);
+  HIP_CHECK(hipEventRecord(events_[5], aux_stream_));
+  launch_reduce(ptr<const float>(p_.slab_conv), cp, nslab, 0, cp, scale, g, s);
+  post_launch(s);
+  ov_conv_->all_reduce_sum_f32(g, size_t(cp), s);
+  launch_sgd_pack_range(model_, dtype_, ptr<float>(p_.params), g, ptr<float>(p_.mom), ptr<void>(p_.pack), 0, cp, lr_,
+                        momentum_, gs, ptr<int32_t>(p_.step), s);
+  post_launch(s);
 }
 
 std::vector<Bucket> Trainer::coalesced_buckets() const {

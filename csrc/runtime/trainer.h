@@ -42,7 +42,12 @@ struct Bucket {
 //           whose grid can be capped to leave whole CUs free for RCCL's kernels; MLP: beside the layer-1
 //           weight gradient) and phase 0's parameters are updated right after them on the same stream;
 //           phase 1's buckets follow its reduce, then its update (which also bumps the step counters).
-enum class Plan : int { JOIN = 0, SPLIT = 1 };
+//   OVERLAP (LeNet, one-shot data plane): the single-GPU concurrent schedule with an all-reduce inside each
+//           branch -- aux: FC wgrad -> reduce -> one-shot AR(FC) -> FC update, beside conv_bwd; main: conv_bwd ->
+//           reduce -> one-shot AR(conv) -> conv update + step bump; the aux branch is joined by the next step's
+//           head like the local schedule.  Two one-shot instances (one per branch/stream, each with its own
+//           slots, flags and sequence numbers); no RCCL call and no cross-stream event behind a collective.
+enum class Plan : int { JOIN = 0, SPLIT = 1, OVERLAP = 2 };
 
 class Trainer {
  public:
@@ -54,6 +59,13 @@ class Trainer {
   // Works with or without an RCCL communicator attached (parameter broadcast then goes over the control plane).
   void set_oneshot(std::shared_ptr<OneShotAllReduce> o) { invalidate(); oneshot_ = std::move(o); }
   bool has_oneshot() const { return oneshot_ != nullptr; }
+  // Plan::OVERLAP's two one-shot instances: FC range [conv_params, n) on the aux stream, conv range on main
+  void set_overlap(std::shared_ptr<OneShotAllReduce> fc, std::shared_ptr<OneShotAllReduce> conv) {
+    invalidate();
+    ov_fc_ = std::move(fc);
+    ov_conv_ = std::move(conv);
+  }
+  bool has_overlap() const { return ov_fc_ != nullptr && ov_conv_ != nullptr; }
   // Timing only (exposed-communication measurement): with a communicator attached, run the local
   // single-GPU schedule without any collective.  Cached graphs are keyed by it.
   void set_comm_enabled(bool on) { comm_enabled_ = on; }
@@ -64,7 +76,9 @@ class Trainer {
   void set_buckets(const std::vector<Bucket>& b) { buckets_ = b; invalidate(); }
   std::vector<Bucket> buckets() const { return buckets_; }
   void set_plan(int p) {
-    if (p != 0 && p != 1) throw std::invalid_argument("plan must be 0 (join) or 1 (split)");
+    if (p < 0 || p > 2) throw std::invalid_argument("plan must be 0 (join), 1 (split) or 2 (overlap)");
+    if (p == 2 && (model_ != ModelKind::LENET || !has_overlap()))
+      throw std::invalid_argument("plan overlap: LeNet with two one-shot instances attached (set_overlap) only");
     plan_ = static_cast<Plan>(p);
   }
   int plan() const { return static_cast<int>(plan_); }
@@ -90,7 +104,7 @@ class Trainer {
   int bwd_grid() const;
   // The collectives one full-batch step issues under the current plan, in issue order.
   std::vector<Bucket> issued_collectives() const;
-  bool has_comm() const { return comm_ != nullptr || oneshot_ != nullptr; }
+  bool has_comm() const { return comm_ != nullptr || oneshot_ != nullptr || has_overlap(); }
   int world() const { return world_; }
   // first parameter of backward phase 0 (see Plan): LeNet conv_params, MLP the layer-2 weight offset
   int phase_split() const;
@@ -145,10 +159,12 @@ class Trainer {
   // wgrad + FC update) un-joined at the end of the step; the NEXT step's head waits for it instead.
   void launch_step(int B, hipStream_t s, bool defer_join = false);
   void launch_lenet_comm_tail(int B, int nslab, int splits, hipStream_t s);
+  // Plan::OVERLAP after the fork (conv_bwd launched on s, nothing yet on aux); returns with the aux branch open
+  void launch_lenet_overlap(int B, int nslab, hipStream_t s, const HeadBuffers& hb, int hrows);
   void launch_mlp_comm_tail(int B, hipStream_t s, const HeadBuffers& hb, int hrows);
   // comm stream: wait for `ready`, all-reduce phase `phase`'s buckets, update its parameter range
   void comm_phase(int phase, hipEvent_t ready, bool bump);
-  bool use_comm() const { return (comm_ || oneshot_) && comm_enabled_; }
+  bool use_comm() const { return (comm_ || oneshot_ || has_overlap()) && comm_enabled_; }
   void sync_own_streams();
   struct GraphSlot {
     hipGraph_t graph = nullptr;
@@ -178,6 +194,7 @@ class Trainer {
   int max_conv_slabs_ = 0;  // rows of the conv slab (lenet_conv_bwd_max_blocks(batch) at the default target)
   std::shared_ptr<RcclComm> comm_;
   std::shared_ptr<OneShotAllReduce> oneshot_;
+  std::shared_ptr<OneShotAllReduce> ov_fc_, ov_conv_;
   std::vector<Bucket> buckets_;
   hipStream_t comm_stream_ = nullptr;
   hipStream_t aux_stream_ = nullptr;  // concurrent FC wgrad branch (fork/join inside the step graph)

@@ -32,7 +32,7 @@ from ..models import MODEL_IDS, build_model, flatten_state, unflatten_state
 from ..ops.native import require_gpu
 from ..parallel.comm import comm_timeout  # noqa: F401  (re-exported: watchdog deadline)
 
-PLANS = {"join": 0, "split": 1}
+PLANS = {"join": 0, "split": 1, "overlap": 2}
 
 
 def resolve_plan(name: Optional[str]) -> Optional[str]:
@@ -202,6 +202,7 @@ class NativeTrainer:
         self.world = 1
         self.comm = None
         self.oneshot = None         # one-shot xGMI all-reduce data plane (attach_oneshot)
+        self.overlap = None         # (FC, conv) one-shot instances of the OVERLAP plan (attach_overlap)
         self.ext_allreduce = None   # external data plane (attach_external_allreduce)
         self.module_template = build_model(model)
         if init is not None:
@@ -253,6 +254,17 @@ class NativeTrainer:
         self.rt.set_world(self.world)
         self.set_plan(plan, 0)
 
+    def attach_overlap(self, fc, conv, world: int) -> None:
+        """LeNet: the OVERLAP plan's two one-shot instances (``make_oneshot`` each; FC range and conv range) --
+        the concurrent single-GPU schedule with each branch's all-reduce inside it (csrc/runtime/trainer.h
+        Plan::OVERLAP).  The installed plan is not changed: ``set_plan('overlap')`` / the calibration picks it."""
+        if self.model_name != "lenet5":
+            raise ValueError("the overlap plan is LeNet-only")
+        self.overlap = (fc, conv)
+        self.world = int(world)
+        self.rt.set_overlap(fc, conv)
+        self.rt.set_world(self.world)
+
     def set_plan(self, plan: str, bwd_blocks: int = 0) -> None:
         if plan not in PLANS:
             raise ValueError(f"unknown step plan {plan!r} (choices: {sorted(PLANS)})")
@@ -273,9 +285,10 @@ class NativeTrainer:
     def plan_info(self) -> dict:
         """What a full-batch step runs: plan, conv_bwd grid, and the collectives in issue order."""
         coll = [(b.p0, b.p1) for b in self.rt.issued_collectives()]
-        dp = self.comm is not None or self.oneshot is not None
+        dp = self.comm is not None or self.oneshot is not None or self.overlap is not None
+        ov = self.plan == "overlap"
         return {"plan": self.plan if dp else ("local" if self.rt.concurrent else "local-serial"),
-                "allreduce": "oneshot" if self.oneshot is not None else ("rccl" if self.comm is not None else None),
+                "allreduce": "oneshot" if (self.oneshot is not None or ov) else ("rccl" if self.comm is not None else None),
                 "conv_bwd_grid": self.rt.bwd_grid if self.model_name == "lenet5" else None,
                 "collectives": [{"params": [a, b], "bytes": 4 * (b - a)} for a, b in coll]}
 
@@ -330,8 +343,8 @@ class NativeTrainer:
     def check_comm(self) -> None:
         """Health poll (once per epoch): abort + raise on an asynchronous RCCL error; raise if a one-shot
         all-reduce flag wait timed out."""
-        if self.oneshot is not None:
-            err = self.oneshot.check()
+        for o in ([self.oneshot] if self.oneshot is not None else []) + list(self.overlap or ()):
+            err = o.check()
             if err:
                 raise CollectiveError(err)
         if self.comm is None:
@@ -480,6 +493,7 @@ class NativeTrainer:
                                     mlp_plan_candidates)
         forced = forced_plan()
         dp = self.comm is not None or self.oneshot is not None  # a gradient data plane is attached
+        ovl = dp and self.overlap is not None and self.model_name == "lenet5"  # + the one-shot OVERLAP plan
         if dp and forced:
             self.set_plan(forced, 0)
             return {"chosen": forced, "timings_ms": {}, "forced": True}
@@ -492,6 +506,8 @@ class NativeTrainer:
                     candidates = mlp_plan_candidates()
                 if self.world > 1 and not os.environ.get("MNIST_AMD_TRY_SPLIT"):
                     candidates = {k: v for k, v in candidates.items() if v.get("plan", "join") == "join"}
+                if ovl:
+                    candidates["overlap"] = dict(plan="overlap")
             elif self.model_name == "lenet5" and self.batch <= SMALL_BATCH_SERIAL:
                 # Small LeNet batches: the serial schedule, not calibrated.  run_steps measured serial 32.8 vs
                 # concurrent 35.0 us/step at B=128 (equal at 1024), but inside the calibration the serial
@@ -541,7 +557,7 @@ class NativeTrainer:
         * ``probe``: a validated one-shot all-reduce that the step does NOT use (measure-only): its standalone
           latency per collective is reported next to RCCL's (``oneshot_us``).
         Collective: every rank calls it at the same point."""
-        if self.comm is None and self.oneshot is None:
+        if self.comm is None and self.oneshot is None and self.overlap is None:
             return {"rccl_world": None}
         colls = []
         for c in self.plan_info()["collectives"]:
@@ -560,7 +576,8 @@ class NativeTrainer:
                 med = ts[len(ts) // 2]
                 med = reduce_max(med) if reduce_max is not None else med
                 row["allreduce_us"] = round(med * 1000.0, 2)
-            os_ = self.oneshot if self.oneshot is not None else probe
+            os_ = self.oneshot if self.oneshot is not None else (probe if probe is not None else
+                                                                  (self.overlap[0] if self.overlap else None))
             if os_ is not None:
                 from ..parallel.oneshot import time_oneshot
                 med = time_oneshot(os_, b - a, self.device, iters=iters, warmup=warmup)
@@ -578,7 +595,7 @@ class NativeTrainer:
             t = self.time_schedules({"plan": cur, **loc}, iters=iters, warmup=warmup, reduce_max=reduce_max)
             plan_ms, local_ms = t["plan"], min(t["nocomm"], t["nocomm_serial"])
         return {"rccl_world": int(self.comm.world) if self.comm is not None else None,
-                "allreduce": "oneshot" if self.oneshot is not None else "rccl", "collectives": colls,
+                "allreduce": self.plan_info()["allreduce"], "collectives": colls,
                 "step_plan_ms": round(plan_ms, 4), "step_local_ms": round(local_ms, 4),
                 "exposed_comm_us": round((plan_ms - local_ms) * 1000.0, 2)}
 
@@ -592,6 +609,7 @@ class NativeTrainer:
         self.rt.release()
         self.comm = None
         self.oneshot = None
+        self.overlap = None
 
     # ------------------------------------------------------------------ training
     def set_epoch_indices(self, indices: torch.Tensor) -> None:

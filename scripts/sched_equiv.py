@@ -10,7 +10,7 @@ rank's "all-reduced" gradient is its own): they must equal a local run at half t
 ``_k<k>`` variants run the steps as ONE k-step graph (run_steps), whose steps may leave the aux
 branch join to the next step's head; they must equal the same number of single-step graphs.
 Usage: python scripts/sched_equiv.py [--model mlp|lenet5] [--dtype bf16|fp32] [--batch B] VARIANT [VARIANT ...]
-  VARIANT = {local,local_halflr,join,split}[_b<blocks>][_w2][_k<k>]
+  VARIANT = {local,local_halflr,join,split,overlap}[_b<blocks>][_w2][_k<k>]   (overlap: LeNet, world-1 one-shot)
 """
 import argparse
 import hashlib
@@ -39,7 +39,7 @@ C = load_c()
 order = torch.randperm(4096, generator=torch.Generator().manual_seed(1)).to(torch.int32)
 
 for v in a.variants:
-    m = re.fullmatch(r"(local_halflr|local|join|split)(?:_b(\d+))?(_w2)?(?:_k(\d+))?", v)
+    m = re.fullmatch(r"(local_halflr|local|join|split|overlap)(?:_b(\d+))?(_w2)?(?:_k(\d+))?", v)
     if not m:
         raise SystemExit(f"unknown variant {v}")
     kind, blocks, w2, k = m.group(1), int(m.group(2) or 0), bool(m.group(3)), int(m.group(4) or 0)
@@ -51,6 +51,10 @@ for v in a.variants:
         tr.attach_comm(C.RcclComm(C.RcclComm.make_unique_id(), 0, 1, 0), 2 if w2 else 1, plan=kind,
                        bwd_blocks=blocks)
         tr.broadcast_params(0)
+    elif kind == "overlap":  # world-1 one-shot instances (identity sums), the 1/W of a 2-rank job with _w2
+        fc, conv = C.OneShotAllReduce(0, 1, 0, tr.nparam), C.OneShotAllReduce(0, 1, 0, int(tr.rt.conv_params))
+        tr.attach_overlap(fc, conv, 2 if w2 else 1)
+        tr.set_plan("overlap", blocks)
     elif blocks:
         tr.rt.set_bwd_blocks(blocks)
     tr.set_epoch_indices(order)

@@ -74,15 +74,19 @@ def _bench(args, timeout=540):
 
 
 @pytest.mark.timeout(600)
-def test_oneshot_two_ranks_share_one_gpu(native, tmp_path):
+@pytest.mark.parametrize("plan", ["fixed", "overlap"])
+def test_oneshot_two_ranks_share_one_gpu(native, tmp_path, plan):
+    """``fixed`` = JOIN (one all-reduce of the whole slab after the backward join); ``overlap`` = Plan::OVERLAP
+    (two one-shot instances, the FC range's all-reduce + update inside the aux branch beside conv_bwd)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from test_shared_gpu_ranks import _emulate
     steps, warmup, batch = 4, 2, 2048
     out, err = _bench(["--gpus", "2", "--comm", "gloo", "--allreduce", "oneshot", "--batch", str(batch),
-                       "--steps", str(steps), "--warmup", str(warmup), "--no-eval", "--digest", "--plan", "fixed",
+                       "--steps", str(steps), "--warmup", str(warmup), "--no-eval", "--digest", "--plan", plan,
                        "--dump-params", str(tmp_path / "p")])
     assert out["n_gpus"] == 2 and out["allreduce"] == "oneshot" and out["value"] > 0
     assert "one-shot" in out["config"]["comm"]
+    assert out["config"]["plan"]["plan"] == ("join" if plan == "fixed" else "overlap")
     prof = out["comm_profile"]
     assert prof["allreduce"] == "oneshot" and all(0 < c["oneshot_us"] < 10000 for c in prof["collectives"])
     digests = dict(re.findall(r"digest rank=(\d) ([0-9a-f]{64})", err))

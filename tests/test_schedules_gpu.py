@@ -8,7 +8,8 @@ backward, then phase 1's).  All of them reduce in the same fixed order, so the t
 be bitwise identical; a capped conv_bwd grid changes the summation order, so capped variants are
 compared among themselves.  The ``_w2`` variants check the 1/W averaging of both plans against a local
 run at half the learning rate; ``_k4`` variants run the steps as one 4-step graph (deferred aux join).
-The MLP has the same plans (layers 2+3 sent beside the layer-1 weight gradient).
+The MLP has the same plans (layers 2+3 sent beside the layer-1 weight gradient).  ``overlap`` (LeNet): world-1
+one-shot all-reduces inside the concurrent schedule's two branches (Plan::OVERLAP).
 """
 import os
 import re
@@ -35,11 +36,12 @@ def test_schedules_bitwise_equal(native):
     serial = _digests({"MNIST_AMD_CONCURRENT": "0"}, ["local", "local_halflr"])
     d = _digests({"MNIST_AMD_CONCURRENT": "1"},
                  ["local", "join", "split", "join_w2", "split_w2", "local_b480", "join_b480", "split_b480",
-                  "local_k4", "join_k4", "split_k4"])
+                  "local_k4", "join_k4", "split_k4", "overlap", "overlap_w2", "overlap_k4"])
     ref = serial["local"]
-    for k in ("local", "join", "split", "local_k4", "join_k4", "split_k4"):
+    for k in ("local", "join", "split", "local_k4", "join_k4", "split_k4", "overlap", "overlap_k4"):
         assert d[k] == ref, k
     assert d["join_w2"] == serial["local_halflr"] and d["split_w2"] == serial["local_halflr"]
+    assert d["overlap_w2"] == serial["local_halflr"]
     assert d["join_b480"] == d["local_b480"] and d["split_b480"] == d["local_b480"]
 
 
