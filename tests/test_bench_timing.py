@@ -74,6 +74,7 @@ def test_resolve_plan():
     assert resolve_plan("auto") is None and resolve_plan(None) is None
     assert resolve_plan("fixed") == "join"              # no calibration, default plan (no KeyError)
     assert resolve_plan("join") == "join" and resolve_plan("split") == "split"
+    assert resolve_plan("overlap") == "overlap"          # LeNet one-shot plan (needs a validated data plane)
     with pytest.raises(ValueError):
         resolve_plan("bogus")
 
