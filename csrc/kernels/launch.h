@@ -134,6 +134,12 @@ void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetC
 int launch_lenet_fwd_head(DType t, const BatchRef& br, const LenetConvBuffers& cb, const HeadBuffers& hb,
                           hipStream_t s);
 bool lenet_fwd_head_applies(DType t, int B);
+// Small LeNet bf16 batches (B <= 2048, below the fused fwd_head_kernel): conv_fwd + the 16-row head in ONE
+// launch (two images per workgroup, each 16-row group's last-arriving workgroup runs the head); `counters`:
+// [ceil(B / 16)] zeroed ints.  Returns the head rows per tile (16), or 0 when it does not apply (always 0
+// unless built with -DMNIST_AMD_FWD_HEAD_SMALL: measured slower at B = 128).
+int launch_lenet_fwd_head_small(DType t, const BatchRef& br, const LenetConvBuffers& cb, const HeadBuffers& hb,
+                                int* counters, hipStream_t s);
 // LeNet training head alone as the 16-row register-B head (lenet.hip head16_kernel) on the pool2 rows of
 // conv_fwd: bf16, B <= 2048.  Returns launch_head's rows value, or 0 when it
 // does not apply (the caller launches launch_head).

@@ -105,6 +105,13 @@ Trainer::Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const
   for (auto& e : events_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_CHECK(hipMalloc(&zero_counter_, 2 * sizeof(int32_t)));
   HIP_CHECK(hipMemset(zero_counter_, 0, 2 * sizeof(int32_t)));
+#ifdef MNIST_AMD_FWD_HEAD_SMALL
+  if (model_ == ModelKind::LENET) {
+    const size_t ng = size_t(batch_ + 15) / 16;
+    HIP_CHECK(hipMalloc(&group_counter_, ng * sizeof(int32_t)));
+    HIP_CHECK(hipMemset(group_counter_, 0, ng * sizeof(int32_t)));
+  }
+#endif
 }
 
 Trainer::~Trainer() {
@@ -116,6 +123,7 @@ Trainer::~Trainer() {
   if (comm_stream_) hipStreamDestroy(comm_stream_);
   if (aux_stream_) hipStreamDestroy(aux_stream_);
   if (zero_counter_) hipFree(zero_counter_);
+  if (group_counter_) hipFree(group_counter_);
 }
 
 void Trainer::release() {
@@ -247,7 +255,8 @@ void Trainer::forward_backward(int B, uintptr_t stream) {
   int hrows = 0;
   if (model_ == ModelKind::LENET) {
     if (fwd_head_active(B)) hrows = launch_lenet_fwd_head(dtype_, br, conv_buffers(), hb, s);
-    else launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(), s);
+    else hrows = launch_lenet_fwd_head_small(dtype_, br, conv_buffers(), hb, group_counter_, s);
+    if (!hrows) launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(), s);
     post_launch(s);
   }
   if (!hrows) {
@@ -348,7 +357,9 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
       join_aux();
       hrows = launch_lenet_fwd_head(dtype_, br, conv_buffers(), hb, s);
     } else {
-      launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(), s);
+      join_aux();  // (no-op unless a deferred join is pending: the small fused kernel also contains the head)
+      hrows = launch_lenet_fwd_head_small(dtype_, br, conv_buffers(), hb, group_counter_, s);
+      if (!hrows) launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(), s);
     }
     post_launch(s);
   }

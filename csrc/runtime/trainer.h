@@ -204,4 +204,5 @@ class Trainer {
   int multi_k_ = 0;
   int zero_step_dev_ = 0;
   int32_t* zero_counter_ = nullptr;  // device {0,0} for eval batch addressing
+  int32_t* group_counter_ = nullptr;  // [ceil(batch / 16)] zeroed: fwd_head_small_kernel hand-off counters
 };
