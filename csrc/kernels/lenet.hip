@@ -958,6 +958,13 @@ struct BwdRoles {
   }
 };
 
+// phase-B LDS prefetch distance (chunks of fragments in flight ahead of the MFMAs).  LeNet bf16 B=8192, 2000
+// steps (profiles/r4_session2/ab_conv_bwd_pd.txt): PD 1 / 2 / 3 = 0.1038-0.1041 / 0.1024-0.1034 / 0.1036-0.1038
+// ms/step, bitwise-equal parameters; fp32 unchanged (0.439 ms).
+#ifndef MNIST_AMD_BWD_PD
+#define MNIST_AMD_BWD_PD 2
+#endif
+constexpr int BWD_PD = MNIST_AMD_BWD_PD;
 // One conv_bwd workgroup: block `blk` of `nblk` (the conv_bwd part of the grid).
 template <typename T, int NW>
 DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int ipb, const int blk, const int nblk) {
@@ -1299,24 +1306,22 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
         return M::load(p1t + w2off[i] + (p0 >> 4) * 16 + (p0 & 15));
       };
       // NT real tiles on this wave: no zero-plane filler tile
+      // fragments of chunk kc + PD are issued before chunk kc's MFMAs (constant indices: registers)
       auto wgrad2 = [&](auto ntc) {
         constexpr int NTL = decltype(ntc)::value;
-        Frag a = ld_a(0), bb[NTL];
+        Frag fa[W2CH], fb[W2CH][NTL];
+        auto issue = [&](int kc) {
+          fa[kc] = ld_a(kc);
 #pragma unroll
-        for (int i = 0; i < NTL; ++i) bb[i] = ld_b(0, i);
+          for (int i = 0; i < NTL; ++i) fb[kc][i] = ld_b(kc, i);
+        };
+#pragma unroll
+        for (int kc = 0; kc < BWD_PD && kc < W2CH; ++kc) issue(kc);
 #pragma unroll
         for (int kc = 0; kc < W2CH; ++kc) {
-          Frag an = a, bn[NTL];
-          if (kc + 1 < W2CH) {
-            an = ld_a(kc + 1);
+          if (kc + BWD_PD < W2CH) issue(kc + BWD_PD);
 #pragma unroll
-            for (int i = 0; i < NTL; ++i) bn[i] = ld_b(kc + 1, i);
-          }
-#pragma unroll
-          for (int i = 0; i < NTL; ++i) M::mma(accW2[i], a, bb[i]);
-          a = an;
-#pragma unroll
-          for (int i = 0; i < NTL; ++i) bb[i] = bn[i];
+          for (int i = 0; i < NTL; ++i) M::mma(accW2[i], fa[kc], fb[kc][i]);
         }
       };
       if (nw == 2) wgrad2(std::integral_constant<int, 2>{});
@@ -1370,20 +1375,19 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
           // y1 loads only its first SH chunks (20 instead of 30 A reads per pair for bf16).
           constexpr int SH = 160 / KC;  // chunks per two kernel rows (10 taps x 16 channels)
           static_assert(SH < D2CH, "row-pair A reuse needs more than two kernel rows of K");
-          Frag A0[D2CH];
-          Frag fb = M::load(bq), fa1 = M::load(a1 + doff(0));
-          A0[0] = M::load(a0 + doff(0));
+          Frag A0[D2CH], A1[D2CH], FB[D2CH];
+          auto issue = [&](int kc) {
+            FB[kc] = M::load(bq + kc * KC);
+            A0[kc] = M::load(a0 + doff(kc));
+            A1[kc] = kc < SH ? M::load(a1 + doff(kc)) : A0[kc - SH];
+          };
 #pragma unroll
-          for (int kc = 0; kc < D2CH; ++kc) {  // next chunk's fragments in flight during this one's MFMAs
-            Frag nb = fb, na1 = fa1;
-            if (kc + 1 < D2CH) {
-              nb = M::load(bq + (kc + 1) * KC);
-              A0[kc + 1] = M::load(a0 + doff(kc + 1));
-              na1 = kc + 1 < SH ? M::load(a1 + doff(kc + 1)) : A0[kc + 1 - SH];
-            }
-            M::mma(acc0, A0[kc], fb);
-            M::mma(acc1, fa1, fb);
-            fb = nb; fa1 = na1;
+          for (int kc = 0; kc < BWD_PD; ++kc) issue(kc);
+#pragma unroll
+          for (int kc = 0; kc < D2CH; ++kc) {  // chunk kc + PD's fragments in flight during this one's MFMAs
+            if (kc + BWD_PD < D2CH) issue(kc + BWD_PD);
+            M::mma(acc0, A0[kc], FB[kc]);
+            M::mma(acc1, A1[kc], FB[kc]);
           }
           dgrad_tile_epi(y0, acc0);
           dgrad_tile_epi(y1, acc1);
@@ -1391,16 +1395,17 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
           const int y0 = 2 * q0;
           const T* a0 = dys + ((y0 + 4) * 18 + x + 4) * 16;
           f32x4 acc0 = zero4();
-          Frag fb = M::load(bq), fa0 = M::load(a0 + doff(0));
+          Frag A0[D2CH], FB[D2CH];
+          auto issue = [&](int kc) {
+            FB[kc] = M::load(bq + kc * KC);
+            A0[kc] = M::load(a0 + doff(kc));
+          };
+#pragma unroll
+          for (int kc = 0; kc < BWD_PD; ++kc) issue(kc);
 #pragma unroll
           for (int kc = 0; kc < D2CH; ++kc) {
-            Frag nb = fb, na0 = fa0;
-            if (kc + 1 < D2CH) {
-              nb = M::load(bq + (kc + 1) * KC);
-              na0 = M::load(a0 + doff(kc + 1));
-            }
-            M::mma(acc0, fa0, fb);
-            fb = nb; fa0 = na0;
+            if (kc + BWD_PD < D2CH) issue(kc + BWD_PD);
+            M::mma(acc0, A0[kc], FB[kc]);
           }
           dgrad_tile_epi(y0, acc0);
         }
