@@ -56,7 +56,8 @@ PYBIND11_MODULE(_C, m) {
   m.attr("RAW_ROWS") = true;
 #else
   m.attr("RAW_ROWS") = false;
-#endif  // rows of the MNIST_AMD_STAMPS buffer (launch.h)
+#endif
+  m.attr("XB_MAX_B") = Trainer::XB_MAX_B;  // LeNet: batch-ordered pixel rows conv_fwd -> conv_bwd up to this batch
   m.def("device_count", [] {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -85,7 +86,7 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init<>())
 #define RW(f) .def_readwrite(#f, &TrainerPtrs::f)
       RW(images) RW(labels) RW(idx) RW(step) RW(params) RW(grad) RW(mom) RW(pack) RW(slab_fc) RW(slab_conv)
-      RW(metrics) RW(xT) RW(h1T) RW(h2T) RW(dy1T) RW(dy2T) RW(dy3T) RW(p1) RW(m1) RW(p2) RW(m2) RW(dp2) RW(z1p) RW(stamps) RW(xnext) RW(ynext) RW(xrows);
+      RW(metrics) RW(xT) RW(h1T) RW(h2T) RW(dy1T) RW(dy2T) RW(dy3T) RW(p1) RW(m1) RW(p2) RW(m2) RW(dp2) RW(z1p) RW(stamps) RW(xnext) RW(ynext) RW(xrows) RW(xb);
 #undef RW
 
   py::class_<Bucket>(m, "Bucket")

@@ -67,6 +67,10 @@ struct LenetConvBuffers {
   uint8_t* m2;           // [B][400]
   const void* dp2;       // [B][416] T   (backward input)
   float* slab;           // conv partial grads, row per workgroup: [G][2572]
+  // optional [B][784] u8: this step's pixel rows in batch order, written by conv_fwd_kernel (training) and read
+  // by conv_bwd instead of re-gathering them through the sample index (small batches: the index chain
+  // step counter -> index -> pixels was conv_bwd's start-up latency); null = gather by index
+  uint8_t* xb = nullptr;
   int ablate = 0;        // diagnostics only: bitmask of phases to skip (timing ablation, wrong results)
   unsigned long long* stamps = nullptr;  // optional phase timestamps (profiling): fwd [block][16], bwd [block][16]
 };

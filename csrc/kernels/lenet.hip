@@ -55,9 +55,9 @@ DEV void zero_lds(T* p, int n, int tid = -1, int nth = 0) {
 constexpr int MAX_IPB = 64;
 struct BlockIdx {
   int v;
-  DEV BlockIdx(const int32_t* idx, int first, int count, int B) {
+  DEV BlockIdx(const int32_t* idx, int first, int count, int B) {  // idx null: unused (all zero)
     const int l = threadIdx.x & 63;
-    v = (l < count && first + l < B) ? idx[first + l] : 0;
+    v = (idx && l < count && first + l < B) ? idx[first + l] : 0;
   }
   DEV int operator[](int t) const { return __builtin_amdgcn_readlane(v, t); }
 };
@@ -309,6 +309,13 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
     const int b = first + t;
     const bool valid = b < br.B;
     const Raw u = u_next;
+    // this image's pixel rows in batch order for conv_bwd (cb.xb): columns 8sg .. 8sg+7 of row sy - 2 are the
+    // window's words 1 and 2 (word 2 of sg = 3 is a clamped duplicate)
+    if (TRAIN && !XROWS && cb.xb && valid && tid < 224 && sh == 0) {
+      uint8_t* d = cb.xb + (size_t)b * 784 + (sy - 2) * 28 + 8 * sg;
+      *reinterpret_cast<uint32_t*>(d) = u.d[1];
+      if (sg < 3) *reinterpret_cast<uint32_t*>(d + 4) = u.d[2];
+    }
     // ---- stage: normalise once, 4 aligned 16-byte plane stores per thread
     if (tid < 224 && !ABLATED(cb.ablate, 1)) {
       float f[16];
@@ -984,7 +991,10 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
   float* red = reinterpret_cast<float*>(smem + S::OFF_RED);
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
   const int unit = xcd_unit(blk, nblk, br.xcd);  // images [unit * ipb, +ipb), slab row unit
-  const BlockIdx bidx(br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride, unit * ipb, ipb, br.B);
+  // pixel rows: batch-ordered copy from conv_fwd (cb.xb: no index chain in front of the first image), else
+  // gathered through the sample index
+  const uint8_t* const xb = cb.xb;
+  const BlockIdx bidx(xb ? nullptr : br.idx_epoch + (size_t)br.step_ptr[0] * br.batch_stride, unit * ipb, ipb, br.B);
   const T* pack = reinterpret_cast<const T*>(cb.pack);
   const T* dp2 = reinterpret_cast<const T*>(cb.dp2);
   const T* p1g = reinterpret_cast<const T*>(cb.p1);
@@ -1030,7 +1040,8 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
     const int bb = min(unit * ipb + t, br.B - 1);
     if (R::loads_px(w)) {
       const int xt = min(tid - R::XS_T0, R::XS_N - 1);
-      const uint8_t* rowp = br.images + (size_t)bidx[live ? t : 0] * 784 + ((xt >> 2) % 28) * 28;
+      const uint8_t* rowp = (xb ? xb + (size_t)min(unit * ipb + (live ? t : 0), br.B - 1) * 784
+                                : br.images + (size_t)bidx[live ? t : 0] * 784) + ((xt >> 2) % 28) * 28;
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int col = 8 * (xt & 3) - 4 + 4 * k;
@@ -1088,15 +1099,23 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
   // kh' + r is outside 0..4.  N = (r, c) holds 12 live columns of 16 (was 6 with one row per tile).
   // Row (r, c) is C2D row c shifted by 5 taps: r = 0 -> [80 zeros | C2D[c][0..400)], r = 1 ->
   // [C2D[c][0..400) | 80 zeros]; copied as 16-byte vectors (rows c >= 6 are all zero).
+  // Every thread's loads are issued (branch-free, clamped addresses) before its first LDS store: one memory
+  // round trip for the whole image instead of one per loop trip.
   {
-    constexpr int VE = 16 / (int)sizeof(T), RV = 480 / VE, SH = 80 / VE;
-    for (int e = tid; e < 16 * RV; e += NT) {
-      const int nr = e / RV, v = e % RV, r = nr >> 3, c = nr & 7;
+    constexpr int VE = 16 / (int)sizeof(T), RV = 480 / VE, SH = 80 / VE, NV = 16 * RV, IT = (NV + NT - 1) / NT;
+    u32x4 wv[IT];
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = min(tid + i * NT, NV - 1), nr = e / RV, v = e % RV, r = nr >> 3, c = nr & 7;
       const int src = r == 0 ? v - SH : v;  // source vector within C2D row c
-      uint4 val = make_uint4(0, 0, 0, 0);
-      if (c < 6 && src >= 0 && src < 400 / VE)
-        val = *reinterpret_cast<const uint4*>(pack + L::C2D + c * 416 + src * VE);
-      *reinterpret_cast<uint4*>(w2 + nr * S::W2P + v * VE) = val;
+      wv[i] = *reinterpret_cast<const u32x4*>(pack + L::C2D + min(c, 5) * 416 + min(max(src, 0), 400 / VE - 1) * VE);
+    }
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = tid + i * NT, nr = e / RV, v = e % RV, r = nr >> 3, c = nr & 7;
+      const int src = r == 0 ? v - SH : v;
+      const bool ok = c < 6 && src >= 0 && src < 400 / VE;
+      if (e < NV) *reinterpret_cast<u32x4*>(w2 + nr * S::W2P + v * VE) = ok ? wv[i] : u32x4{0u, 0u, 0u, 0u};
     }
   }
   // ---- static work split of phase B (dgrad row-pair tile = 15 K-chunks, wgrad tile = 5): BwdRoles

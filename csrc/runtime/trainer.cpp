@@ -225,8 +225,13 @@ void Trainer::set_regather(HeadBuffers& hb, const BatchRef& br, bool fused_wgrad
 #endif
 }
 
-LenetConvBuffers Trainer::conv_buffers() const {
+LenetConvBuffers Trainer::conv_buffers(int B) const {
   LenetConvBuffers cb;
+  // a training step of B rows whose forward is conv_fwd_kernel (not the fused forward + head) hands conv_bwd
+  // its pixel rows in batch order (small batches only: there the index chain is conv_bwd's start-up latency)
+#ifndef MNIST_AMD_FWD_HEAD_SMALL
+  if (B > 0 && B <= XB_MAX_B && p_.xb && !fwd_head_active(B)) cb.xb = ptr<uint8_t>(p_.xb);
+#endif
   cb.params = ptr<const float>(p_.params);
   cb.pack = ptr<const void>(p_.pack);
   cb.p1 = ptr<void>(p_.p1);
@@ -254,9 +259,9 @@ void Trainer::forward_backward(int B, uintptr_t stream) {
   set_regather(hb, br, false);
   int hrows = 0;
   if (model_ == ModelKind::LENET) {
-    if (fwd_head_active(B)) hrows = launch_lenet_fwd_head(dtype_, br, conv_buffers(), hb, s);
-    else hrows = launch_lenet_fwd_head_small(dtype_, br, conv_buffers(), hb, group_counter_, s);
-    if (!hrows) launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(), s);
+    if (fwd_head_active(B)) hrows = launch_lenet_fwd_head(dtype_, br, conv_buffers(B), hb, s);
+    else hrows = launch_lenet_fwd_head_small(dtype_, br, conv_buffers(B), hb, group_counter_, s);
+    if (!hrows) launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(B), s);
     post_launch(s);
   }
   if (!hrows) {
@@ -267,7 +272,7 @@ void Trainer::forward_backward(int B, uintptr_t stream) {
   launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s, hrows);
   post_launch(s);
   if (model_ == ModelKind::LENET) {
-    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), nullptr, s, bwd_blocks_);
+    launch_lenet_conv_bwd(dtype_, br, conv_buffers(B), nullptr, s, bwd_blocks_);
     post_launch(s);
   }
 }
@@ -355,11 +360,11 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
   if (model_ == ModelKind::LENET) {
     if (fwd_head_active(B)) {
       join_aux();
-      hrows = launch_lenet_fwd_head(dtype_, br, conv_buffers(), hb, s);
+      hrows = launch_lenet_fwd_head(dtype_, br, conv_buffers(B), hb, s);
     } else {
       join_aux();  // (no-op unless a deferred join is pending: the small fused kernel also contains the head)
-      hrows = launch_lenet_fwd_head_small(dtype_, br, conv_buffers(), hb, group_counter_, s);
-      if (!hrows) launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(), s);
+      hrows = launch_lenet_fwd_head_small(dtype_, br, conv_buffers(B), hb, group_counter_, s);
+      if (!hrows) launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(B), s);
     }
     post_launch(s);
   }
@@ -377,7 +382,7 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     HIP_CHECK(hipEventRecord(events_[4], s));
     HIP_CHECK(hipStreamWaitEvent(aux_stream_, events_[4], 0));
     int nslab = 0;
-    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s, bwd_blocks_);
+    launch_lenet_conv_bwd(dtype_, br, conv_buffers(B), &nslab, s, bwd_blocks_);
     post_launch(s);
     if (comm && plan_ == Plan::OVERLAP) {
       launch_lenet_overlap(B, nslab, s, hb, hrows);
@@ -444,13 +449,13 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
                     momentum_ != 0.f ? ptr<float>(p_.mom) : nullptr, ptr<void>(p_.pack), nullptr};
 #ifndef MNIST_AMD_NO_BWD_FC  // (A/B builds only: the FC wgrad + update as its own kernel before conv_bwd)
     // ... as extra workgroups of the conv_bwd launch (one kernel instead of two)
-    const int nslab = launch_lenet_conv_bwd_fc(dtype_, br, conv_buffers(), hb, f, s, bwd_blocks_);
+    const int nslab = launch_lenet_conv_bwd_fc(dtype_, br, conv_buffers(B), hb, f, s, bwd_blocks_);
     post_launch(s);
 #else
     launch_head_wgrad(model_, dtype_, hb, B, 1, ptr<float>(p_.slab_fc), nparam_, s, hrows, &f);
     post_launch(s);
     int nslab = 0;
-    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s, bwd_blocks_);
+    launch_lenet_conv_bwd(dtype_, br, conv_buffers(B), &nslab, s, bwd_blocks_);
     post_launch(s);
 #endif
     launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
@@ -463,7 +468,7 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
   post_launch(s);
   int nslab = 0;
   if (model_ == ModelKind::LENET) {  // serial single-GPU schedule (MNIST_AMD_CONCURRENT=0)
-    launch_lenet_conv_bwd(dtype_, br, conv_buffers(), &nslab, s, bwd_blocks_);
+    launch_lenet_conv_bwd(dtype_, br, conv_buffers(B), &nslab, s, bwd_blocks_);
     post_launch(s);
   }
   // no communicator: ONE fused reduce + SGD + pack kernel (2 boundaries fewer than reduce -> sgd)

@@ -24,6 +24,7 @@ struct TrainerPtrs {
   uintptr_t z1p = 0;  // optional: enables the small-batch layer-1 split path
   uintptr_t stamps = 0;  // optional: per-block phase timestamps of the head kernel (profiling)
   uintptr_t xnext = 0, ynext = 0;  // optional: small-batch MLP look-ahead gather buffers (BatchRef)
+  uintptr_t xb = 0;     // optional: LeNet [batch][784] uint8 pixel rows in batch order (conv_fwd -> conv_bwd)
   uintptr_t xrows = 0;  // optional: MLP bf16 raw-row hand-off head -> layer-1 wgrad ([batch][784] uint8)
 };
 
@@ -51,6 +52,8 @@ enum class Plan : int { JOIN = 0, SPLIT = 1, OVERLAP = 2 };
 
 class Trainer {
  public:
+  // LeNet training steps of B <= XB_MAX_B rows hand conv_bwd batch-ordered pixel rows (TrainerPtrs::xb)
+  static constexpr int XB_MAX_B = 2048;
   Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const TrainerPtrs& p);
   ~Trainer();
 
@@ -154,7 +157,8 @@ class Trainer {
   // MLP bf16 training: the head hands the batch's raw uint8 rows to the layer-1 weight gradient instead of a
   // bf16 X^T, unless the step's wgrad is the SGD-fused one (no LDS staging) or no row buffer was given
   void set_regather(HeadBuffers& hb, const BatchRef& br, bool fused_wgrad) const;
-  LenetConvBuffers conv_buffers() const;
+  // B > 0: the buffers of a training step of B rows (cb.xb set when conv_fwd_kernel writes batch-ordered rows)
+  LenetConvBuffers conv_buffers(int B = 0) const;
   // defer_join: (single GPU, concurrent schedule, inside a multi-step graph) leave the aux branch (FC
   // wgrad + FC update) un-joined at the end of the step; the NEXT step's head waits for it instead.
   void launch_step(int B, hipStream_t s, bool defer_join = false);

@@ -178,6 +178,10 @@ class NativeTrainer:
         raw = getattr(C, "RAW_ROWS", False) and model == "mlp" and dtype == "bf16"
         self.xrows = z(self.batch, 784, dt=torch.uint8) if raw else None
 
+        # LeNet small batches: conv_fwd's pixel rows in batch order for conv_bwd (no index chain at its start)
+        xbm = getattr(C, "XB_MAX_B", 0)
+        self.xb = z(self.batch, 784, dt=torch.uint8) if model == "lenet5" and self.batch <= xbm else None
+
         P = C.TrainerPtrs()
         ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
         P.images, P.labels, P.idx, P.step = ptr(self.images), ptr(self.labels), ptr(self.idx), ptr(self.step_ctr)
@@ -190,6 +194,8 @@ class NativeTrainer:
         P.xnext, P.ynext = ptr(self.xnext), ptr(self.ynext)
         if hasattr(P, "xrows"):  # (A/B runs load older builds through MNIST_AMD_C_PATH)
             P.xrows = ptr(self.xrows)
+        if hasattr(P, "xb"):
+            P.xb = ptr(self.xb)
         # MNIST_AMD_STAMPS=1: per-workgroup phase timestamps (wall clock, 100 MHz), 16 slots per workgroup,
         # one row range per kernel (csrc/kernels/launch.h STAMP_*; later workgroups skip)
         self.stamps = z(C.STAMP_ROWS * 16, dt=torch.int64) if os.environ.get("MNIST_AMD_STAMPS") else None
