@@ -56,6 +56,7 @@ struct HeadBuffers {
   // layer-1 weight gradient normalises them in registers -- bitwise the operand X^T would have held
   uint8_t* xrows = nullptr;
   int32_t gx_B = 0;      // rows of the batch (rows past it read as zero)
+  const uint8_t* yb = nullptr;  // LeNet head16: this step's labels in batch order (LenetConvBuffers::yb) or null
 };
 
 struct LenetConvBuffers {
@@ -71,6 +72,7 @@ struct LenetConvBuffers {
   // by conv_bwd instead of re-gathering them through the sample index (small batches: the index chain
   // step counter -> index -> pixels was conv_bwd's start-up latency); null = gather by index
   uint8_t* xb = nullptr;
+  uint8_t* yb = nullptr;  // [B] u8: the labels in batch order, written with xb (read by the head16 head)
   int ablate = 0;        // diagnostics only: bitmask of phases to skip (timing ablation, wrong results)
   unsigned long long* stamps = nullptr;  // optional phase timestamps (profiling): fwd [block][16], bwd [block][16]
 };

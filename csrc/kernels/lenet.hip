@@ -149,7 +149,7 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
   // It fetches the dword-aligned 20-byte window [8g-4, 8g+16) of image row y-2 (pixel at padded
   // column 8g+i is window byte i+2), normalises its 16 pixels once, and writes planes 4h..4h+3 as
   // ALIGNED 16-byte stores: xs[s][y][8g..8g+7] = xpad[y][8g+s..8g+s+7].  Rows 0,1,30,31 stay zero.
-  struct Raw { uint32_t d[5]; };
+  struct Raw { uint32_t d[5], lab; };
   const int sy = 2 + (tid >> 3), sg = (tid >> 1) & 3, sh = tid & 1;
   // Branch-free: every lane issues the same 5 loads, addresses clamped into the image; the words are
   // kept raw (selecting on a loaded value right after the load made the wave wait for it).  Words
@@ -161,6 +161,8 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
     const uint8_t* rowp = br.images + (size_t)bidx[live ? t : 0] * 784 + min(sy - 2, 27) * 28;
 #pragma unroll
     for (int k = 0; k < 5; ++k) r.d[k] = *reinterpret_cast<const uint32_t*>(rowp + min(max(8 * sg - 4 + 4 * k, 0), 24));
+    r.lab = 0u;
+    if constexpr (TRAIN && !XROWS) r.lab = br.labels[bidx[live ? t : 0]];  // (batch-ordered labels, cb.yb)
     return r;
   };
   Raw u_next = fetch(0);  // issued before the setup below, so its latency overlaps it
@@ -315,6 +317,7 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
       uint8_t* d = cb.xb + (size_t)b * 784 + (sy - 2) * 28 + 8 * sg;
       *reinterpret_cast<uint32_t*>(d) = u.d[1];
       if (sg < 3) *reinterpret_cast<uint32_t*>(d + 4) = u.d[2];
+      if (tid == 0) cb.yb[b] = (uint8_t)u.lab;
     }
     // ---- stage: normalise once, 4 aligned 16-byte plane stores per thread
     if (tid < 224 && !ABLATED(cb.ablate, 1)) {
@@ -564,8 +567,12 @@ DEV void head16_tile(const BatchRef& br, const HeadBuffers& hb, char* ht, T* sX,
   int lab = 0;
   if (tid >= 512 - 16) {  // labels of the tile (the last wave: its L2 tile is a dummy)
     const int t = tid - (512 - 16), rg = r0 + t;
-    const int id = rg < B ? br.idx_epoch[(size_t)br.step_ptr[0] * br.batch_stride + rg] : -1;
-    lab = id >= 0 ? (int)br.labels[id] : 0;
+    if (hb.yb) {  // batch-ordered labels from conv_fwd_kernel (small batches): no index chain
+      lab = rg < B ? (int)hb.yb[rg] : 0;
+    } else {
+      const int id = rg < B ? br.idx_epoch[(size_t)br.step_ptr[0] * br.batch_stride + rg] : -1;
+      lab = id >= 0 ? (int)br.labels[id] : 0;
+    }
   }
   // sX complete (caller), `ht` free: a raw barrier after the LDS writes drained -- __syncthreads() would also
   // wait (vmcnt(0)) for the weight fragments just issued
@@ -803,10 +810,19 @@ __global__ __launch_bounds__(512) void head16_kernel(BatchRef br, HeadBuffers hb
   const int r0 = xcd_unit(blockIdx.x, gridDim.x, br.xcd) * 16;
   const T* xin = reinterpret_cast<const T*>(hb.xin);
   constexpr int CH = H::K0P * (int)sizeof(T) / 16;  // 16-byte chunks per row (52)
-  for (int e = tid; e < 16 * CH; e += 512) {
-    const int r = e / CH, c = e - CH * r;
-    const uint4 v = r0 + r < br.B ? reinterpret_cast<const uint4*>(xin + (size_t)(r0 + r) * H::K0P)[c] : make_uint4(0, 0, 0, 0);
-    *reinterpret_cast<uint4*>(sX + r * S::PX + c * (16 / (int)sizeof(T))) = v;
+  constexpr int IT = (16 * CH + 511) / 512;
+  // every load issued (branch-free, clamped row) before the first LDS store: one memory round trip
+  u32x4 xv[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int e = min(tid + 512 * i, 16 * CH - 1), r = e / CH, c = e - CH * r;
+    xv[i] = reinterpret_cast<const u32x4*>(xin + (size_t)min(r0 + r, br.B - 1) * H::K0P)[c];
+  }
+#pragma unroll
+  for (int i = 0; i < IT; ++i) {
+    const int e = tid + 512 * i, r = e / CH, c = e - CH * r;
+    if (e < 16 * CH)
+      *reinterpret_cast<u32x4*>(sX + r * S::PX + c * (16 / (int)sizeof(T))) = r0 + r < br.B ? xv[i] : u32x4{0u, 0u, 0u, 0u};
   }
   head16_tile<T>(br, hb, smem + S::X_BYTES, sX, r0, blockIdx.x);  // barriers before reading sX
 }

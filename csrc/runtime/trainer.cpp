@@ -230,7 +230,10 @@ LenetConvBuffers Trainer::conv_buffers(int B) const {
   // a training step of B rows whose forward is conv_fwd_kernel (not the fused forward + head) hands conv_bwd
   // its pixel rows in batch order (small batches only: there the index chain is conv_bwd's start-up latency)
 #ifndef MNIST_AMD_FWD_HEAD_SMALL
-  if (B > 0 && B <= XB_MAX_B && p_.xb && !fwd_head_active(B)) cb.xb = ptr<uint8_t>(p_.xb);
+  if (B > 0 && B <= XB_MAX_B && p_.xb && !fwd_head_active(B)) {
+    cb.xb = ptr<uint8_t>(p_.xb);                          // [batch][784] pixel rows
+    cb.yb = ptr<uint8_t>(p_.xb) + (size_t)batch_ * 784;   // then [batch] labels
+  }
 #endif
   cb.params = ptr<const float>(p_.params);
   cb.pack = ptr<const void>(p_.pack);
@@ -256,6 +259,7 @@ void Trainer::forward_backward(int B, uintptr_t stream) {
   if (B <= 0 || B > batch_) throw std::invalid_argument("forward_backward: bad batch size");
   const BatchRef br = batch_ref(B);
   HeadBuffers hb = head_buffers(ptr<float>(p_.metrics));
+  if (model_ == ModelKind::LENET) hb.yb = conv_buffers(B).yb;  // (small batches: labels from conv_fwd_kernel)
   set_regather(hb, br, false);
   int hrows = 0;
   if (model_ == ModelKind::LENET) {
@@ -341,6 +345,7 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
   if (B <= 0 || B > batch_) throw std::invalid_argument("train_step: bad batch size");
   const BatchRef br = batch_ref(B);
   HeadBuffers hb = head_buffers(ptr<float>(p_.metrics));
+  if (model_ == ModelKind::LENET) hb.yb = conv_buffers(B).yb;  // (small batches: labels from conv_fwd_kernel)
   const float scale = 1.0f / float(B);
   const int cp = model_conv_params(model_);
   const bool comm = use_comm();

@@ -24,7 +24,8 @@ struct TrainerPtrs {
   uintptr_t z1p = 0;  // optional: enables the small-batch layer-1 split path
   uintptr_t stamps = 0;  // optional: per-block phase timestamps of the head kernel (profiling)
   uintptr_t xnext = 0, ynext = 0;  // optional: small-batch MLP look-ahead gather buffers (BatchRef)
-  uintptr_t xb = 0;     // optional: LeNet [batch][784] uint8 pixel rows in batch order (conv_fwd -> conv_bwd)
+  uintptr_t xb = 0;     // optional: LeNet [batch][784] uint8 pixel rows + [batch] labels in batch order (conv_fwd ->
+                        // conv_bwd / head16)
   uintptr_t xrows = 0;  // optional: MLP bf16 raw-row hand-off head -> layer-1 wgrad ([batch][784] uint8)
 };
 

@@ -180,7 +180,7 @@ class NativeTrainer:
 
         # LeNet small batches: conv_fwd's pixel rows in batch order for conv_bwd (no index chain at its start)
         xbm = getattr(C, "XB_MAX_B", 0)
-        self.xb = z(self.batch, 784, dt=torch.uint8) if model == "lenet5" and self.batch <= xbm else None
+        self.xb = z(self.batch * 785, dt=torch.uint8) if model == "lenet5" and self.batch <= xbm else None  # rows | labels
 
         P = C.TrainerPtrs()
         ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
