@@ -160,21 +160,6 @@ def bench_data(world: int, rank: int, batch: int, total_steps: int, mode: str = 
     return torch.from_numpy(images), torch.from_numpy(labels), idx_all, test_x, test_y
 
 
-def attach_overlap_plan(ctx, tr, fc_inst, world: int) -> str:
-    """LeNet: make the one-shot OVERLAP plan available (csrc/runtime/trainer.h Plan::OVERLAP) -- ``fc_inst`` (a
-    validated one-shot instance, >= the FC range) carries the FC range on the aux stream, a second instance,
-    built and validated here, the conv range on the main stream.  Collective; never fatal: returns "" or why
-    the plan is unavailable (agreed by every rank)."""
-    if tr.model_name != "lenet5":
-        return "LeNet-only plan"
-    from pytorch_ddp_mnist_amd.parallel.oneshot import probe_oneshot
-    conv, err = probe_oneshot(ctx, int(tr.rt.conv_params))
-    if conv is None:
-        return err
-    tr.attach_overlap(fc_inst, conv, world)
-    return ""
-
-
 def netcdf_data(ctx, images, labels, data_dir, mode: str):
     """BASELINE config 3 (the PnetCDF loader path): rank 0 writes the run's train split as a CDF-5 file (the
     notebook's to_nc() layout, nb#c2:83-104, through the native writer), every rank then loads it through the
@@ -287,6 +272,7 @@ def main(argv=None) -> int:
         if err:
             raise SystemExit(f"[bench] one-shot all-reduce failed its check: {err}")
         tr.attach_oneshot(oneshot, W)
+        from pytorch_ddp_mnist_amd.parallel.oneshot import attach_overlap_plan
         ov_err = attach_overlap_plan(ctx, tr, oneshot, W)
         if ov_err and pinned == "overlap":
             raise SystemExit(f"[bench] --plan overlap: {ov_err}")
@@ -315,7 +301,7 @@ def main(argv=None) -> int:
         elif W > 1 and os.environ.get("MNIST_AMD_PROBE_ONESHOT", "1") != "0":
             # measure-only: the one-shot all-reduce is built, validated against the exact sum and timed in
             # comm_profile next to RCCL's latency; the step keeps RCCL (never fatal)
-            from pytorch_ddp_mnist_amd.parallel.oneshot import probe_oneshot
+            from pytorch_ddp_mnist_amd.parallel.oneshot import attach_overlap_plan, probe_oneshot
             probe, probe_err = probe_oneshot(ctx, tr.nparam)
             if probe is not None:
                 # the validated instance also carries the OVERLAP plan's FC range (a calibration candidate)

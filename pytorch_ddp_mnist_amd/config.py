@@ -11,7 +11,7 @@ Reference behaviour reproduced here:
     ``LOCAL_RANK`` env var).
 
 Additive flags (survey §5.6): --model, --dtype, --momentum, --lr, --synthetic,
---bucket_cap_kb, --profile, --seed, --no_save, --comm, --no_graph, --plan, --tqdm, --progress_every,
+--bucket_cap_kb, --profile, --seed, --no_save, --comm, --no_graph, --plan, --allreduce, --tqdm, --progress_every,
 --resume, --io_mode.
 """
 from __future__ import annotations
@@ -58,7 +58,8 @@ class TrainConfig:
     local_rank: Optional[int] = None
     shard_eval: bool = False
     progress_every: int = 0     # --tqdm update period in batches (0 = ~20 updates per epoch)
-    plan: str = "auto"          # multi-GPU step plan: "auto" (timed at start-up) | "join" | "split"
+    plan: str = "auto"          # multi-GPU step plan: "auto" (timed at start-up) | "join" | "split" | "overlap"
+    allreduce: str = "rccl"     # gradient data plane with --comm rccl: "rccl" | "oneshot" (parallel/oneshot.py)
     io_mode: str = "bulk"       # netCDF: "bulk" (one pread per variable) | "per_sample" (reference __getitem__
                                 # reads, whole epoch first) | "interleaved" (each batch read before its step)
     resume: Optional[str] = None  # params + momentum + epoch file: loaded if present, rewritten each epoch
@@ -109,8 +110,12 @@ def _add_extra_flags(p: argparse.ArgumentParser, defaults: TrainConfig) -> None:
     add("--tqdm", action="store_true", help="rank-0 progress bars with the batch loss (reference: tqdm per batch)")
     add("--progress_every", type=int, default=None, help="--tqdm update period in batches (one device sync each)")
     add("--shard_eval", action="store_true", help="shard the test set across ranks (reference: every rank evaluates all)")
-    add("--plan", type=str, default=None, choices=["auto", "join", "split", "fixed"],
-        help="step plan (auto: time the candidate schedules at start-up; join/split: multi-GPU plan; fixed: defaults)")
+    add("--plan", type=str, default=None, choices=["auto", "join", "split", "overlap", "fixed"],
+        help="step plan (auto: time the candidate schedules at start-up; join/split: multi-GPU plan; overlap: LeNet, "
+             "one-shot all-reduces inside the backward branches; fixed: defaults)")
+    add("--allreduce", type=str, default=None, choices=["rccl", "oneshot"],
+        help="gradient data plane with --comm rccl: RCCL, or the one-shot all-reduce over IPC-mapped peer slots "
+             "(validated at start-up; RCCL still broadcasts the initial parameters)")
     add("--io_mode", type=str, default=None, choices=["bulk", "per_sample", "interleaved"],
         help="netCDF input: bulk pread (default), or the reference's per-sample __getitem__ reads, timed (MB/s): "
              "per_sample reads the epoch first, interleaved reads each batch beside the training steps")
@@ -121,7 +126,7 @@ def _add_extra_flags(p: argparse.ArgumentParser, defaults: TrainConfig) -> None:
 def _apply_extra(cfg: TrainConfig, a: argparse.Namespace) -> None:
     for name in ("model", "dtype", "lr", "momentum", "dropout", "seed", "init_seed", "data_format",
                  "device", "bucket_cap_kb", "comm", "save_path", "metrics_jsonl", "plan", "resume", "progress_every",
-                 "io_mode"):
+                 "io_mode", "allreduce"):
         v = getattr(a, name, None)
         if v is not None:
             setattr(cfg, name, v)

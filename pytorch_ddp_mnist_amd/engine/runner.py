@@ -52,9 +52,23 @@ class NativeEngine:
         cap = None if cfg.bucket_cap_kb is None else cfg.bucket_cap_kb * 1024
         self.tr.set_buckets(plan_buckets(model_phases(cfg.model), cap))
         self.torch_comm = ctx.world > 1 and ctx.rccl is None
+        self.plan_pinned = cfg.plan != "auto"
+        self.plan_forced = resolve_plan(cfg.plan)  # 'fixed' = no calibration, default join plan
+        if cfg.allreduce == "oneshot" and not (ctx.world > 1 and ctx.rccl is not None):
+            raise SystemExit("--allreduce oneshot needs world > 1 and the native RCCL communicator (--comm rccl)")
+        self.oneshot_note = None
         if ctx.world > 1 and ctx.rccl is not None:
             self.tr.attach_comm(ctx.rccl, ctx.world)
             self.tr.broadcast_params(0)
+            # one-shot data plane (--allreduce oneshot), or a validated measure-only probe that makes the LeNet
+            # OVERLAP plan a calibration candidate (parallel/oneshot.py setup_oneshot; collective)
+            from ..parallel.oneshot import setup_oneshot
+            try:
+                _, _, why = setup_oneshot(ctx, self.tr, ctx.world, cfg.allreduce,
+                                          self.plan_forced if self.plan_pinned else None)
+            except RuntimeError as e:
+                raise SystemExit(f"[rank{ctx.rank}] {e}") from e
+            self.oneshot_note = why or "available"
         elif self.torch_comm:
             # c10d data plane: the all-reduce is enqueued behind the backward on the trainer stream and the
             # SGD kernel that follows on the same stream waits for it (c10d makes the current stream wait);
@@ -67,8 +81,6 @@ class NativeEngine:
             self.tr.attach_external_allreduce(lambda t: dist.all_reduce(t), ctx.world, host=host)
         self.use_graph = cfg.graph and not self.torch_comm
         self.fault = FaultInjector(ctx.rank)
-        self.plan_pinned = cfg.plan != "auto"
-        self.plan_forced = resolve_plan(cfg.plan)  # 'fixed' = no calibration, default join plan
         self.tuned = not self.use_graph  # the calibration times captured steps
         self.tune = None
 

@@ -120,3 +120,45 @@ def probe_oneshot(ctx, max_count: int):
         return None, err or "one-shot bring-up failed on another rank"
     err = validate_oneshot(ctx, o, max_count)
     return (None, err) if err else (o, "")
+
+
+def attach_overlap_plan(ctx, tr, fc_inst, world: int) -> str:
+    """LeNet: make the one-shot OVERLAP plan available (csrc/runtime/trainer.h Plan::OVERLAP) -- ``fc_inst`` (a
+    validated one-shot instance, >= the FC range) carries the FC range on the aux stream, a second instance,
+    built and validated here, the conv range on the main stream.  Collective; never fatal: returns "" or why
+    the plan is unavailable (agreed by every rank)."""
+    if tr.model_name != "lenet5":
+        return "LeNet-only plan"
+    conv, err = probe_oneshot(ctx, int(tr.rt.conv_params))
+    if conv is None:
+        return err
+    tr.attach_overlap(fc_inst, conv, world)
+    return ""
+
+
+def setup_oneshot(ctx, tr, world: int, mode: str, pinned: Optional[str] = None):
+    """The one-shot data plane of a trainer with an RCCL communicator attached (bench.py and the entry-script
+    runner).  ``mode == "oneshot"``: the step's collectives run on a validated one-shot instance (failure is
+    fatal: RuntimeError); ``"rccl"``: at world > 1 a measure-only instance is probed (``MNIST_AMD_PROBE_ONESHOT``,
+    default on) and, when it validates, the OVERLAP plan becomes a calibration candidate.  A pinned ``overlap``
+    plan without it is fatal.  Collective.  Returns (step instance or None, probe instance or None, reason)."""
+    oneshot = probe = None
+    why = ""
+    if mode == "oneshot":
+        oneshot = make_oneshot(ctx, tr.nparam)
+        err = validate_oneshot(ctx, oneshot, tr.nparam)  # exact-sum check, agreed by every rank
+        if err:
+            raise RuntimeError(f"one-shot all-reduce failed its check: {err}")
+        tr.attach_oneshot(oneshot, world)
+        why = attach_overlap_plan(ctx, tr, oneshot, world)
+    elif world > 1 and os.environ.get("MNIST_AMD_PROBE_ONESHOT", "1") != "0":
+        probe, why = probe_oneshot(ctx, tr.nparam)
+        if probe is not None:
+            why = attach_overlap_plan(ctx, tr, probe, world)
+            why = f"overlap plan unavailable: {why}" if why else ""
+    else:
+        why = "not probed"
+    if pinned == "overlap" and why:
+        raise RuntimeError(f"--plan overlap: {why}")
+    return oneshot, probe, why
+

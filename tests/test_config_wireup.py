@@ -47,6 +47,15 @@ def test_additive_flags():
     assert not cfg.graph and cfg.save_path is None and cfg.bucket_cap_kb == 64 and cfg.data_format == "synthetic"
 
 
+def test_allreduce_and_overlap_plan_flags():
+    from pytorch_ddp_mnist_amd.engine.native import resolve_plan
+    cfg = C.configure(["--allreduce", "oneshot", "--plan", "overlap"])
+    assert cfg.allreduce == "oneshot" and cfg.plan == "overlap" and resolve_plan(cfg.plan) == "overlap"
+    assert C.configure([]).allreduce == "rccl"
+    with pytest.raises(SystemExit):
+        C.configure(["--allreduce", "nccl"])
+
+
 # ------------------------------------------------------------------------------------ wire-up
 def test_slurm_full_env():
     env = {"SLURM_LAUNCH_NODE_IPADDR": "10.0.0.7", "SLURM_SRUN_COMM_PORT": "4242", "SLURM_NTASKS": "8",
