@@ -843,11 +843,7 @@ __global__ __launch_bounds__(512) void head16_kernel(BatchRef br, HeadBuffers hb
 // 1 / 2 / 4 images per half 27.2 / 28.7 / 33.1 us.  The hand-off chain (sc1 stores drained, the add's round trip,
 // sc1 loads of the rows) costs what the kernel boundary cost, and the conv part loses the 128-workgroup spread.
 constexpr int FHS_MAX_B = 2048;
-#ifndef MNIST_AMD_FHS_IPH
-#define MNIST_AMD_FHS_IPH 1  // images per 4-wave half (rows per workgroup = 2 * IPH; 16 / (2 * IPH) per group)
-#endif
-constexpr int FHS_IPH = MNIST_AMD_FHS_IPH;
-static_assert(FHS_IPH == 1 || FHS_IPH == 2 || FHS_IPH == 4, "FHS_IPH: 1, 2 or 4");
+constexpr int FHS_IPH = 1;  // images per 4-wave half (measured: 2 / 4 per half slower still, 28.7 / 33.1 us)
 template <typename T>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void fwd_head_small_kernel(
     BatchRef br, LenetConvBuffers cb, HeadBuffers hb, int* counters) {
