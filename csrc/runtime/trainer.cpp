@@ -367,8 +367,10 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
       join_aux();
       hrows = launch_lenet_fwd_head(dtype_, br, conv_buffers(B), hb, s);
     } else {
-      join_aux();  // (no-op unless a deferred join is pending: the small fused kernel also contains the head)
+#ifdef MNIST_AMD_FWD_HEAD_SMALL
+      join_aux();  // the opt-in small fused kernel also contains the head
       hrows = launch_lenet_fwd_head_small(dtype_, br, conv_buffers(B), hb, group_counter_, s);
+#endif
       if (!hrows) launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(B), s);
     }
     post_launch(s);
