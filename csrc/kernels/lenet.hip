@@ -121,9 +121,15 @@ DEV void copy_out16(void* dst, const void* src, int bytes, int tid, int nth) {
 // per workgroup; fwd_head_kernel runs two (one per 4-wave half) and then the FC head on their rows.
 // XROWS (fwd_head_kernel): pool2 of image t goes to row xrow0 + t of the head's LDS input tile `xrows`
 // (row pitch XPITCH, zero for images past the batch) instead of global memory.
-template <typename T, bool TRAIN, bool XROWS = false, int XPITCH = 0>
+// NW = 8 (fp32 conv_fwd_kernel): the same image stream on 8 waves -- waves 4-7 take conv1's tiles 4..6 and
+// conv2's M-tiles one per wave -- so the fp32 matrix pipe has 4 waves per SIMD to switch between (two
+// 512-thread workgroups per CU at the same LDS footprint)
+template <typename T, bool TRAIN, bool XROWS = false, int XPITCH = 0, int NW = 4>
 DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int first, int ipb, char* smem, int tid,
                          int w, bool stamper, T* xrows) {
+  static_assert(NW == 4 || NW == 8, "conv_fwd_images: 4 or 8 waves");
+  constexpr int NT = NW * 64;
+  const int wc = w & 3, hh = NW == 8 ? (w >> 2) : 0;  // column group of conv1's tiles, tile half (8 waves)
   using M = Mma<T>;
   using Frag = typename M::Frag;
   using S = FwdSmem<T>;
@@ -158,11 +164,15 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
   auto fetch = [&](int t) -> Raw {  // software pipeline: image t+1's bytes are in flight during image t
     Raw r;
     const bool live = t < ipb && first + t < br.B;  // wave-uniform
-    const uint8_t* rowp = br.images + (size_t)bidx[live ? t : 0] * 784 + min(sy - 2, 27) * 28;
 #pragma unroll
-    for (int k = 0; k < 5; ++k) r.d[k] = *reinterpret_cast<const uint32_t*>(rowp + min(max(8 * sg - 4 + 4 * k, 0), 24));
+    for (int k = 0; k < 5; ++k) r.d[k] = 0u;
     r.lab = 0u;
-    if constexpr (TRAIN && !XROWS) r.lab = br.labels[bidx[live ? t : 0]];  // (batch-ordered labels, cb.yb)
+    if (NW == 4 || w < 4) {  // (8 waves: the staging threads are waves 0-3; wave-uniform)
+      const uint8_t* rowp = br.images + (size_t)bidx[live ? t : 0] * 784 + min(sy - 2, 27) * 28;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) r.d[k] = *reinterpret_cast<const uint32_t*>(rowp + min(max(8 * sg - 4 + 4 * k, 0), 24));
+      if constexpr (TRAIN && !XROWS) r.lab = br.labels[bidx[live ? t : 0]];  // (batch-ordered labels, cb.yb)
+    }
     return r;
   };
   Raw u_next = fetch(0);  // issued before the setup below, so its latency overlaps it
@@ -187,7 +197,7 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
   Frag b2r[S::W2LDS ? 1 : C2CH];
   if constexpr (S::W2LDS) {
     constexpr int VE = 16 / (int)sizeof(T);
-    for (int e = tid; e < 16 * 224 / VE; e += 256) {
+    for (int e = tid; e < 16 * 224 / VE; e += NT) {
       const int r = e / (224 / VE), c = (e % (224 / VE)) * VE;
       *reinterpret_cast<uint4*>(w2s + r * S::W2P + c) = *reinterpret_cast<const uint4*>(pack + L::C2F + r * 224 + c);
     }
@@ -210,19 +220,19 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
     for (int kc = 0; kc < C1CH; ++kc) {
       const int k0 = kc * KC + grp * KV;
       const int khp = k0 >> 3, xx = xt + (k0 & 7);
-      c1base[kc] = (xx & 7) * S::XP + ((e >> 1) + khp) * 32 + 8 * w + (xx & ~7);
+      c1base[kc] = (xx & 7) * S::XP + ((e >> 1) + khp) * 32 + 8 * wc + (xx & ~7);
     }
   }
-  const bool c1valid = 4 * w + grp < 14;  // wave 3, lane groups 2-3: padding columns 14, 15
+  const bool c1valid = 4 * wc + grp < 14;  // column group 3, lane groups 2-3: padding columns 14, 15
   // Branch-free epilogues: a lane without an output (padding column / channel) stores into the junk area.  Each
   // store address is a per-lane base (real or junk, chosen ONCE) plus a per-tile immediate offset, so the 7
   // tiles' stores need 3 address registers, not 21, and no exec-masked branch breaks the lgkmcnt counting.
   char* junk = smem + S::OFF_JUNK + (int)sizeof(T) * lane;
   const int n1 = row & 7;
   const bool st1 = c1valid && n1 < 6;
-  T* const e1_p1s = c1valid ? p1s + ((row >> 3) * 14 + 4 * w + grp) * 8 + n1 : reinterpret_cast<T*>(junk);
-  T* const e1_p1c = st1 ? p1c + n1 * P1CP + (row >> 3) * 16 + 4 * w + grp : reinterpret_cast<T*>(junk);
-  uint8_t* const e1_m1s = st1 ? m1s + n1 * M1CP + (row >> 3) * 16 + 4 * w + grp : reinterpret_cast<uint8_t*>(junk);
+  T* const e1_p1s = c1valid ? p1s + ((row >> 3) * 14 + 4 * wc + grp) * 8 + n1 : reinterpret_cast<T*>(junk);
+  T* const e1_p1c = st1 ? p1c + n1 * P1CP + (row >> 3) * 16 + 4 * wc + grp : reinterpret_cast<T*>(junk);
+  uint8_t* const e1_m1s = st1 ? m1s + n1 * M1CP + (row >> 3) * 16 + 4 * wc + grp : reinterpret_cast<uint8_t*>(junk);
   auto c1_epi = [&](int t, const f32x4& acc) {  // pool + bias + ReLU, staged in LDS (pooled row 2t + r)
     float mx = acc[0];
     int am = 0;
@@ -292,15 +302,15 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
   };
   auto flush_p2 = [&](int bprev) {  // previous image's pool2 outputs -> HBM (16-byte stores)
     if (bprev >= 0 && bprev < br.B) {
-      if constexpr (!XROWS) copy_out16(reinterpret_cast<T*>(cb.p2) + (size_t)bprev * K0P, p2s, 400 * (int)sizeof(T), tid, 256);
-      if (TRAIN) copy_out16(cb.m2 + (size_t)bprev * 400, m2s, 400, tid, 256);
+      if constexpr (!XROWS) copy_out16(reinterpret_cast<T*>(cb.p2) + (size_t)bprev * K0P, p2s, 400 * (int)sizeof(T), tid, NT);
+      if (TRAIN) copy_out16(cb.m2 + (size_t)bprev * 400, m2s, 400, tid, NT);
     }
   };
 
-  zero_lds<T>(xs, 8 * S::XP + S::XTAIL, tid, 256);
+  zero_lds<T>(xs, 8 * S::XP + S::XTAIL, tid, NT);
   if (TRAIN) {
-    zero_lds<T>(p1c, P1IMG, tid, 256);
-    zero_lds<uint8_t>(m1s, M1IMG, tid, 256);
+    zero_lds<T>(p1c, P1IMG, tid, NT);
+    zero_lds<uint8_t>(m1s, M1IMG, tid, NT);
   }
   // b1 / b2r / biases are loop-invariant registers loaded from global memory above (image 0's pixels
   // are also in flight and consumed right after this barrier anyway)
@@ -388,37 +398,55 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
       // (rows kh' = 0..3) IS tile t's second half (kh' = 4..7): c1base[kc + C1CH/2] = c1base[kc] + 128.
       // Only the second half is read per tile (8 instead of 14 A reads per wave and image, bf16).
       constexpr int HC = C1CH / 2;
-      Frag fa[C1CH];
+      // tiles [T0, T1) of this wave's column group (4 waves: all 7; 8 waves: 0..3 / 4..6 by tile half)
+      auto conv1_tiles = [&](auto t0c, auto t1c) {
+        constexpr int T0 = decltype(t0c)::value, T1 = decltype(t1c)::value;
+        Frag fa[C1CH];
 #pragma unroll
-      for (int kc = 0; kc < C1CH; ++kc) fa[kc] = M::load(xs + c1base[kc]);
-      f32x4 prev = zero4();
+        for (int kc = 0; kc < C1CH; ++kc) fa[kc] = M::load(xs + c1base[kc] + T0 * 128);
+        f32x4 prev = zero4();
 #pragma unroll
-      for (int t = 0; t < 7; ++t) {
-        f32x4 acc = zero4();
+        for (int t = T0; t < T1; ++t) {
+          f32x4 acc = zero4();
 #pragma unroll
-        for (int kc = 0; kc < C1CH; ++kc) M::mma(acc, fa[kc], b1[kc]);
-        if (t + 1 < 7) {
+          for (int kc = 0; kc < C1CH; ++kc) M::mma(acc, fa[kc], b1[kc]);
+          if (t + 1 < T1) {
 #pragma unroll
-          for (int kc = 0; kc < HC; ++kc) fa[kc] = fa[kc + HC];
+            for (int kc = 0; kc < HC; ++kc) fa[kc] = fa[kc + HC];
 #pragma unroll
-          for (int kc = HC; kc < C1CH; ++kc) fa[kc] = M::load(xs + c1base[kc] + (t + 1) * 128);
+            for (int kc = HC; kc < C1CH; ++kc) fa[kc] = M::load(xs + c1base[kc] + (t + 1) * 128);
+          }
+          if (t > T0) c1_epi(t - 1, prev);
+          prev = acc;
         }
-        if (t > 0) c1_epi(t - 1, prev);
-        prev = acc;
+        c1_epi(T1 - 1, prev);
+      };
+      if constexpr (NW == 4) {
+        conv1_tiles(std::integral_constant<int, 0>{}, std::integral_constant<int, 7>{});
+      } else if (hh == 0) {  // (wave-uniform)
+        conv1_tiles(std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
+      } else {
+        conv1_tiles(std::integral_constant<int, 4>{}, std::integral_constant<int, 7>{});
       }
-      c1_epi(6, prev);
     }
     __syncthreads();
     if (t < 4) stamp(3 + 3 * t);
 
     // ---- pool1 -> HBM for the backward pass (16-byte stores), overlapped with conv2
     if (TRAIN && valid && !ABLATED(cb.ablate, 1024)) {
-      copy_out16<true>(reinterpret_cast<T*>(cb.p1) + (size_t)b * P1IMG, p1c, P1IMG * (int)sizeof(T), tid, 256);
-      copy_out16<true>(cb.m1 + (size_t)b * M1IMG, m1s, M1IMG, tid, 256);
+      copy_out16<true>(reinterpret_cast<T*>(cb.p1) + (size_t)b * P1IMG, p1c, P1IMG * (int)sizeof(T), tid, NT);
+      copy_out16<true>(cb.m1 + (size_t)b * M1IMG, m1s, M1IMG, tid, NT);
     }
     // ---- conv2 + bias + ReLU + maxpool: 100 rows (25 pooled x 4) = 7 M-tiles, N = 16
     if (!ABLATED(cb.ablate, 4)) {
-      if (w < 3) {  // waves 0-2: tiles (2w, 2w+1) as a pair; wave 3: tile 6
+      if constexpr (NW == 8) {  // one M-tile per wave (wave 7: none)
+        if (w < 7) {
+          const int mts[1] = {w};
+          f32x4 acc[1] = {zero4()};
+          c2_acc(std::integral_constant<int, 1>{}, mts, acc);
+          c2_epi(t, valid, w, acc[0]);
+        }
+      } else if (w < 3) {  // waves 0-2: tiles (2w, 2w+1) as a pair; wave 3: tile 6
         const int mts[2] = {2 * w, 2 * w + 1};
         f32x4 acc[2] = {zero4(), zero4()};
         c2_acc(std::integral_constant<int, 2>{}, mts, acc);
@@ -439,12 +467,13 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
   flush_p2(first + ipb - 1);
 }
 
-template <typename T, bool TRAIN>
-// (f32: its ~64 KB of LDS allows 2 workgroups per CU anyway, so it may use up to 256 VGPRs instead of spilling)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 2 ? 4 : 2))) void conv_fwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
+template <typename T, bool TRAIN, int NW = 4>
+// (f32, 4 waves: its ~64 KB of LDS allows 2 workgroups per CU anyway, so it may use up to 256 VGPRs instead of
+//  spilling; 8 waves: 2 x 8 waves per CU, 128 VGPRs)
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 2 || NW == 8 ? 4 : 2))) void conv_fwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
   __shared__ __attribute__((aligned(16))) char smem[FwdSmem<T>::TOTAL];
   const int unit = xcd_unit(blockIdx.x, gridDim.x, br.xcd);  // this workgroup's images: [unit * ipb, +ipb)
-  conv_fwd_images<T, TRAIN>(br, cb, unit * ipb, ipb, smem, threadIdx.x, wave_id(), threadIdx.x == 0, nullptr);
+  conv_fwd_images<T, TRAIN, false, 0, NW>(br, cb, unit * ipb, ipb, smem, threadIdx.x, wave_id(), threadIdx.x == 0, nullptr);
 }
 
 // ====================================================================================
@@ -1561,8 +1590,11 @@ int lenet_conv_bwd_max_blocks(int B, int target) {
 void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetConvBuffers& cb, hipStream_t s) {
   if (br.B <= 0) return;
   const int ipb = fwd_ipb(br.B), grid = (br.B + ipb - 1) / ipb;
+  // fp32 training conv_fwd on 8 waves: LeNet fp32 B=8192 0.4331-0.4339 vs 0.4380-0.4392 ms with 4, B=128 47.0 vs
+  // 47.9 us, bitwise-equal parameters (profiles/r4_session2/ab_conv_fwd_f32_8waves.txt)
+  constexpr int FNW = 8;
   if (t == DType::F32) {
-    if (train) hipLaunchKernelGGL((conv_fwd_kernel<float, true>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
+    if (train) hipLaunchKernelGGL((conv_fwd_kernel<float, true, FNW>), dim3(grid), dim3(FNW * 64), 0, s, br, cb, ipb);
     else hipLaunchKernelGGL((conv_fwd_kernel<float, false>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
   } else {
     if (train) hipLaunchKernelGGL((conv_fwd_kernel<bf16, true>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
