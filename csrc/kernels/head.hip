@@ -1387,9 +1387,10 @@ void head_launch_split(bool train, const BatchRef& br, const HeadBuffers& hb, hi
 // returns the batch rows per workgroup actually used (the wgrad kernel's XCD-aware mapping needs it)
 template <typename T, class H>
 int head_launch_t(bool train, const BatchRef& br, const HeadBuffers& hb, int rows, hipStream_t s) {
-  // the split layer 1 pays for its extra launch only on the 784-deep MLP layer; LeNet's 400-deep layer 1
-  // runs inside the head (B=128: 38.2 vs 39.9 us per step with the split)
-  constexpr bool split_l1 = H::K0 >= 512;
+  // the split layer 1 pays for its extra launch on the 784-deep MLP layer and, for fp32 (matrix rate 1/8 of
+  // bf16: the 16-row head is matrix-bound on its 8 CUs), on LeNet's 400-deep one: LeNet fp32 B=128 46.9 -> 44.4 us,
+  // B=1024 122.3 -> 112.8 us (profiles/r4_session2/ab_lenet_f32_l1_split.txt); LeNet bf16 keeps layer 1 in the head
+  constexpr bool split_l1 = H::K0 >= 512 || sizeof(T) == 4;
   if (hb.z1p && br.B <= L1_SPLIT_MAX_B && split_l1) {
     // (l1_split_kernel, not the head, reads the pixels there: it writes X^T, never the raw rows)
     if (train && hb.xrows) throw std::logic_error("head: the raw-row hand-off needs the head's own gather");
