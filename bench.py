@@ -93,6 +93,8 @@ def parse(argv=None):
                     help="every rank prints a sha256 of its final parameters to stderr (replica consistency check)")
     ap.add_argument("--dump-params", default=None,
                     help="every rank saves its final parameter slab to PATH.rank<r>.pt (tests)")
+    ap.add_argument("--rank-logs", default=None,
+                    help="--gpus N self-launch: also write each rank's stderr to DIR/rank<r>.stderr")
     ap.add_argument("--dry-run", action="store_true",
                     help="check the launch wiring only: every rank validates its env, rank 0 prints a JSON line, no GPU")
     return ap.parse_args(argv)
@@ -111,7 +113,11 @@ def spawn_ranks(a) -> int:
     """``--gpus N`` without a launcher: start N rank processes and relay rank 0's JSON line."""
     L = _launcher()
     cmd = [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
-    rc, lines = L.launch_relay(cmd, a.gpus, style="torch", relay_rank=0)
+    # crash evidence of every rank: the native backtrace of a host fault (MNIST_AMD_SEGV_TRACE), then the
+    # Python stacks of every thread (faulthandler); the launcher keeps each rank's stderr separately
+    env = {k: os.environ.get(k, "1") for k in ("MNIST_AMD_SEGV_TRACE", "PYTHONFAULTHANDLER")}
+    rc, lines = L.launch_relay(cmd, a.gpus, style="torch", relay_rank=0, extra_env=env, log_dir=a.rank_logs,
+                               timeout=float(os.environ.get("MNIST_AMD_LAUNCH_TIMEOUT", "0")))
     if rc == 0 and not any(l.lstrip().startswith("{") for l in lines):
         print("[bench] rank 0 printed no result line", file=sys.stderr)
         return 1
@@ -262,20 +268,9 @@ def main(argv=None) -> int:
     tr.set_epoch_indices(idx_all)
     comm, rccl_version, tune, prof = None, None, None, None
     oneshot, probe, probe_err = None, None, None
+    if a.allreduce == "oneshot" and a.comm == "torch":
+        raise SystemExit("--allreduce oneshot needs --comm rccl (RCCL kept for broadcast / comparison) or gloo")
     external = a.comm in ("torch", "gloo") and W > 1 and a.allreduce != "oneshot"
-    if a.allreduce == "oneshot":
-        if a.comm == "torch":
-            raise SystemExit("--allreduce oneshot needs --comm rccl (RCCL kept for broadcast / comparison) or gloo")
-        from pytorch_ddp_mnist_amd.parallel.oneshot import make_oneshot, validate_oneshot
-        oneshot = make_oneshot(ctx, tr.nparam)
-        err = validate_oneshot(ctx, oneshot, tr.nparam)  # exact-sum check, agreed by every rank
-        if err:
-            raise SystemExit(f"[bench] one-shot all-reduce failed its check: {err}")
-        tr.attach_oneshot(oneshot, W)
-        from pytorch_ddp_mnist_amd.parallel.oneshot import attach_overlap_plan
-        ov_err = attach_overlap_plan(ctx, tr, oneshot, W)
-        if ov_err and pinned == "overlap":
-            raise SystemExit(f"[bench] --plan overlap: {ov_err}")
     if external:
         import torch.distributed as dist
         if a.comm == "gloo":
@@ -296,25 +291,19 @@ def main(argv=None) -> int:
                 comm = C.RcclComm(bytes(C.RcclComm.make_unique_id()), 0, 1, ctx.local_rank)
         rccl_version = C.rccl_version()
         tr.attach_comm(comm, W)
-        if oneshot is not None:
-            tr.attach_oneshot(oneshot, W)  # the step's collectives; RCCL broadcasts and is timed for comparison
-        elif W > 1 and os.environ.get("MNIST_AMD_PROBE_ONESHOT", "1") != "0":
-            # measure-only: the one-shot all-reduce is built, validated against the exact sum and timed in
-            # comm_profile next to RCCL's latency; the step keeps RCCL (never fatal)
-            from pytorch_ddp_mnist_amd.parallel.oneshot import attach_overlap_plan, probe_oneshot
-            probe, probe_err = probe_oneshot(ctx, tr.nparam)
-            if probe is not None:
-                # the validated instance also carries the OVERLAP plan's FC range (a calibration candidate)
-                ov_err = attach_overlap_plan(ctx, tr, probe, W)
-                if ov_err:
-                    probe_err = f"overlap plan unavailable: {ov_err}"
-        tr.broadcast_params(0)
-        if pinned is not None:
-            tr.set_plan(pinned)
     elif a.comm_world1:
         raise SystemExit("--comm-world1 needs --comm rccl")
-    elif oneshot is not None:
-        tr.broadcast_params(0)  # over the c10d control plane
+    if not external and (a.allreduce == "oneshot" or comm is not None):
+        # the one-shot data plane, exactly as the entry scripts set it up (parallel/oneshot.py setup_oneshot):
+        # --allreduce oneshot = the step's collectives (validated against the exact sum; RCCL, when attached,
+        # broadcasts and is timed for comparison); with RCCL at world > 1 an opt-in measure-only probe
+        from pytorch_ddp_mnist_amd.parallel.oneshot import setup_oneshot
+        try:
+            oneshot, probe, probe_err = setup_oneshot(ctx, tr, W, a.allreduce, pinned)
+        except RuntimeError as e:
+            raise SystemExit(f"[bench] {e}")
+    if comm is not None or oneshot is not None:
+        tr.broadcast_params(0)  # over RCCL, or over the c10d control plane with only the one-shot plane
         if pinned is not None:
             tr.set_plan(pinned)
 
@@ -330,8 +319,8 @@ def main(argv=None) -> int:
         tune = {"chosen": "eager-phases", "timings_ms": {}, "note": "external data plane: no graph schedules"}
     if (comm is not None or oneshot is not None) and use_graph:
         prof = tr.comm_profile(reduce_max=ctx.all_reduce_max, tune=tune, probe=probe)
-        if probe is not None or probe_err:
-            prof["oneshot_probe"] = "validated (measure-only)" if probe is not None else f"unavailable: {probe_err}"
+        if oneshot is None and W > 1:
+            prof["oneshot_probe"] = "validated (measure-only)" if probe is not None else (probe_err or "not probed")
 
     def run(n):
         tr.run_steps(n, use_graph=use_graph)  # k-step graphs (MNIST_AMD_GRAPH_STEPS), then single steps

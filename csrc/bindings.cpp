@@ -6,6 +6,7 @@
 #include <signal.h>
 #include <unistd.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <stdexcept>
 #include <pybind11/stl.h>
@@ -18,22 +19,50 @@
 namespace py = pybind11;
 
 namespace {
-// MNIST_AMD_SEGV_TRACE=1: print the native backtrace of a host segfault (faulthandler shows only
-// Python frames), then re-raise with the default action.
-void segv_trace(int sig) {
+// MNIST_AMD_SEGV_TRACE=1: print the native backtrace of a host SIGSEGV / SIGBUS / SIGILL / SIGFPE (faulthandler
+// shows only Python frames), then hand the signal to the handler installed before ours -- Python's faulthandler
+// (PYTHONFAULTHANDLER=1, set for bench.py's rank processes) prints every thread's Python stack and re-raises --
+// or, without one, re-raise it with the default action (core / exit status 128 + sig).
+constexpr int kTraced[] = {SIGSEGV, SIGBUS, SIGILL, SIGFPE};
+struct sigaction g_prev[sizeof(kTraced) / sizeof(kTraced[0])];
+
+void segv_trace(int sig, siginfo_t* info, void* uctx) {
   void* frames[64];
   const int n = backtrace(frames, 64);
-  const char msg[] = "\n[mnist_amd] native backtrace:\n";
-  (void)!write(2, msg, sizeof(msg) - 1);
+  char msg[128];
+  const int len = snprintf(msg, sizeof(msg), "\n[mnist_amd] signal %d at address %p, native backtrace:\n", sig,
+                           info ? info->si_addr : nullptr);
+  (void)!write(2, msg, len > 0 ? (size_t)len : 0);
   backtrace_symbols_fd(frames, n, 2);
+  for (size_t i = 0; i < sizeof(kTraced) / sizeof(kTraced[0]); ++i) {
+    if (kTraced[i] != sig) continue;
+    const struct sigaction& p = g_prev[i];
+    sigaction(sig, &p, nullptr);  // the previous disposition, for the re-raise below as well
+    if (p.sa_flags & SA_SIGINFO) {
+      if (p.sa_sigaction) { p.sa_sigaction(sig, info, uctx); return; }
+    } else if (p.sa_handler != SIG_DFL && p.sa_handler != SIG_IGN && p.sa_handler) {
+      p.sa_handler(sig);
+      return;
+    }
+  }
   signal(sig, SIG_DFL);
   raise(sig);
+}
+
+void install_segv_trace() {
+  for (size_t i = 0; i < sizeof(kTraced) / sizeof(kTraced[0]); ++i) {
+    struct sigaction sa {};
+    sa.sa_sigaction = segv_trace;
+    sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+    sigemptyset(&sa.sa_mask);
+    sigaction(kTraced[i], &sa, &g_prev[i]);
+  }
 }
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "MI355X (gfx950) native kernels, step runtime and RCCL communicator";
-  if (const char* e = std::getenv("MNIST_AMD_SEGV_TRACE"); e && *e == '1') signal(SIGSEGV, segv_trace);
+  if (const char* e = std::getenv("MNIST_AMD_SEGV_TRACE"); e && *e == '1') install_segv_trace();
 
   m.def("model_nparam", [](int model) { return model_nparam(static_cast<ModelKind>(model)); });
   m.def("model_conv_params", [](int model) { return model_conv_params(static_cast<ModelKind>(model)); });
@@ -166,7 +195,7 @@ PYBIND11_MODULE(_C, m) {
 
   py::class_<OneShotAllReduce, std::shared_ptr<OneShotAllReduce>>(m, "OneShotAllReduce")
       .def(py::init<int, int, int, int, int, double>(), py::arg("rank"), py::arg("world"), py::arg("device"),
-           py::arg("max_count"), py::arg("nblk") = 64, py::arg("timeout") = 30.0)
+           py::arg("max_count"), py::arg("nblk") = 64, py::arg("timeout") = 5.0)
       .def("handle", [](const OneShotAllReduce& o) { return py::bytes(o.handle()); })
       .def("open_peers",
            [](OneShotAllReduce& o, const std::vector<py::bytes>& hs) {
@@ -179,6 +208,10 @@ PYBIND11_MODULE(_C, m) {
              o.all_reduce_sum_f32(reinterpret_cast<float*>(buf), n, reinterpret_cast<hipStream_t>(s));
            })
       .def("check", &OneShotAllReduce::check)
+      .def("clear_error", &OneShotAllReduce::clear_error)
+      .def("enable_stamps", &OneShotAllReduce::enable_stamps)
+      .def("stamps", &OneShotAllReduce::stamps)
+      .def_property_readonly("calls", &OneShotAllReduce::calls)
       .def_property_readonly("rank", &OneShotAllReduce::rank)
       .def_property_readonly("world", &OneShotAllReduce::world)
       .def_property_readonly("max_count", &OneShotAllReduce::max_count)

@@ -165,19 +165,22 @@ int lenet_conv_bwd_max_blocks(int B, int target_blocks = 0);  // slab rows neede
 // `count` floats at buf; peer_data / peer_flags are device tables of every rank's receive region.
 void launch_oneshot_allreduce(float* buf, int count, int rank, int world, int max_count, float* const* peer_data,
                               uint32_t* const* peer_flags, uint32_t* seq, uint32_t* err, int nblk,
-                              unsigned long long timeout_ticks, hipStream_t s);
+                              unsigned long long timeout_ticks, hipStream_t s, unsigned long long* stamps = nullptr);
 
 // grad[p] = scale * sum_s slab[s][p]  for p in [p0, p1)
 void launch_reduce(const float* slab, int slab_ld, int nslab, int p0, int p1, float scale, float* grad,
                    hipStream_t s);
 
 // SGD (+momentum) on the flat fp32 slab, then re-pack operands; optionally bumps the step counter.
+// `skip`: optional device word (a one-shot all-reduce's latched error, oneshot.hip): when it reads non-zero the
+// parameters and momentum are left as they are (the gradient may hold a partial sum); the step counter still moves.
 void launch_sgd_pack(ModelKind m, DType t, float* params, const float* grad, float* mom, void* pack,
                      int nparam, float lr, float momentum, float gscale, int32_t* step_ptr,
-                     hipStream_t s);
+                     hipStream_t s, const uint32_t* skip = nullptr);
 // Same, over the parameter range [p0, p1) only (per-bucket updates of the split multi-GPU plan).
 void launch_sgd_pack_range(ModelKind m, DType t, float* params, const float* grad, float* mom, void* pack, int p0,
-                           int p1, float lr, float momentum, float gscale, int32_t* step_ptr, hipStream_t s);
+                           int p1, float lr, float momentum, float gscale, int32_t* step_ptr, hipStream_t s,
+                           const uint32_t* skip = nullptr);
 void launch_pack(ModelKind m, DType t, const float* params, void* pack, int nparam, hipStream_t s);
 // Bounded device busy-wait (watchdog tests).
 void launch_spin(double seconds, hipStream_t s);

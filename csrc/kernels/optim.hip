@@ -101,10 +101,12 @@ template <class Model, typename T>
 __global__ __launch_bounds__(256) void sgd_pack_kernel(float* __restrict__ params, const float* __restrict__ grad,
                                                        float* __restrict__ mom, T* __restrict__ pack, int p0, int n,
                                                        float lr, float mu, float gscale, int32_t* step_ptr,
-                                                       int update) {
+                                                       int update, const uint32_t* skip) {
+  // a latched collective failure (skip != 0): keep the parameters, re-pack them unchanged
+  const bool upd = update && !(skip && __hip_atomic_load(const_cast<uint32_t*>(skip), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   for (int p = p0 + blockIdx.x * blockDim.x + threadIdx.x; p < n; p += gridDim.x * blockDim.x) {
     float v = params[p];
-    if (update) {
+    if (upd) {
       float g = grad[p] * gscale;
       if (mom) {
         const float b = mu * mom[p] + g;
@@ -220,10 +222,10 @@ void reduce_sgd_t(const float* sa, int lda, int na, const float* sb, int ldb, in
 
 template <class Model, typename T>
 void sgd_launch(float* params, const float* grad, float* mom, void* pack, int p0, int n, float lr, float mu,
-                float gscale, int32_t* step_ptr, int update, hipStream_t s) {
+                float gscale, int32_t* step_ptr, int update, hipStream_t s, const uint32_t* skip = nullptr) {
   const int grid = std::max(1, std::min(1024, (n - p0 + 255) / 256));
   hipLaunchKernelGGL((sgd_pack_kernel<Model, T>), dim3(grid), dim3(256), 0, s, params, grad, mom,
-                     reinterpret_cast<T*>(pack), p0, n, lr, mu, gscale, step_ptr, update);
+                     reinterpret_cast<T*>(pack), p0, n, lr, mu, gscale, step_ptr, update, skip);
 }
 
 // Bounded busy wait of `ticks` periods of the 100 MHz wall clock (one lane; tests of the collective
@@ -258,21 +260,22 @@ void launch_reduce(const float* slab, int slab_ld, int nslab, int p0, int p1, fl
 }
 
 void launch_sgd_pack_range(ModelKind m, DType t, float* params, const float* grad, float* mom, void* pack, int p0,
-                           int p1, float lr, float momentum, float gscale, int32_t* step_ptr, hipStream_t s) {
+                           int p1, float lr, float momentum, float gscale, int32_t* step_ptr, hipStream_t s,
+                           const uint32_t* skip) {
   if (p1 <= p0) return;
   float* mb = momentum != 0.f ? mom : nullptr;
   if (m == ModelKind::MLP) {
-    if (t == DType::F32) sgd_launch<MlpModel, float>(params, grad, mb, pack, p0, p1, lr, momentum, gscale, step_ptr, 1, s);
-    else sgd_launch<MlpModel, bf16>(params, grad, mb, pack, p0, p1, lr, momentum, gscale, step_ptr, 1, s);
+    if (t == DType::F32) sgd_launch<MlpModel, float>(params, grad, mb, pack, p0, p1, lr, momentum, gscale, step_ptr, 1, s, skip);
+    else sgd_launch<MlpModel, bf16>(params, grad, mb, pack, p0, p1, lr, momentum, gscale, step_ptr, 1, s, skip);
   } else {
-    if (t == DType::F32) sgd_launch<LenetModel, float>(params, grad, mb, pack, p0, p1, lr, momentum, gscale, step_ptr, 1, s);
-    else sgd_launch<LenetModel, bf16>(params, grad, mb, pack, p0, p1, lr, momentum, gscale, step_ptr, 1, s);
+    if (t == DType::F32) sgd_launch<LenetModel, float>(params, grad, mb, pack, p0, p1, lr, momentum, gscale, step_ptr, 1, s, skip);
+    else sgd_launch<LenetModel, bf16>(params, grad, mb, pack, p0, p1, lr, momentum, gscale, step_ptr, 1, s, skip);
   }
 }
 
 void launch_sgd_pack(ModelKind m, DType t, float* params, const float* grad, float* mom, void* pack, int nparam,
-                     float lr, float momentum, float gscale, int32_t* step_ptr, hipStream_t s) {
-  launch_sgd_pack_range(m, t, params, grad, mom, pack, 0, nparam, lr, momentum, gscale, step_ptr, s);
+                     float lr, float momentum, float gscale, int32_t* step_ptr, hipStream_t s, const uint32_t* skip) {
+  launch_sgd_pack_range(m, t, params, grad, mom, pack, 0, nparam, lr, momentum, gscale, step_ptr, s, skip);
 }
 
 void launch_spin(double seconds, hipStream_t s) {

@@ -1,5 +1,8 @@
 #include "oneshot.h"
 
+#include <cstdio>
+
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -22,6 +25,13 @@ OneShotAllReduce::OneShotAllReduce(int rank, int world, int device, int max_coun
   HIP_CHECK(hipMalloc(&d_local_, (nblk + 1) * sizeof(uint32_t)));
   HIP_CHECK(hipMemset(d_local_, 0, (nblk + 1) * sizeof(uint32_t)));
   HIP_CHECK(hipDeviceSynchronize());
+  // test-only fault injection: "rank:call" -- this rank does not issue its call number `call` (0-based), so its
+  // peers' flag waits run out (the latched-error path)
+  if (const char* e = std::getenv("MNIST_AMD_ONESHOT_SKIP_CALL"); e && *e) {
+    int r = -1;
+    long long c = -1;
+    if (std::sscanf(e, "%d:%lld", &r, &c) == 2 && r == rank_) skip_call_ = c;
+  }
   if (world == 1) open_peers({});
 }
 
@@ -30,6 +40,7 @@ OneShotAllReduce::~OneShotAllReduce() {
   if (d_data_) (void)hipFree(d_data_);
   if (d_flags_) (void)hipFree(d_flags_);
   if (d_local_) (void)hipFree(d_local_);
+  if (d_stamps_) (void)hipFree(d_stamps_);
   if (region_) (void)hipFree(region_);
 }
 
@@ -69,8 +80,9 @@ void OneShotAllReduce::all_reduce_sum_f32(float* buf, size_t count, hipStream_t 
   if (!ready_) throw std::runtime_error("OneShotAllReduce: open_peers() first");
   if (count > (size_t)max_count_) throw std::invalid_argument("OneShotAllReduce: count exceeds max_count");
   if (reinterpret_cast<uintptr_t>(buf) % 16) throw std::invalid_argument("OneShotAllReduce: buffer not 16-byte aligned");
+  if (calls_++ == skip_call_) return;  // fault injection (tests)
   launch_oneshot_allreduce(buf, (int)count, rank_, world_, max_count_, d_data_, d_flags_, d_local_, d_local_ + nblk_,
-                           nblk_, timeout_ticks_, s);
+                           nblk_, timeout_ticks_, s, d_stamps_);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -78,7 +90,31 @@ std::string OneShotAllReduce::check() {
   uint32_t e = 0;
   HIP_CHECK(hipMemcpy(&e, d_local_ + nblk_, sizeof(e), hipMemcpyDeviceToHost));
   if (!e) return "";
-  const uint32_t z = 0;
-  HIP_CHECK(hipMemcpy(d_local_ + nblk_, &z, sizeof(z), hipMemcpyHostToDevice));
-  return "rank " + std::to_string(rank_) + ": one-shot all-reduce flag wait timed out (a peer did not arrive)";
+  return "rank " + std::to_string(rank_) + ": one-shot all-reduce flag wait timed out (a peer did not arrive within " +
+         std::to_string(timeout_ticks_ / 100000000ull) + " s); the error is latched: later calls and the parameter "
+         "updates behind them are skipped";
+}
+
+void OneShotAllReduce::clear_error() {
+  HIP_CHECK(hipMemset(d_local_ + nblk_, 0, sizeof(uint32_t)));
+  HIP_CHECK(hipDeviceSynchronize());
+}
+
+void OneShotAllReduce::enable_stamps(bool on) {
+  if (on && !d_stamps_) {
+    HIP_CHECK(hipMalloc(&d_stamps_, (size_t)nblk_ * 4 * sizeof(unsigned long long)));
+    HIP_CHECK(hipMemset(d_stamps_, 0, (size_t)nblk_ * 4 * sizeof(unsigned long long)));
+  } else if (!on && d_stamps_) {
+    HIP_CHECK(hipDeviceSynchronize());
+    HIP_CHECK(hipFree(d_stamps_));
+    d_stamps_ = nullptr;
+  }
+}
+
+std::vector<unsigned long long> OneShotAllReduce::stamps() {
+  std::vector<unsigned long long> out;
+  if (!d_stamps_) return out;
+  out.resize((size_t)nblk_ * 4);
+  HIP_CHECK(hipMemcpy(out.data(), d_stamps_, out.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  return out;
 }

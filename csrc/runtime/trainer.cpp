@@ -495,7 +495,7 @@ void Trainer::comm_phase(int phase, hipEvent_t ready, bool bump) {
   const int p0 = phase == 0 ? ps : 0, p1 = phase == 0 ? nparam_ : ps;
   launch_sgd_pack_range(model_, dtype_, ptr<float>(p_.params), ptr<const float>(p_.grad), ptr<float>(p_.mom),
                         ptr<void>(p_.pack), p0, p1, lr_, momentum_, 1.0f / float(world_),
-                        bump ? ptr<int32_t>(p_.step) : nullptr, comm_stream_);
+                        bump ? ptr<int32_t>(p_.step) : nullptr, comm_stream_, dp_skip());
   post_launch(comm_stream_);
 }
 
@@ -514,7 +514,7 @@ void Trainer::launch_mlp_comm_tail(int B, hipStream_t s, const HeadBuffers& hb, 
     post_launch(s);
     all_reduce(coalesced_buckets(), -1, s);
     launch_sgd_pack(model_, dtype_, ptr<float>(p_.params), g, ptr<float>(p_.mom), ptr<void>(p_.pack), nparam_, lr_,
-                    momentum_, 1.0f / float(world_), ptr<int32_t>(p_.step), s);
+                    momentum_, 1.0f / float(world_), ptr<int32_t>(p_.step), s, dp_skip());
     post_launch(s);
     return;
   }
@@ -550,7 +550,7 @@ void Trainer::launch_lenet_comm_tail(int B, int nslab, int splits, hipStream_t s
     HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));
     all_reduce(coalesced_buckets(), -1, s);
     launch_sgd_pack(model_, dtype_, ptr<float>(p_.params), g, ptr<float>(p_.mom), ptr<void>(p_.pack), nparam_, lr_,
-                    momentum_, gs, ptr<int32_t>(p_.step), s);
+                    momentum_, gs, ptr<int32_t>(p_.step), s, dp_skip());
     post_launch(s);
     return;
   }
@@ -586,14 +586,14 @@ void Trainer::launch_lenet_overlap(int B, int nslab, hipStream_t s, const HeadBu
   post_launch(aux_stream_);
   ov_fc_->all_reduce_sum_f32(g + cp, size_t(nparam_ - cp), aux_stream_);
   launch_sgd_pack_range(model_, dtype_, ptr<float>(p_.params), g, ptr<float>(p_.mom), ptr<void>(p_.pack), cp, nparam_,
-                        lr_, momentum_, gs, nullptr, aux_stream_);
+                        lr_, momentum_, gs, nullptr, aux_stream_, ov_fc_->err_word());
   post_launch(aux_stream_);
   HIP_CHECK(hipEventRecord(events_[5], aux_stream_));
   launch_reduce(ptr<const float>(p_.slab_conv), cp, nslab, 0, cp, scale, g, s);
   post_launch(s);
   ov_conv_->all_reduce_sum_f32(g, size_t(cp), s);
   launch_sgd_pack_range(model_, dtype_, ptr<float>(p_.params), g, ptr<float>(p_.mom), ptr<void>(p_.pack), 0, cp, lr_,
-                        momentum_, gs, ptr<int32_t>(p_.step), s);
+                        momentum_, gs, ptr<int32_t>(p_.step), s, ov_conv_->err_word());
   post_launch(s);
 }
 

@@ -170,6 +170,8 @@ class Trainer {
   // comm stream: wait for `ready`, all-reduce phase `phase`'s buckets, update its parameter range
   void comm_phase(int phase, hipEvent_t ready, bool bump);
   bool use_comm() const { return (comm_ || oneshot_ || has_overlap()) && comm_enabled_; }
+  // the update kernels' skip word: the one-shot data plane's latched error (oneshot.hip), none with RCCL
+  const uint32_t* dp_skip() const { return oneshot_ ? oneshot_->err_word() : nullptr; }
   void sync_own_streams();
   struct GraphSlot {
     hipGraph_t graph = nullptr;

@@ -348,11 +348,8 @@ class NativeTrainer:
 
     def check_comm(self) -> None:
         """Health poll (once per epoch): abort + raise on an asynchronous RCCL error; raise if a one-shot
-        all-reduce flag wait timed out."""
-        for o in ([self.oneshot] if self.oneshot is not None else []) + list(self.overlap or ()):
-            err = o.check()
-            if err:
-                raise CollectiveError(err)
+        all-reduce flag wait timed out (also raised by every :meth:`synchronize`)."""
+        self._check_oneshot()
         if self.comm is None:
             return
         err = self.comm.async_error()
@@ -608,10 +605,13 @@ class NativeTrainer:
     def release(self) -> None:
         """Teardown (before the communicator is destroyed): drain the streams, drop every cached graph --
         they captured collectives -- and detach the communicator.  The trainer can still run local steps."""
-        if self.comm is not None and not self.comm.aborted:
-            self.synchronize()
-        else:
-            self.stream.synchronize()
+        try:
+            if self.comm is not None and not self.comm.aborted:
+                self.synchronize()
+            else:
+                self.stream.synchronize()
+        except CollectiveError:
+            pass  # already raised to the caller at its last wait; teardown goes on
         self.rt.release()
         self.comm = None
         self.oneshot = None
@@ -761,13 +761,25 @@ class NativeTrainer:
         """Wait for the step stream.  With a communicator this is the collective watchdog: RCCL async
         errors are polled while waiting and a deadline (``MNIST_AMD_COMM_TIMEOUT``) aborts the
         communicator and raises :class:`CollectiveError` instead of hanging in hipStreamSynchronize."""
+        t0 = time.perf_counter()
         if self.comm is None:
             self.stream.synchronize()
-            return
-        t0 = time.perf_counter()
-        err = self.comm.wait_stream(self.stream.cuda_stream, comm_timeout() if timeout is None else timeout)
-        if err:
-            detected = time.perf_counter() - t0
-            self.comm.abort()  # ncclCommAbort: RCCL kernels still waiting on peers exit
-            raise CollectiveError(f"rank {self.comm.rank}: RCCL collective failed: {err} (communicator aborted)",
-                                  detected)
+        else:
+            err = self.comm.wait_stream(self.stream.cuda_stream, comm_timeout() if timeout is None else timeout)
+            if err:
+                detected = time.perf_counter() - t0
+                self.comm.abort()  # ncclCommAbort: RCCL kernels still waiting on peers exit
+                raise CollectiveError(f"rank {self.comm.rank}: RCCL collective failed: {err} (communicator aborted)",
+                                      detected)
+        self._check_oneshot(t0)
+
+    def _oneshot_instances(self):
+        return ([self.oneshot] if self.oneshot is not None else []) + list(self.overlap or ())
+
+    def _check_oneshot(self, t0: Optional[float] = None) -> None:
+        """One-shot data plane: a flag wait that timed out is latched on the device (no sum written, later calls
+        and the updates behind them skipped, csrc/kernels/oneshot.hip); raise it at this host wait."""
+        for o in self._oneshot_instances():
+            err = o.check()
+            if err:
+                raise CollectiveError(err, 0.0 if t0 is None else time.perf_counter() - t0)

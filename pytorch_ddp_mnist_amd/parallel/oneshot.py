@@ -22,9 +22,13 @@ _GEN = [0]
 
 
 def oneshot_timeout() -> float:
-    """In-kernel bound of a flag wait (``MNIST_AMD_ONESHOT_TIMEOUT`` seconds, default 30): a rank whose peer
-    never arrives finishes the kernel with the error word set, reported by ``check()``."""
-    return float(os.environ.get("MNIST_AMD_ONESHOT_TIMEOUT", "30"))
+    """In-kernel bound of a flag wait (``MNIST_AMD_ONESHOT_TIMEOUT`` seconds, default 5): it bounds how far a
+    rank may run ahead of its slowest peer inside the step loop.  A rank whose peer does not arrive in time
+    LATCHES the error word (csrc/kernels/oneshot.hip): that call writes no sum, every later call does nothing,
+    the parameter updates behind them are skipped, and the next host wait raises :class:`CollectiveError`
+    (``NativeTrainer.synchronize`` polls ``check()``).  A few seconds, not the RCCL watchdog's 600: a kernel
+    must not spin for minutes on a dead peer."""
+    return float(os.environ.get("MNIST_AMD_ONESHOT_TIMEOUT", "5"))
 
 
 def make_oneshot(ctx, max_count: int, nblk: int = 64, timeout_s: Optional[float] = None, init_timeout_s: float = 180.0):
@@ -52,8 +56,14 @@ def make_oneshot(ctx, max_count: int, nblk: int = 64, timeout_s: Optional[float]
     handles = [bytes(store.get(k)) for k in keys]
     if any(not x for x in handles):
         raise RuntimeError(f"rank {ctx.rank}: a peer failed to create its one-shot region")
-    o.open_peers(handles)
-    ctx.barrier()  # every rank has mapped every region before the first call
+    err = ""
+    try:
+        o.open_peers(handles)
+    except Exception as e:  # noqa: BLE001 -- agreed below, so every rank issues the same collectives
+        err = f"rank {ctx.rank}: mapping the peers' regions failed: {e}"
+    # one agreement (also the barrier: every rank has mapped every region before the first call)
+    if ctx.all_reduce_sum([1.0 if err else 0.0])[0]:
+        raise RuntimeError(err or "a peer failed to map the one-shot regions")
     return o
 
 
@@ -139,9 +149,11 @@ def attach_overlap_plan(ctx, tr, fc_inst, world: int) -> str:
 def setup_oneshot(ctx, tr, world: int, mode: str, pinned: Optional[str] = None):
     """The one-shot data plane of a trainer with an RCCL communicator attached (bench.py and the entry-script
     runner).  ``mode == "oneshot"``: the step's collectives run on a validated one-shot instance (failure is
-    fatal: RuntimeError); ``"rccl"``: at world > 1 a measure-only instance is probed (``MNIST_AMD_PROBE_ONESHOT``,
-    default on) and, when it validates, the OVERLAP plan becomes a calibration candidate.  A pinned ``overlap``
-    plan without it is fatal.  Collective.  Returns (step instance or None, probe instance or None, reason)."""
+    fatal: RuntimeError); ``"rccl"``: at world > 1, only when ``MNIST_AMD_PROBE_ONESHOT=1`` (opt-in: the one-shot
+    plane has not moved a byte over real xGMI links yet, so a default multi-GPU run must not pick it up), a
+    measure-only instance is probed and, when it validates, the OVERLAP plan becomes a calibration candidate.  A
+    pinned ``overlap`` plan without it is fatal.  Collective.  Returns (step instance or None, probe instance or
+    None, reason)."""
     oneshot = probe = None
     why = ""
     if mode == "oneshot":
@@ -151,13 +163,13 @@ def setup_oneshot(ctx, tr, world: int, mode: str, pinned: Optional[str] = None):
             raise RuntimeError(f"one-shot all-reduce failed its check: {err}")
         tr.attach_oneshot(oneshot, world)
         why = attach_overlap_plan(ctx, tr, oneshot, world)
-    elif world > 1 and os.environ.get("MNIST_AMD_PROBE_ONESHOT", "1") != "0":
+    elif world > 1 and os.environ.get("MNIST_AMD_PROBE_ONESHOT", "0") == "1":
         probe, why = probe_oneshot(ctx, tr.nparam)
         if probe is not None:
             why = attach_overlap_plan(ctx, tr, probe, world)
             why = f"overlap plan unavailable: {why}" if why else ""
     else:
-        why = "not probed"
+        why = "not probed (MNIST_AMD_PROBE_ONESHOT=1 opts in)"
     if pinned == "overlap" and why:
         raise RuntimeError(f"--plan overlap: {why}")
     return oneshot, probe, why

@@ -9,10 +9,8 @@
   (the DDP arithmetic, reference ddp_tutorial_multi_gpu.py:72,94).
 (A real 8-GPU node exercises the xGMI links themselves; here the peer "remote" stores go to the same device.)
 """
-import json
 import os
 import re
-import subprocess
 import sys
 
 import pytest
@@ -63,14 +61,10 @@ def test_oneshot_world1_trainer_matches_local(native, small_mnist):
     assert torch.equal(out[0], out[1])
 
 
-def _bench(args, timeout=540):
-    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py")] + args, env=env,
-                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout)
-    assert r.returncode == 0, r.stderr[-3000:]
-    lines = [l for l in r.stdout.splitlines() if l.lstrip().startswith("{")]
-    assert len(lines) == 1, r.stdout
-    return json.loads(lines[0]), r.stderr
+def _bench(args, timeout=540, log_dir=None):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_shared_gpu_ranks import _bench as run
+    return run(args, timeout=timeout, log_dir=log_dir)
 
 
 @pytest.mark.timeout(600)
@@ -83,7 +77,7 @@ def test_oneshot_two_ranks_share_one_gpu(native, tmp_path, plan):
     steps, warmup, batch = 4, 2, 2048
     out, err = _bench(["--gpus", "2", "--comm", "gloo", "--allreduce", "oneshot", "--batch", str(batch),
                        "--steps", str(steps), "--warmup", str(warmup), "--no-eval", "--digest", "--plan", plan,
-                       "--dump-params", str(tmp_path / "p")])
+                       "--dump-params", str(tmp_path / "p")], log_dir=tmp_path / "ranks")
     assert out["n_gpus"] == 2 and out["allreduce"] == "oneshot" and out["value"] > 0
     assert "one-shot" in out["config"]["comm"]
     assert out["config"]["plan"]["plan"] == ("join" if plan == "fixed" else "overlap")
@@ -96,6 +90,37 @@ def test_oneshot_two_ranks_share_one_gpu(native, tmp_path, plan):
     emu = _emulate("lenet5", "bf16", batch, steps + warmup, 0.0)
     rel = ((p[0] - emu[0]).norm() / emu[0].norm()).item()
     assert rel <= 1e-6, rel
+
+
+@pytest.mark.timeout(300)
+def test_oneshot_missing_peer_call_latches(native, tmp_path):
+    """A rank that does not issue one all-reduce (fault injection) makes its peer's flag wait run out: the peer
+    raises CollectiveError at its next host wait within the in-kernel bound + 1 s, and the update behind the
+    failed call leaves its parameters untouched (no partial sum is ever applied)."""
+    import json
+    import subprocess
+    torch.cuda.synchronize()
+    bound = 2.0
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(MNIST_AMD_ONESHOT_SKIP_CALL="1:3", MNIST_AMD_ONESHOT_TIMEOUT=str(bound), MNIST_AMD_SEGV_TRACE="1",
+               PYTHONFAULTHANDLER="1")
+    code = ("import sys; sys.path.insert(0, %r); from pytorch_ddp_mnist_amd.parallel.launch import launch_relay; "
+            "rc, _ = launch_relay([sys.executable, %r], 2, style='torch', timeout=200, log_dir=%r); sys.exit(rc)"
+            % (ROOT, os.path.join(ROOT, "tests", "_oneshot_fault_rank.py"), str(tmp_path / "ranks")))
+    r = subprocess.run([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       text=True, timeout=260)
+    assert r.returncode == 0, r.stderr[-8000:]
+    res = {}
+    for line in (r.stdout + "\n" + r.stderr).splitlines():
+        line = line.strip()
+        if line.startswith("{") and '"rank"' in line:
+            d = json.loads(line)
+            res[d["rank"]] = d
+    assert set(res) == {0, 1}, r.stdout + r.stderr[-4000:]
+    assert res[0]["raised"] and "timed out" in res[0]["msg"], res[0]
+    assert res[0]["seconds"] <= bound + 1.0, res[0]
+    assert res[0]["params_unchanged"], res[0]
+    assert res[1]["calls"] == 4 and res[0]["calls"] == 4
 
 
 @pytest.mark.timeout(300)

@@ -21,11 +21,21 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _bench(args, timeout=540):
+def _bench(args, timeout=540, log_dir=None):
+    """Run bench.py in a subprocess.  The pytest process drains its own device work first (nothing of ours
+    runs beside the ranks), the ranks carry the crash tracers (native backtrace + faulthandler, bench.py
+    spawn_ranks), the launcher bounds the whole job below ``timeout`` and terminates every rank on its way
+    out, and a failure reports each rank's exit status and stderr tail (``log_dir``: full per-rank logs)."""
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
-    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py")] + args, env=env,
+    env.update(MNIST_AMD_SEGV_TRACE="1", PYTHONFAULTHANDLER="1", MNIST_AMD_LAUNCH_TIMEOUT=str(max(60, timeout - 60)))
+    extra = ["--rank-logs", str(log_dir)] if log_dir is not None and "--gpus" in args else []
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py")] + args + extra, env=env,
                        stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout)
-    assert r.returncode == 0, r.stderr[-3000:]
+    if r.returncode != 0:
+        print(r.stderr[-20000:], file=sys.stderr)  # every rank's block (launch_relay) -- shown by pytest on failure
+    assert r.returncode == 0, r.stderr[-6000:]
     lines = [l for l in r.stdout.splitlines() if l.lstrip().startswith("{")]
     assert len(lines) == 1, r.stdout
     return json.loads(lines[0]), r.stderr
@@ -65,7 +75,7 @@ def test_two_ranks_share_one_gpu(native, tmp_path, model, dtype, batch):
     steps, warmup = 4, 2
     out, err = _bench(["--gpus", "2", "--comm", "gloo", "--model", model, "--dtype", dtype, "--batch", str(batch),
                        "--steps", str(steps), "--warmup", str(warmup), "--no-eval", "--digest",
-                       "--dump-params", str(tmp_path / "p")])
+                       "--dump-params", str(tmp_path / "p")], log_dir=tmp_path / "ranks")
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["value"] > 0
     assert "gloo" in out["config"]["comm"]
     # the host (gloo) data plane runs the eager phase API, not the captured schedules: nothing is calibrated
