@@ -188,6 +188,13 @@ PYBIND11_MODULE(_C, m) {
       .def("wait_stream",
            [](RcclComm& c, uintptr_t s, double timeout) { return c.wait_stream(reinterpret_cast<hipStream_t>(s), timeout); },
            py::call_guard<py::gil_scoped_release>())
+      .def("probe_cross_stream_capture",
+           [](RcclComm& c, uintptr_t buf, size_t n, uintptr_t s, int replays, double timeout) {
+             return c.probe_cross_stream_capture(reinterpret_cast<float*>(buf), n, reinterpret_cast<hipStream_t>(s),
+                                                 replays, timeout);
+           },
+           py::arg("buf"), py::arg("count"), py::arg("stream"), py::arg("replays") = 3, py::arg("timeout") = 60.0,
+           py::call_guard<py::gil_scoped_release>())
       .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("aborted", &RcclComm::aborted)
       .def_property_readonly("rank", &RcclComm::rank)

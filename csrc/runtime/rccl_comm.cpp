@@ -1,5 +1,7 @@
 #include "rccl_comm.h"
 
+#include "../kernels/launch.h"
+
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -202,6 +204,55 @@ std::vector<float> RcclComm::time_all_reduce(float* buf, size_t count, int warmu
   }  // else: the replays may still be in flight -- leak rather than destroy under them; the caller aborts
   if (!err.empty()) throw std::runtime_error("time_all_reduce: " + err);
   return out;
+}
+
+std::string RcclComm::probe_cross_stream_capture(float* buf, size_t count, hipStream_t s, int replays,
+                                                 double timeout_s) {
+  if (!comm_) return "communicator destroyed / aborted";
+  hipStream_t cs = nullptr, as = nullptr;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  hipGraph_t g = nullptr;
+  hipGraphExec_t ge = nullptr;
+  std::string err;
+  bool capturing = false;
+  try {
+    HIP_CHECK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    HIP_CHECK(hipStreamCreateWithFlags(&as, hipStreamNonBlocking));
+    for (auto& e : ev) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
+    capturing = true;
+    HIP_CHECK(hipEventRecord(ev[0], s));
+    HIP_CHECK(hipStreamWaitEvent(cs, ev[0], 0));
+    const ncclResult_t r = ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm_, cs);
+    if (r != ncclSuccess && r != ncclInProgress) throw std::runtime_error(std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    HIP_CHECK(hipEventRecord(ev[1], cs));          // recorded behind the captured collective ...
+    HIP_CHECK(hipStreamWaitEvent(as, ev[1], 0));   // ... and waited on by another stream
+    launch_spin(0.0, as);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipEventRecord(ev[2], as));
+    HIP_CHECK(hipStreamWaitEvent(s, ev[2], 0));
+    capturing = false;
+    HIP_CHECK(hipStreamEndCapture(s, &g));
+    settle(r, "all_reduce (captured, cross-stream probe)");
+    HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    for (int i = 0; i < replays; ++i) HIP_CHECK(hipGraphLaunch(ge, s));
+    err = wait_stream(s, timeout_s);
+  } catch (const std::exception& e) {
+    err = e.what();
+    if (capturing) {
+      hipGraph_t g2 = nullptr;
+      (void)hipStreamEndCapture(s, &g2);
+      if (g2) hipGraphDestroy(g2);
+    }
+  }
+  if (err.empty() || err.find("timeout") == std::string::npos) {  // (a stuck replay is leaked, not destroyed)
+    if (ge) hipGraphExecDestroy(ge);
+    if (g) hipGraphDestroy(g);
+    for (auto& e : ev) if (e) hipEventDestroy(e);
+    if (cs) hipStreamDestroy(cs);
+    if (as) hipStreamDestroy(as);
+  }
+  return err;
 }
 
 std::string RcclComm::async_error() {

@@ -41,6 +41,11 @@ class RcclComm {
   // the same count, in the same order.  Waits through wait_stream (throws on an RCCL error / timeout).
   std::vector<float> time_all_reduce(float* buf, size_t count, int warmup, int iters, hipStream_t s,
                                      double timeout_s);
+  // Capture probe of the pattern the SPLIT plan was built to avoid (ROCm 7.0 segfaulted in hipStreamEndCapture on a
+  // related form): inside ONE captured graph a side stream runs the all-reduce, a THIRD stream waits on an event
+  // recorded behind it and runs a kernel, the capturing stream joins that stream; the graph is instantiated and
+  // replayed `replays` times.  Returns "" or what failed.  Collective (every rank, same count).
+  std::string probe_cross_stream_capture(float* buf, size_t count, hipStream_t s, int replays, double timeout_s);
   // Returns "" if healthy, else the error string.  Non-blocking.
   std::string async_error();
   // Wait for `s` with async-error polling: "" once it drains, else the RCCL error or "timeout after …".

@@ -210,6 +210,7 @@ class NativeTrainer:
         self.oneshot = None         # one-shot xGMI all-reduce data plane (attach_oneshot)
         self.overlap = None         # (FC, conv) one-shot instances of the OVERLAP plan (attach_overlap)
         self.ext_allreduce = None   # external data plane (attach_external_allreduce)
+        self.capture_failures = {}  # candidate schedules the runtime refused to capture (time_schedules)
         self.module_template = build_model(model)
         if init is not None:
             self.load_module(init)
@@ -407,11 +408,22 @@ class NativeTrainer:
         self._sync_in()
         st = self.stream
         names = list(candidates)
+        failed = {}
         for name in names:                 # all captures (host work) before any timed replay
-            self.apply_plan(candidates[name])
-            self.prepare_graphs()
-            if multi and self.rt.multi_steps != k:
-                self.rt.capture_multi(st.cuda_stream, k)
+            try:
+                self.apply_plan(candidates[name])
+                self.prepare_graphs()
+                if multi and self.rt.multi_steps != k:
+                    self.rt.capture_multi(st.cuda_stream, k)
+            except RuntimeError as e:      # a capture the runtime refuses drops that candidate, not the run
+                failed[name] = str(e)
+        # every rank drops the same candidates (a captured collective has not run yet: dropping one is safe)
+        agree = reduce_max if reduce_max is not None else (lambda v: v)
+        names = [n for n in names if not agree(1.0 if n in failed else 0.0)]
+        self.capture_failures = failed
+        if not names:
+            raise RuntimeError(f"time_schedules: no candidate could be captured: {failed}")
+        self.apply_plan(candidates[names[0]])
         ev = {name: [] for name in names}
         with torch.cuda.stream(st):
             self.step_ctr[0].zero_()       # every replay trains on batch 0 of the loaded order
@@ -443,7 +455,9 @@ class NativeTrainer:
                     pos += per
                     if r > 0 and j > 0:
                         ev[name].append((a, b))
-        self.synchronize()
+        # the calibration's own watchdog: a candidate whose collectives never complete fails the start-up within
+        # minutes, naming the calibration, instead of after the step loop's full deadline
+        self.synchronize(timeout=min(comm_timeout(), float(os.environ.get("MNIST_AMD_CALIB_TIMEOUT", "180"))))
         timings = {}
         if os.environ.get("MNIST_AMD_CALIB_DEBUG"):
             for name in names:
@@ -485,10 +499,14 @@ class NativeTrainer:
         sustained clock before the caller's warm-up steps (measured: steps 1-20 after a cold start run ~6 %
         slower than steps 100+, scripts/step_times.py).
 
-        At world >= 2 only plans whose capture pattern is the plain one (every collective and the update
-        on the main step stream: JOIN) are candidates unless ``MNIST_AMD_TRY_SPLIT=1``: the SPLIT plans put
-        kernels on a side stream behind a captured RCCL call, a pattern that has not run on a real
-        multi-GPU communicator yet (it made hipStreamEndCapture fail on ROCm 7.0 in a related form).
+        At world >= 2 the SPLIT plans are candidates too (``MNIST_AMD_NO_SPLIT=1`` keeps JOIN only): their
+        collectives and updates run on ONE comm stream in a fixed order (FC buckets beside conv_bwd, then the
+        conv buckets), and only the main stream consumes the comm stream's completion, once, at the end of the
+        step -- the capture pattern that made hipStreamEndCapture fail on ROCm 7.0 (a stream waiting on an event
+        recorded behind a captured RCCL call) is not used, and a world-1 test replays that pattern on the box's
+        runtime (``RcclComm.probe_cross_stream_capture``).  A candidate whose capture the runtime refuses is
+        dropped on every rank (:meth:`time_schedules`), and the calibration waits under its own watchdog
+        (``MNIST_AMD_CALIB_TIMEOUT``, default 180 s).
         ``exposed_comm_ms`` is measured against the local schedule with the chosen plan's fwd_head /
         conv_bwd-grid settings and the faster of the concurrent / serial single-GPU branch.
         """
@@ -507,7 +525,7 @@ class NativeTrainer:
                     candidates = default_plan_candidates(self.C.conv_bwd_blocks(self.batch), ncu)
                 else:
                     candidates = mlp_plan_candidates()
-                if self.world > 1 and not os.environ.get("MNIST_AMD_TRY_SPLIT"):
+                if self.world > 1 and os.environ.get("MNIST_AMD_NO_SPLIT", "0") == "1":
                     candidates = {k: v for k, v in candidates.items() if v.get("plan", "join") == "join"}
                 if ovl:
                     candidates["overlap"] = dict(plan="overlap")
@@ -534,13 +552,18 @@ class NativeTrainer:
             self.apply_plan(candidates[chosen])
             return {"chosen": chosen, "timings_ms": {}, "candidates": candidates, "single_candidate": True}
         timings = self.time_schedules({**candidates, **extra}, iters=iters, warmup=warmup, reduce_max=reduce_max)
-        chosen = choose_plan({k: timings[k] for k in candidates}, prefer=prefer, margin=margin)
+        ok = {k: timings[k] for k in candidates if k in timings}
+        if not ok:
+            raise RuntimeError(f"autotune_plan: no candidate could be captured: {self.capture_failures}")
+        chosen = choose_plan(ok, prefer=prefer, margin=margin)
         self.apply_plan(candidates[chosen])
         out = {"chosen": chosen, "timings_ms": {k: round(v, 4) for k, v in timings.items()},
                "candidates": candidates, "replays_per_candidate": self.last_timing["replays"],
                "steps_per_replay": self.last_timing["graph_steps"], "interleaved": True}
-        if extra:
-            local = min(timings[k] for k in extra)
+        if self.capture_failures:
+            out["capture_failures"] = self.capture_failures
+        if extra and any(k in timings for k in extra):
+            local = min(timings[k] for k in extra if k in timings)
             out["nocomm_ms"] = round(local, 4)
             out["exposed_comm_ms"] = round(timings[chosen] - local, 4)
         if log is not None:

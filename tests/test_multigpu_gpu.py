@@ -109,3 +109,20 @@ def test_autotune_plan_restores_state(native, small_mnist):
     tr.step(512)                                    # the installed plan trains
     tr.synchronize()
     assert torch.isfinite(tr.params).all()
+
+
+def test_rccl_cross_stream_capture_pattern(native):
+    """The capture pattern the SPLIT plan was written to avoid (ROCm 7.0: hipStreamEndCapture segfaulted on a
+    related form): a stream waiting on an event recorded behind a captured RCCL all-reduce, joined back into the
+    capturing stream.  On the box's runtime it captures, instantiates and replays (world 1), and the all-reduce
+    it carries is the identity there."""
+    comm = native.RcclComm(native.RcclComm.make_unique_id(), 0, 1, 0)
+    x = torch.randn(61706, device="cuda")
+    ref = x.clone()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    err = comm.probe_cross_stream_capture(x.data_ptr(), x.numel(), s.cuda_stream, replays=3, timeout=60.0)
+    assert err == "", err
+    s.synchronize()
+    assert torch.equal(x, ref)
+    assert comm.destroy(60.0) == ""
