@@ -77,14 +77,9 @@ PYBIND11_MODULE(_C, m) {
   m.attr("L1_SPLIT_MAX_B") = L1_SPLIT_MAX_B;
   m.attr("STAMP_ROWS") = STAMP_ROWS;
 #ifdef MNIST_AMD_F32_SPLIT
-  m.attr("F32_SPLIT") = (int)MNIST_AMD_F32_SPLIT;  // fp32 products as bf16-part MFMAs (common.h Mma<float>)
+  m.attr("F32_SPLIT") = 3;  // fp32 products as 3-part bf16 MFMAs (common.h Mma<float>, opt-in build)
 #else
   m.attr("F32_SPLIT") = 0;
-#endif
-#ifdef MNIST_AMD_RAW_ROWS
-  m.attr("RAW_ROWS") = true;
-#else
-  m.attr("RAW_ROWS") = false;
 #endif
   m.attr("XB_MAX_B") = Trainer::XB_MAX_B;  // LeNet: batch-ordered pixel rows conv_fwd -> conv_bwd up to this batch
   m.def("device_count", [] {
@@ -115,7 +110,7 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init<>())
 #define RW(f) .def_readwrite(#f, &TrainerPtrs::f)
       RW(images) RW(labels) RW(idx) RW(step) RW(params) RW(grad) RW(mom) RW(pack) RW(slab_fc) RW(slab_conv)
-      RW(metrics) RW(xT) RW(h1T) RW(h2T) RW(dy1T) RW(dy2T) RW(dy3T) RW(p1) RW(m1) RW(p2) RW(m2) RW(dp2) RW(z1p) RW(stamps) RW(xnext) RW(ynext) RW(xrows) RW(xb);
+      RW(metrics) RW(xT) RW(h1T) RW(h2T) RW(dy1T) RW(dy2T) RW(dy3T) RW(p1) RW(m1) RW(p2) RW(m2) RW(dp2) RW(z1p) RW(stamps) RW(xnext) RW(ynext) RW(xb);
 #undef RW
 
   py::class_<Bucket>(m, "Bucket")

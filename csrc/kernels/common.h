@@ -41,11 +41,13 @@ template <> struct Mma<float> {
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[3], b.v[3], acc, 0, 0, 0);
   }
 #else
-  // Opt-in build (MNIST_AMD_F32_SPLIT=2 or 3): fp32 operands as 2 or 3 bf16 parts (hi = x rounded to bf16, then
-  // each exact remainder rounded to bf16), products on v_mfma_f32_16x16x16_bf16, whose lane layout (4
-  // contiguous k per lane, K = 16) is this chunk's.  =2: lo*lo + lo*hi + hi*lo + hi*hi, 4 bf16 MFMAs instead of
-  // 4 f32 ones (at 1/16 of the bf16 rate), ~2^-16 relative error per product (the rounding of lo).  =3: the six
-  // terms of weight >= 2^-16 of (hi + mid + lo)^2, ~2^-24 (fp32-like).
+  // Opt-in build (-DMNIST_AMD_F32_SPLIT): fp32 operands as 3 bf16 parts (hi = x rounded to bf16, then each exact
+  // remainder rounded to bf16), the six products of weight >= 2^-16 of (hi + mid + lo)^2 on
+  // v_mfma_f32_16x16x16_bf16, whose lane layout (4 contiguous k per lane, K = 16) is this chunk's: ~2^-24 relative
+  // error (fp32-like; passes the fp32 tolerances) but 40 % SLOWER than the exact fp32 MFMAs, because the split is
+  // VALU work paid per fragment use (profiles/r4_session2/NOTES.md).  Pre-split LDS operand images would remove that
+  // cost but need 1.5x the fp32 images' LDS (conv_bwd fp32 already uses 150 KB of the 160 KB); not built.  (The
+  // 2-part / truncated 3-term forms failed the tolerances and were removed in round 5.)
   typedef __attribute__((ext_vector_type(4))) short s16x4;
   // (whole vectors are bit-cast: hipcc (ROCm 7.2) lowered __builtin_bit_cast of an ext-vector ELEMENT --
   // x.y, x[j] -- to a read of element 0)
@@ -65,10 +67,8 @@ template <> struct Mma<float> {
     return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, acc, 0, 0, 0);
   }
   static DEV void mma(f32x4& acc, const Frag& a, const Frag& b) {
-    f32x4 ra, rb;
+    f32x4 ra, rb, ra2, rb2;
     const s16x4 ah = part(a.v, ra), bh = part(b.v, rb);
-#if MNIST_AMD_F32_SPLIT >= 3
-    f32x4 ra2, rb2;
     const s16x4 am = part(ra, ra2), bm = part(rb, rb2);
     const s16x4 al = part(ra2, ra), bl = part(rb2, rb);
     acc = mf(al, bh, acc);
@@ -77,13 +77,6 @@ template <> struct Mma<float> {
     acc = mf(am, bh, acc);
     acc = mf(ah, bm, acc);
     acc = mf(ah, bh, acc);
-#else
-    const s16x4 al = part(ra, ra), bl = part(rb, rb);
-    acc = mf(al, bl, acc);
-    acc = mf(al, bh, acc);
-    acc = mf(ah, bl, acc);
-    acc = mf(ah, bh, acc);
-#endif
   }
 #endif
   static DEV Frag load(const float* p) { Frag f; f.v = *reinterpret_cast<const f32x4*>(p); return f; }

@@ -343,12 +343,6 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       // around the loads' consumers
       const int eu = tid + i * NTH, e = min(eu, NGI - 1), r = (e % (R / 4)) * 4, c = e / (R / 4);
       const bool item = eu < NGI;
-      if (TRAIN && hb.xrows != nullptr && item && c < H::K0 / 16) {
-        // raw-row hand-off to the layer-1 weight gradient: the 16 pixels of each of the 4 rows, as loaded
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (r0 + r + q < B) *reinterpret_cast<u32x4*>(hb.xrows + (size_t)(r0 + r + q) * 784 + c * 16) = px[i][q];
-      }
       if constexpr (sizeof(T) == 2) {
         // each row's 16 pixels -> 16 bf16 packed in 8 registers (two 16-byte LDS stores); the xT store of
         // pixel j takes halfword j of the four rows (as the pool2-row path below)
@@ -368,7 +362,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
             if (item) *reinterpret_cast<u32x4*>(sX + (r + q) * S::PX + c * 16 + h * 8) = pk[q][h];
           }
         }
-        if (TRAIN && item && !ABLATED(hb.ablate, 1) && hb.xrows == nullptr) {
+        if (TRAIN && item && !ABLATED(hb.ablate, 1)) {
 #pragma unroll
           for (int j = 0; j < 16; ++j) {
             const int h = j >> 3, wd = (j & 7) >> 1, sh = 16 * (j & 1);
@@ -1080,18 +1074,13 @@ struct WgRows {
 //  * loads: interval i's 16-byte chunks are issued two intervals ahead into one of two register slots (slot
 //    i & 1, statically alternated by a two-way unrolled loop), so two intervals of loads are in flight behind
 //    the MFMAs; ONE LDS buffer (20 KB at SUB 2), written between two barriers (a double-buffered SUB-4
-//    version -- 72 KB, two workgroups per CU -- ran the MLP's 560-workgroup grid in two rounds);
-//  * GX (gather job, bf16; builds with MNIST_AMD_RAW_ROWS only): the layer-1 input comes from the raw uint8
-//    batch rows the head wrote (HeadBuffers::xrows, half the bytes of a bf16 X^T): the B tile is [SUB * 32
-//    batch rows][64 pixels] (row pitch PG), filled from 16-pixel chunks normalised in registers, read with
-//    transposing ds_read_b64_tr_b16.  Measured slower than the bf16 X^T it replaces (35.5 vs 33.2 us per MLP
-//    step at SUB 2, same box): the head's row stores cost what its X^T stores cost (~1.1 us of the staging
-//    phase) and the in-register normalise + 8-byte transposing reads cost more than 16-byte X^T fragment
-//    reads; re-gathering through the epoch's sample indices instead put an index round trip in front of every
-//    interval's pixel loads.  Every load sits in straight-line code or behind a block-uniform branch.
+//    version -- 72 KB, two workgroups per CU -- ran the MLP's 560-workgroup grid in two rounds).
+//    (Measured and removed in round 5: the layer-1 B operand as the raw uint8 batch rows the head wrote,
+//    normalised in registers and read with transposing LDS reads -- 35.5 vs 33.2 us per MLP bf16 step;
+//    profiles/r4_session2/ab_mlp8k_raw_rows.txt.)
 // Rows padded by 32 B (conflict-free ds_read_b128 fragment reads).  LDS use keeps it to the schedules where
 // nothing LDS-heavy runs beside it (the MLP; LeNet's FC wgrad runs beside conv_bwd on the LDS-free kernel).
-template <typename T, int SUB, bool GX>
+template <typename T, int SUB>
 DEV void wgrad_lds_body(const WgArgs<T>& a, const int j, const WgRows rows, const int nsteps, const int tile,
                         const int split, T* sa, T* sb) {
   const WgJob<T>& J = a.job[j];
@@ -1099,8 +1088,6 @@ DEV void wgrad_lds_body(const WgArgs<T>& a, const int j, const WgRows rows, cons
   using Frag = typename M::Frag;
   constexpr int KV = M::KV, KC = M::KC;
   constexpr int PE = (SUB * 64 + 32) / (int)sizeof(T);  // row pitch (elements): SUB steps x 64 B + 32 B pad
-  constexpr int PG = 64 + 8, GJ = SUB * KC * 4 / 256, GN = GX ? GJ : 1;
-  static_assert(!GX || (sizeof(T) == 2 && GJ >= 1 && SUB * KC * PG <= 64 * PE), "gather tile");
   const int tid = threadIdx.x, lane = tid & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
   const int nint = (nsteps + SUB - 1) / SUB;  // barrier intervals (block-uniform)
   const int lb = tile - J.blk_begin;
@@ -1117,63 +1104,22 @@ DEV void wgrad_lds_body(const WgArgs<T>& a, const int j, const WgRows rows, cons
   const T* bsrc = J.xT + (size_t)min(kb0 + sr, J.K > 0 ? J.K - 1 : 0) * a.ldB + sc * KV;
   const u32x4 z4 = u32x4{0u, 0u, 0u, 0u};
   struct Slot {
-    u32x4 ra[SUB], rb[GX ? GJ : SUB];
-    bool live[GN];
+    u32x4 ra[SUB], rb[SUB];
   };
   auto fetch = [&](int it, Slot& d) {  // straight-line loads of interval it (steps past nsteps re-read the last)
 #pragma unroll
     for (int q = 0; q < SUB; ++q) {
       const int rc = rows(min(it * SUB + q, nsteps - 1), KC);
       d.ra[q] = *reinterpret_cast<const u32x4*>(asrc + rc);
-      if constexpr (!GX) d.rb[q] = *reinterpret_cast<const u32x4*>(bsrc + rc);
-    }
-    if constexpr (GX) {
-#pragma unroll
-      for (int j = 0; j < GJ; ++j) {
-        const int c = tid + 256 * j, q = c / (4 * KC), rr = (c >> 2) % KC;
-        const int rg = rows(min(it * SUB + q, nsteps - 1), KC) + rr;
-        const int px = min(kb0 + (c & 3) * 16, 784 - 16);  // chunks past the image: any in-row address (k >= K unused)
-        d.rb[j] = *reinterpret_cast<const u32x4*>(a.gx_rows + (size_t)min(rg, a.gx_B - 1) * 784 + px);
-        d.live[j] = rg < a.gx_B;
-      }
+      d.rb[q] = *reinterpret_cast<const u32x4*>(bsrc + rc);
     }
   };
   auto stage = [&](const Slot& d) {
 #pragma unroll
     for (int q = 0; q < SUB; ++q) {
       *reinterpret_cast<u32x4*>(&sa[sr * PE + q * KC + sc * KV]) = a_ok ? d.ra[q] : z4;
-      if constexpr (!GX) *reinterpret_cast<u32x4*>(&sb[sr * PE + q * KC + sc * KV]) = b_ok ? d.rb[q] : z4;
+      *reinterpret_cast<u32x4*>(&sb[sr * PE + q * KC + sc * KV]) = b_ok ? d.rb[q] : z4;
     }
-    if constexpr (GX) {
-#pragma unroll
-      for (int j = 0; j < GJ; ++j) {
-        const int c = tid + 256 * j;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          bf16x8 f;
-#pragma unroll
-          for (int e = 0; e < 8; ++e)
-            f[e] = (bf16)(d.live[j] ? mnist_norm((d.rb[j][2 * h + (e >> 2)] >> (8 * (e & 3))) & 255u) : 0.f);
-          *reinterpret_cast<bf16x8*>(&sb[(c >> 2) * PG + (c & 3) * 16 + h * 8]) = f;
-        }
-      }
-    }
-  };
-  // gather B fragment: pixel column kl (tile-local) of batch rows q * KC + grp * KV .. + 7 (the lane's k run of
-  // the MFMA), two 4-row x 16-column blocks transposed by the read (lane 4 i + p of a 16-lane group addresses
-  // row i, columns 4 p .. 4 p + 3; lane l receives column l)
-  auto load_gx = [&](int q, int kl) -> Frag {
-    Frag f;
-    if constexpr (GX) {
-      typedef short v4s __attribute__((ext_vector_type(4)));
-      const T* p = &sb[(q * KC + grp * KV + ((lane & 15) >> 2)) * PG + kl + 4 * (lane & 3)];
-      const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(const_cast<T*>(p)));
-      const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(const_cast<T*>(p + 4 * PG)));
-      f.v = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-    } else {
-      f = M::zero();
-    }
-    return f;
   };
 
   f32x4 acc[2][2];
@@ -1190,7 +1136,6 @@ DEV void wgrad_lds_body(const WgArgs<T>& a, const int j, const WgRows rows, cons
   const int sel1 = kk1 < J.K ? 0 : (kk1 == J.K && J.bias ? 1 : 2);
   const int ao0 = (n0 - nb0 + row) * PE + grp * KV, ao1 = ao0 + 16 * PE;
   const int bo0 = (k0 - kb0 + row) * PE + grp * KV, bo1 = bo0 + 16 * PE;
-  const int gk0 = k0 - kb0, gk1 = gk0 + 16;  // gather: tile-local pixel columns of this wave's fragments
   // B columns past K: the bias column reads ones, the padding zeros -- loop-invariant per lane, applied as a
   // vector select (a select between whole fragments was lowered to an indexed scratch array)
   const bool use0 = sel0 == 0, use1 = sel1 == 0;
@@ -1201,14 +1146,7 @@ DEV void wgrad_lds_body(const WgArgs<T>& a, const int j, const WgRows rows, cons
     for (int q = 0; q < SUB; ++q) {
       if (q < nq) {
         const Frag a0 = M::load(&sa[ao0 + q * KC]), a1 = M::load(&sa[ao1 + q * KC]);
-        Frag f0, f1;
-        if constexpr (GX) {
-          f0 = load_gx(q, gk0);
-          f1 = load_gx(q, gk1);
-        } else {
-          f0 = M::load(&sb[bo0 + q * KC]);
-          f1 = M::load(&sb[bo1 + q * KC]);
-        }
+        const Frag f0 = M::load(&sb[bo0 + q * KC]), f1 = M::load(&sb[bo1 + q * KC]);
         Frag b0, b1;
         b0.v = use0 ? f0.v : alt0.v;
         b1.v = use1 ? f1.v : alt1.v;
@@ -1263,7 +1201,7 @@ template <typename T, int SUB>
 __global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
   constexpr int KC = Mma<T>::KC;
   constexpr int TILE = 64 * ((SUB * 64 + 32) / (int)sizeof(T));
-  __shared__ __attribute__((aligned(16))) T lds[2][TILE];  // [A = dY^T, B = X^T / gathered rows]
+  __shared__ __attribute__((aligned(16))) T lds[2][TILE];  // [A = dY^T, B = X^T]
   const int lin = blockIdx.y * gridDim.x + blockIdx.x;
   if (a.stamps && threadIdx.x == 0 && lin < 512) a.stamps[(STAMP_WGRAD + lin) * 16] = wall_clock64();
   int tile, split, nsteps;
@@ -1289,15 +1227,7 @@ __global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
   nsteps = __builtin_amdgcn_readfirstlane(nsteps);
   int j = 0;
   while (j + 1 < a.njobs && tile >= a.job[j + 1].blk_begin) ++j;
-  if constexpr (sizeof(T) == 2 && SUB >= 2) {
-    if (a.job[j].gather) {
-      wgrad_lds_body<T, SUB, true>(a, j, rows, nsteps, tile, split, lds[0], lds[1]);
-    } else {
-      wgrad_lds_body<T, SUB, false>(a, j, rows, nsteps, tile, split, lds[0], lds[1]);
-    }
-  } else {
-    wgrad_lds_body<T, SUB, false>(a, j, rows, nsteps, tile, split, lds[0], lds[1]);
-  }
+  wgrad_lds_body<T, SUB>(a, j, rows, nsteps, tile, split, lds[0], lds[1]);
   if (a.stamps && threadIdx.x == 0 && lin < 512) a.stamps[(STAMP_WGRAD + lin) * 16 + 1] = wall_clock64();
 }
 
@@ -1392,8 +1322,6 @@ int head_launch_t(bool train, const BatchRef& br, const HeadBuffers& hb, int row
   // B=1024 122.3 -> 112.8 us (profiles/r4_session2/ab_lenet_f32_l1_split.txt); LeNet bf16 keeps layer 1 in the head
   constexpr bool split_l1 = H::K0 >= 512 || sizeof(T) == 4;
   if (hb.z1p && br.B <= L1_SPLIT_MAX_B && split_l1) {
-    // (l1_split_kernel, not the head, reads the pixels there: it writes X^T, never the raw rows)
-    if (train && hb.xrows) throw std::logic_error("head: the raw-row hand-off needs the head's own gather");
     head_launch_split<T, H>(train, br, hb, s);
     return 16;
   }

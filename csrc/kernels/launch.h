@@ -51,11 +51,6 @@ struct HeadBuffers {
   float drop_p;
   int32_t xcd = 0;       // the head kernel used the XCD-contiguous row mapping (BatchRef::xcd)
   int32_t ablate = 0;    // diagnostics only (MNIST_AMD_HEAD_ABLATE): bit 0 = skip the X^T stores (wrong wgrad)
-  // Raw-row hand-off (MLP bf16, LDS-staged weight gradient): when xrows is set, the head writes its gathered
-  // uint8 pixels in batch-row order ([B][784], 6.4 MB at B = 8192) instead of the bf16 X^T (12.8 MB), and the
-  // layer-1 weight gradient normalises them in registers -- bitwise the operand X^T would have held
-  uint8_t* xrows = nullptr;
-  int32_t gx_B = 0;      // rows of the batch (rows past it read as zero)
   const uint8_t* yb = nullptr;  // LeNet head16: this step's labels in batch order (LenetConvBuffers::yb) or null
 };
 
@@ -140,12 +135,6 @@ void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetC
 int launch_lenet_fwd_head(DType t, const BatchRef& br, const LenetConvBuffers& cb, const HeadBuffers& hb,
                           hipStream_t s);
 bool lenet_fwd_head_applies(DType t, int B);
-// Small LeNet bf16 batches (B <= 2048, below the fused fwd_head_kernel): conv_fwd + the 16-row head in ONE
-// launch (two images per workgroup, each 16-row group's last-arriving workgroup runs the head); `counters`:
-// [ceil(B / 16)] zeroed ints.  Returns the head rows per tile (16), or 0 when it does not apply (always 0
-// unless built with -DMNIST_AMD_FWD_HEAD_SMALL: measured slower at B = 128).
-int launch_lenet_fwd_head_small(DType t, const BatchRef& br, const LenetConvBuffers& cb, const HeadBuffers& hb,
-                                int* counters, hipStream_t s);
 // LeNet training head alone as the 16-row register-B head (lenet.hip head16_kernel) on the pool2 rows of
 // conv_fwd: bf16, B <= 2048.  Returns launch_head's rows value, or 0 when it
 // does not apply (the caller launches launch_head).

@@ -856,71 +856,9 @@ __global__ __launch_bounds__(512) void head16_kernel(BatchRef br, HeadBuffers hb
   head16_tile<T>(br, hb, smem + S::X_BYTES, sX, r0, blockIdx.x);  // barriers before reading sX
 }
 
-// Small batches (LeNet bf16, B <= FHS_MAX_B): forward + FC head in ONE launch without fwd_head_kernel's 16
-// images per workgroup.  Workgroup b (512 threads) runs conv_fwd on images 2b and 2b+1 (one per 4-wave half),
-// hands its two pool2 rows to global memory, and the LAST workgroup of each 8-workgroup group (16 rows) to
-// arrive runs the 16-row head (head16_tile) on the group's rows.  The hand-off is the last-arriver form of
-// MI355X_MICROARCH.md (visibility, Valid forms, first table row): every pool2 byte stored with 16-byte sc1
-// buffer stores and drained (s_waitcnt vmcnt(0)) by every storing wave, a workgroup barrier, ONE lane's
-// agent-scope atomic add to the group counter; the workgroup whose add returned the last value loads the rows
-// with 16-byte sc1 buffer loads after a barrier; nothing waits or spins, so no workgroup depends on another
-// being resident.  Removes the head kernel's launch and the conv_fwd -> head kernel boundary (3.8 us of a
-// 25.8 us step at B = 128, profiles/r4_session2/stamps_lenet_b128.txt).  Bitwise the conv_fwd + head16 pair.
-// `counters`: [ceil(B / 16)] ints, zero before the launch; each group's last arriver resets its own.
-// MEASURED SLOWER, so opt-in (-DMNIST_AMD_FWD_HEAD_SMALL; profiles/r4_session2/ab_lenet_b128_fwd_head_small.txt):
-// LeNet bf16 B = 128, 2000 steps, bitwise-equal parameters: conv_fwd + head16 25.7 us/step; this kernel with
-// 1 / 2 / 4 images per half 27.2 / 28.7 / 33.1 us.  The hand-off chain (sc1 stores drained, the add's round trip,
-// sc1 loads of the rows) costs what the kernel boundary cost, and the conv part loses the 128-workgroup spread.
-constexpr int FHS_MAX_B = 2048;
-constexpr int FHS_IPH = 1;  // images per 4-wave half (measured: 2 / 4 per half slower still, 28.7 / 33.1 us)
-template <typename T>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) void fwd_head_small_kernel(
-    BatchRef br, LenetConvBuffers cb, HeadBuffers hb, int* counters) {
-  using H = LenetModel::Head;
-  using S = FwdHeadSmem<T>;
-  static_assert(sizeof(T) == 2, "fwd_head_small_kernel: bf16 operand layout");
-  constexpr int CH = H::K0P * (int)sizeof(T) / 16;  // 16-byte chunks per pool2 row (52)
-  constexpr int SC1 = 16;                           // buffer-instruction cache policy: sc1
-  __shared__ __attribute__((aligned(16))) char smem[S::TOTAL];
-  __shared__ int s_last;
-  T* sX = reinterpret_cast<T*>(smem + S::OFF_X);
-  const int tid = threadIdx.x, w = wave_id(), half = w >> 2;
-  constexpr int RW = 2 * FHS_IPH, GW = 16 / RW;  // rows per workgroup, workgroups per 16-row group
-  const int b = blockIdx.x, g = b / GW, B = br.B;
-  const int ngrp = (min(B - 16 * g, 16) + RW - 1) / RW;  // workgroups of this group
-  for (int e = tid; e < 16 * S::PX * (int)sizeof(T) / 16; e += 512) reinterpret_cast<uint4*>(sX)[e] = make_uint4(0, 0, 0, 0);
-  conv_fwd_images<T, true, true, S::PX>(br, cb, RW * b + FHS_IPH * half, FHS_IPH, smem + half * S::HALF, tid & 255,
-                                        w & 3, tid == 0, sX + FHS_IPH * half * S::PX);
-  __syncthreads();  // this workgroup's pool2 rows are in sX
-  // hand-off: rows 2b, 2b+1 (those inside the batch) -> global pool2 rows, sc1 16-byte stores
-  T* p2 = reinterpret_cast<T*>(cb.p2);
-  const __amdgpu_buffer_rsrc_t rp = __builtin_amdgcn_make_buffer_rsrc(p2, (short)0, B * H::K0P * (int)sizeof(T), 0x00020000);
-  if (tid < RW * CH) {
-    const int r = tid / CH, c = tid - CH * r, rg = RW * b + r;
-    if (rg < B)
-      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(sX + r * S::PX + c * 8), rp,
-                                             (rg * H::K0P + c * 8) * (int)sizeof(T), 0, SC1);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave: its rows are performed
-  __syncthreads();
-  if (tid == 0) {
-    const int old = __hip_atomic_fetch_add(counters + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == ngrp - 1;
-    if (last) __hip_atomic_store(counters + g, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next step
-    s_last = last;
-  }
-  __syncthreads();
-  if (!s_last) return;  // block-uniform
-  // the group's 16 rows (rows past the batch: zero), sc1 loads after the barrier above
-  const int r0 = 16 * g;
-  for (int e = tid; e < 16 * CH; e += 512) {
-    const int r = e / CH, c = e - CH * r, rg = r0 + r;
-    u32x4 v = u32x4{0u, 0u, 0u, 0u};
-    if (rg < B) v = __builtin_amdgcn_raw_buffer_load_b128(rp, (rg * H::K0P + c * 8) * (int)sizeof(T), 0, SC1);
-    *reinterpret_cast<u32x4*>(sX + r * S::PX + c * 8) = v;
-  }
-  head16_tile<T>(br, hb, smem, sX, r0, g);  // its first barrier: every row is in sX, the conv regions dead
-}
+// (A single-launch small-batch forward + head -- conv_fwd per image pair, pool2 rows handed to the 16-row
+// group's last-arriving workgroup -- measured SLOWER than conv_fwd + head16 at B = 128: 27.2-33.1 vs 25.7 us per
+// step, bitwise-equal parameters; profiles/r4_session2/ab_lenet_b128_fwd_head_small.txt.  Removed in round 5.)
 
 // ====================================================================================
 // backward
@@ -1612,19 +1550,6 @@ int launch_lenet_fwd_head(DType t, const BatchRef& br, const LenetConvBuffers& c
   const int grid = br.B / 16;
   hipLaunchKernelGGL(fwd_head_kernel<bf16>, dim3(grid), dim3(512), 0, s, br, cb, hb);
   return 32;
-}
-
-int launch_lenet_fwd_head_small(DType t, const BatchRef& br, const LenetConvBuffers& cb, const HeadBuffers& hb,
-                                int* counters, hipStream_t s) {
-#ifndef MNIST_AMD_FWD_HEAD_SMALL  // opt-in build: measured slower than conv_fwd + head16 (see the kernel's comment)
-  (void)t; (void)br; (void)cb; (void)hb; (void)counters; (void)s;
-  return 0;
-#else
-  if (t != DType::BF16 || br.B <= 0 || br.B > FHS_MAX_B || lenet_fwd_head_applies(t, br.B) || !counters) return 0;
-  const int grid = (br.B + 2 * FHS_IPH - 1) / (2 * FHS_IPH);
-  hipLaunchKernelGGL(fwd_head_small_kernel<bf16>, dim3(grid), dim3(512), 0, s, br, cb, hb, counters);
-  return 16;
-#endif
 }
 
 int launch_lenet_head16(DType t, const BatchRef& br, const HeadBuffers& hb, hipStream_t s) {

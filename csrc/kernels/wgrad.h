@@ -23,7 +23,6 @@ struct WgJob {
   const T* dyT;
   const T* xT;
   int N, K, NP, bias, out_off, nblk_k, blk_begin;
-  int gather;  // B operand from the raw uint8 batch rows (WgArgs::gx_rows) instead of read from xT
 };
 template <typename T>
 struct WgArgs {
@@ -39,8 +38,6 @@ struct WgArgs {
   SgdFuse sgd;          // used when fuse != 0 (then splits == 1)
   int fuse;
   unsigned long long* stamps;  // optional phase stamps (MNIST_AMD_STAMPS): slots [STAMP_WGRAD + block][16]
-  const uint8_t* gx_rows;      // gather jobs: the batch's raw uint8 rows [gx_B][784] (HeadBuffers::xrows)
-  int gx_B;
 };
 
 // Weight-gradient GEMM + SGD update for one GPU and ONE batch split (small batches), one 32x32 output tile
@@ -151,15 +148,6 @@ WgArgs<T> make_args(const HeadBuffers& hb, int B, int& splits, float* slab, int 
   };
   int blk = 0;
   mk(0, hb.dy1T, hb.xT, H::N1, H::K0, H::N1P, true, H::W1, blk);
-  const bool gather = hb.xrows != nullptr && (job_mask & 1);
-  if (gather) {
-    // only the LDS-staged MLP bf16 weight gradient gathers (the head skipped its X^T stores for it)
-    if (!std::is_same<Model, MlpModel>::value || sizeof(T) != 2 || fuse)
-      throw std::invalid_argument("wgrad: the raw-row hand-off needs the MLP bf16 LDS-staged weight gradient");
-    a.job[0].gather = 1;
-    a.gx_rows = hb.xrows;
-    a.gx_B = hb.gx_B;
-  }
   mk(1, hb.dy2T, hb.h1T, H::N2, H::N1, H::N2P, true, H::W2, blk);
   mk(2, hb.dy3T, hb.h2T, H::NC, H::N2, H::NCP, H::BIAS3, H::W3, blk);
   if (nj == 0) throw std::invalid_argument("wgrad: empty job mask");

@@ -105,13 +105,6 @@ Trainer::Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const
   for (auto& e : events_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_CHECK(hipMalloc(&zero_counter_, 2 * sizeof(int32_t)));
   HIP_CHECK(hipMemset(zero_counter_, 0, 2 * sizeof(int32_t)));
-#ifdef MNIST_AMD_FWD_HEAD_SMALL
-  if (model_ == ModelKind::LENET) {
-    const size_t ng = size_t(batch_ + 15) / 16;
-    HIP_CHECK(hipMalloc(&group_counter_, ng * sizeof(int32_t)));
-    HIP_CHECK(hipMemset(group_counter_, 0, ng * sizeof(int32_t)));
-  }
-#endif
 }
 
 Trainer::~Trainer() {
@@ -123,7 +116,6 @@ Trainer::~Trainer() {
   if (comm_stream_) hipStreamDestroy(comm_stream_);
   if (aux_stream_) hipStreamDestroy(aux_stream_);
   if (zero_counter_) hipFree(zero_counter_);
-  if (group_counter_) hipFree(group_counter_);
 }
 
 void Trainer::release() {
@@ -214,27 +206,14 @@ HeadBuffers Trainer::head_buffers(float* metrics) const {
   return hb;
 }
 
-void Trainer::set_regather(HeadBuffers& hb, const BatchRef& br, bool fused_wgrad) const {
-#ifdef MNIST_AMD_RAW_ROWS  // opt-in build: measured slower than the bf16 X^T (head.hip wgrad_lds_body, GX)
-  // (not with the small-batch layer-1 split path: there l1_split_kernel, not the head, reads the pixels)
-  if (model_ != ModelKind::MLP || dtype_ != DType::BF16 || fused_wgrad || !p_.xrows || p_.z1p) return;
-  hb.xrows = ptr<uint8_t>(p_.xrows);
-  hb.gx_B = br.B;
-#else
-  (void)hb; (void)br; (void)fused_wgrad;
-#endif
-}
-
 LenetConvBuffers Trainer::conv_buffers(int B) const {
   LenetConvBuffers cb;
   // a training step of B rows whose forward is conv_fwd_kernel (not the fused forward + head) hands conv_bwd
   // its pixel rows in batch order (small batches only: there the index chain is conv_bwd's start-up latency)
-#ifndef MNIST_AMD_FWD_HEAD_SMALL
   if (B > 0 && B <= XB_MAX_B && p_.xb && !fwd_head_active(B)) {
     cb.xb = ptr<uint8_t>(p_.xb);                          // [batch][784] pixel rows
     cb.yb = ptr<uint8_t>(p_.xb) + (size_t)batch_ * 784;   // then [batch] labels
   }
-#endif
   cb.params = ptr<const float>(p_.params);
   cb.pack = ptr<const void>(p_.pack);
   cb.p1 = ptr<void>(p_.p1);
@@ -260,11 +239,9 @@ void Trainer::forward_backward(int B, uintptr_t stream) {
   const BatchRef br = batch_ref(B);
   HeadBuffers hb = head_buffers(ptr<float>(p_.metrics));
   if (model_ == ModelKind::LENET) hb.yb = conv_buffers(B).yb;  // (small batches: labels from conv_fwd_kernel)
-  set_regather(hb, br, false);
   int hrows = 0;
   if (model_ == ModelKind::LENET) {
     if (fwd_head_active(B)) hrows = launch_lenet_fwd_head(dtype_, br, conv_buffers(B), hb, s);
-    else hrows = launch_lenet_fwd_head_small(dtype_, br, conv_buffers(B), hb, group_counter_, s);
     if (!hrows) launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(B), s);
     post_launch(s);
   }
@@ -349,7 +326,6 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
   const float scale = 1.0f / float(B);
   const int cp = model_conv_params(model_);
   const bool comm = use_comm();
-  set_regather(hb, br, model_ == ModelKind::MLP && !comm && fc_splits_ == 1 && fuse_wgrad_sgd_);
   last_stream_ = s;
   // deferred join of the previous step's aux branch: the head overwrites the activations its FC wgrad
   // read and reads the FC weights its FC update wrote (conv_fwd touches neither, so with separate
@@ -367,11 +343,7 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
       join_aux();
       hrows = launch_lenet_fwd_head(dtype_, br, conv_buffers(B), hb, s);
     } else {
-#ifdef MNIST_AMD_FWD_HEAD_SMALL
-      join_aux();  // the opt-in small fused kernel also contains the head
-      hrows = launch_lenet_fwd_head_small(dtype_, br, conv_buffers(B), hb, group_counter_, s);
-#endif
-      if (!hrows) launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(B), s);
+      launch_lenet_conv_fwd(dtype_, true, br, conv_buffers(B), s);
     }
     post_launch(s);
   }
@@ -454,17 +426,10 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     // reduce + SGD covers the conv parameters only (bitwise equal to wgrad -> reduce_sgd over all of them)
     const SgdFuse f{scale, lr_, momentum_, ptr<float>(p_.params), ptr<float>(p_.grad),
                     momentum_ != 0.f ? ptr<float>(p_.mom) : nullptr, ptr<void>(p_.pack), nullptr};
-#ifndef MNIST_AMD_NO_BWD_FC  // (A/B builds only: the FC wgrad + update as its own kernel before conv_bwd)
-    // ... as extra workgroups of the conv_bwd launch (one kernel instead of two)
+    // ... as extra workgroups of the conv_bwd launch (one kernel instead of two; the FC wgrad + update as its own
+    // kernel before conv_bwd measured 31.0 vs 25.8 us per B = 128 step, profiles/r4_session2/NOTES.md)
     const int nslab = launch_lenet_conv_bwd_fc(dtype_, br, conv_buffers(B), hb, f, s, bwd_blocks_);
     post_launch(s);
-#else
-    launch_head_wgrad(model_, dtype_, hb, B, 1, ptr<float>(p_.slab_fc), nparam_, s, hrows, &f);
-    post_launch(s);
-    int nslab = 0;
-    launch_lenet_conv_bwd(dtype_, br, conv_buffers(B), &nslab, s, bwd_blocks_);
-    post_launch(s);
-#endif
     launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
                       nparam_, 1, cp, 0, cp, scale, ptr<float>(p_.params), ptr<float>(p_.grad), ptr<float>(p_.mom),
                       ptr<void>(p_.pack), lr_, momentum_, ptr<int32_t>(p_.step), s);

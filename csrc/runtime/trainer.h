@@ -26,7 +26,6 @@ struct TrainerPtrs {
   uintptr_t xnext = 0, ynext = 0;  // optional: small-batch MLP look-ahead gather buffers (BatchRef)
   uintptr_t xb = 0;     // optional: LeNet [batch][784] uint8 pixel rows + [batch] labels in batch order (conv_fwd ->
                         // conv_bwd / head16)
-  uintptr_t xrows = 0;  // optional: MLP bf16 raw-row hand-off head -> layer-1 wgrad ([batch][784] uint8)
 };
 
 // A gradient bucket = contiguous range of the flat grad slab, all-reduced as one RCCL call as
@@ -157,7 +156,6 @@ class Trainer {
   HeadBuffers head_buffers(float* metrics) const;
   // MLP bf16 training: the head hands the batch's raw uint8 rows to the layer-1 weight gradient instead of a
   // bf16 X^T, unless the step's wgrad is the SGD-fused one (no LDS staging) or no row buffer was given
-  void set_regather(HeadBuffers& hb, const BatchRef& br, bool fused_wgrad) const;
   // B > 0: the buffers of a training step of B rows (cb.xb set when conv_fwd_kernel writes batch-ordered rows)
   LenetConvBuffers conv_buffers(int B = 0) const;
   // defer_join: (single GPU, concurrent schedule, inside a multi-step graph) leave the aux branch (FC
@@ -211,5 +209,4 @@ class Trainer {
   int multi_k_ = 0;
   int zero_step_dev_ = 0;
   int32_t* zero_counter_ = nullptr;  // device {0,0} for eval batch addressing
-  int32_t* group_counter_ = nullptr;  // [ceil(batch / 16)] zeroed: fwd_head_small_kernel hand-off counters
 };

@@ -173,11 +173,6 @@ class NativeTrainer:
         look = model == "mlp" and self.z1p is not None and not os.environ.get("MNIST_AMD_NO_LOOKAHEAD")
         self.xnext = z(_rup(self.batch, 64) * 784, dt=torch.uint8) if look else None
         self.ynext = z(_rup(self.batch, 64), dt=torch.uint8) if look else None
-        # MLP bf16, builds with MNIST_AMD_RAW_ROWS: the head hands its raw uint8 rows to the layer-1 weight
-        # gradient instead of a bf16 X^T (measured slower; csrc/kernels/head.hip wgrad_lds_body)
-        raw = getattr(C, "RAW_ROWS", False) and model == "mlp" and dtype == "bf16"
-        self.xrows = z(self.batch, 784, dt=torch.uint8) if raw else None
-
         # LeNet small batches: conv_fwd's pixel rows in batch order for conv_bwd (no index chain at its start)
         xbm = getattr(C, "XB_MAX_B", 0)
         self.xb = z(self.batch * 785, dt=torch.uint8) if model == "lenet5" and self.batch <= xbm else None  # rows | labels
@@ -192,8 +187,6 @@ class NativeTrainer:
         P.p1, P.m1, P.p2, P.m2, P.dp2 = ptr(self.p1), ptr(self.m1), ptr(self.p2), ptr(self.m2), ptr(self.dp2)
         P.z1p = ptr(self.z1p)
         P.xnext, P.ynext = ptr(self.xnext), ptr(self.ynext)
-        if hasattr(P, "xrows"):  # (A/B runs load older builds through MNIST_AMD_C_PATH)
-            P.xrows = ptr(self.xrows)
         if hasattr(P, "xb"):
             P.xb = ptr(self.xb)
         # MNIST_AMD_STAMPS=1: per-workgroup phase timestamps (wall clock, 100 MHz), 16 slots per workgroup,
