@@ -152,10 +152,11 @@ class NativeTrainer:
         self.xT, self.h1T, self.h2T = z(K0P, self.ld_b), z(N1P, self.ld_b), z(N2P, self.ld_b)
         self.dy1T, self.dy2T, self.dy3T = z(N1P, self.ld_b), z(N2P, self.ld_b), z(16, self.ld_b)
         self.slab_fc = z(fc_splits, self.nparam, dt=torch.float32)
-        # rows for any batch <= self.batch (a partial last batch can need more workgroups than a full one)
-        conv_slabs = C.conv_bwd_max_blocks(self.batch) if model == "lenet5" else 0
+        # conv slab [CONV_PARAMS][ld]: one column per conv_bwd workgroup, for any batch <= self.batch (a partial
+        # last batch can need more workgroups than a full one); the conv update sums each parameter's row
         ncp = C.model_conv_params(mid)
-        self.slab_conv = z(max(conv_slabs, 1), max(ncp, 1), dt=torch.float32)
+        conv_ld = C.conv_slab_ld(self.batch) if model == "lenet5" else 1
+        self.slab_conv = z(max(ncp, 1), conv_ld, dt=torch.float32)
         if model == "lenet5":
             self.p1 = z(self.ld_b * 196 * 8)
             self.m1 = z(self.ld_b * 196 * 8, dt=torch.uint8)
@@ -523,10 +524,12 @@ class NativeTrainer:
                 if ovl:
                     candidates["overlap"] = dict(plan="overlap")
             elif self.model_name == "lenet5" and self.batch <= SMALL_BATCH_SERIAL:
-                # Small LeNet batches: the serial schedule, not calibrated.  run_steps measured serial 32.8 vs
-                # concurrent 35.0 us/step at B=128 (equal at 1024), but inside the calibration the serial
-                # graph timed 38.5 (scripts/calib_probe.py, profiles/r3_session2/NOTES.md): the calibration
-                # would pick the slower schedule.
+                # Small LeNet batches: the serial schedule, not calibrated.  Round 3: run_steps measured serial
+                # 32.8 vs concurrent 35.0 us/step at B=128, but inside the calibration the serial graph timed
+                # 38.6 vs 35.0 -- the calibration picked the slower schedule (profiles/r3_session3/
+                # calib_probe_b128.txt).  Whether it still does with round 4's one-kernel conv_bwd + FC update
+                # (profiles/r4_session2/calib_diag_b128.txt times only the serial form) is measured with
+                # MNIST_AMD_SMALL_SERIAL=0, which turns this rule off (profiles/r5_*/calib_b128*).
                 self.apply_plan({"concurrent": False})
                 return {"chosen": "serial", "timings_ms": {}, "rule": f"batch <= {SMALL_BATCH_SERIAL}"}
             elif self.model_name == "lenet5":

@@ -1,5 +1,8 @@
-"""World-1 latency of the one-shot all-reduce kernel (graph-replayed, median) by block count and size."""
+"""World-1 latency of the one-shot all-reduce kernel (graph-replayed, median) by block count and size, and where a
+call's time goes: per-block wall-clock stamps (entry -> pushes drained -> own flags seen -> slots summed), medians
+over blocks and calls (MNIST_AMD verdict r4 item 4: break the ~14.6 us world-1 floor down)."""
 import os
+import statistics as st
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
@@ -10,8 +13,27 @@ from pytorch_ddp_mnist_amd.parallel.oneshot import time_oneshot  # noqa: E402
 
 C = load_c()
 dev = torch.device("cuda", 0)
-for nblk in (4, 16, 64):
-    o = C.OneShotAllReduce(0, 1, 0, 61706, nblk)
-    for n in (2572, 59134):
+for nblk in (8, 16, 64):
+    o = C.OneShotAllReduce(0, 1, 0, 118272, nblk)
+    for n in (2572, 59134, 118272):
         ms = time_oneshot(o, n, dev, iters=200, warmup=20)
-        print(f"nblk {nblk:3d}  count {n:6d}  {ms * 1000:7.2f} us", flush=True)
+        # phase breakdown (direct launches, stamps on)
+        o.enable_stamps(True)
+        buf = torch.zeros(n, device=dev)
+        s = torch.cuda.current_stream()
+        ph = {"push": [], "flag": [], "sum": [], "span": []}
+        for _ in range(20):
+            o.all_reduce_sum_f32(buf.data_ptr(), n, s.cuda_stream)
+            s.synchronize()
+            t = o.stamps()
+            rows = [t[4 * b:4 * b + 4] for b in range(nblk)]
+            t0 = min(r[0] for r in rows)
+            ph["push"].append(st.median(r[1] - r[0] for r in rows))
+            ph["flag"].append(st.median(r[2] - r[1] for r in rows))
+            ph["sum"].append(st.median(r[3] - r[2] for r in rows))
+            ph["span"].append(max(r[3] for r in rows) - t0)
+        o.enable_stamps(False)
+        med = {k: st.median(v) / 100.0 for k, v in ph.items()}  # 100 MHz ticks -> us
+        print(f"nblk {nblk:3d}  count {n:6d}  replay {ms * 1000:7.2f} us | in-kernel span {med['span']:6.2f}  "
+              f"push {med['push']:5.2f}  flag {med['flag']:5.2f}  sum {med['sum']:5.2f} us", flush=True)
+    assert o.check() == ""
