@@ -72,7 +72,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("fwd_head_applies", [](int dtype, int B) { return lenet_fwd_head_applies(static_cast<DType>(dtype), B); },
         py::arg("dtype"), py::arg("B"));
   m.def("conv_bwd_max_blocks", &lenet_conv_bwd_max_blocks, py::arg("B"), py::arg("target_blocks") = 0);
-  m.def("conv_slab_ld", &lenet_conv_slab_ld, py::arg("B"));
   m.attr("L1_KSPLIT") = L1_KSPLIT;
   m.def("metric_rows", [](int B) { return metric_rows(B); });
   m.attr("L1_SPLIT_MAX_B") = L1_SPLIT_MAX_B;
@@ -174,12 +173,12 @@ PYBIND11_MODULE(_C, m) {
              c.all_reduce_max_f64(reinterpret_cast<double*>(buf), n, reinterpret_cast<hipStream_t>(s));
            })
       .def("time_all_reduce",
-           [](RcclComm& c, uintptr_t buf, size_t n, int warmup, int iters, uintptr_t s, double timeout) {
+           [](RcclComm& c, uintptr_t buf, size_t n, int warmup, int iters, uintptr_t s, double timeout, int per_graph) {
              return c.time_all_reduce(reinterpret_cast<float*>(buf), n, warmup, iters,
-                                      reinterpret_cast<hipStream_t>(s), timeout);
+                                      reinterpret_cast<hipStream_t>(s), timeout, per_graph);
            },
            py::arg("buf"), py::arg("count"), py::arg("warmup"), py::arg("iters"), py::arg("stream"),
-           py::arg("timeout") = 600.0, py::call_guard<py::gil_scoped_release>())
+           py::arg("timeout") = 600.0, py::arg("per_graph") = 1, py::call_guard<py::gil_scoped_release>())
       .def("async_error", &RcclComm::async_error)
       .def("wait_stream",
            [](RcclComm& c, uintptr_t s, double timeout) { return c.wait_stream(reinterpret_cast<hipStream_t>(s), timeout); },

@@ -62,8 +62,7 @@ struct LenetConvBuffers {
   void* p2;              // [B][K0P=416] T pool2 output (NCHW flatten), cols >=400 zero
   uint8_t* m2;           // [B][400]
   const void* dp2;       // [B][416] T   (backward input)
-  float* slab;           // conv partial grads, one COLUMN per workgroup: [CONV_PARAMS][slab_ld] (conv update below)
-  int slab_ld = 0;       // >= workgroups of the launch (lenet_conv_slab_ld)
+  float* slab;           // conv partial grads, row per workgroup: [G][2572]
   // optional [B][784] u8: this step's pixel rows in batch order, written by conv_fwd_kernel (training) and read
   // by conv_bwd instead of re-gathering them through the sample index (small batches: the index chain
   // step counter -> index -> pixels was conv_bwd's start-up latency); null = gather by index
@@ -149,8 +148,6 @@ void launch_lenet_conv_bwd(DType t, const BatchRef& br, const LenetConvBuffers& 
 int launch_lenet_conv_bwd_fc(DType t, const BatchRef& br, const LenetConvBuffers& cb, const HeadBuffers& hb,
                              const SgdFuse& fuse, hipStream_t s, int target_blocks = 0);
 int lenet_conv_bwd_blocks(int B, int target_blocks = 0);
-// row pitch of the conv slab [CONV_PARAMS][ld]: lenet_conv_bwd_max_blocks(B) rounded up to 4 (16-byte rows)
-int lenet_conv_slab_ld(int B);
 int lenet_conv_bwd_max_blocks(int B, int target_blocks = 0);  // slab rows needed for any batch <= B
 
 // One-shot all-reduce over xGMI peer memory (oneshot.hip; host side csrc/runtime/oneshot.h): in-place SUM of
@@ -158,14 +155,6 @@ int lenet_conv_bwd_max_blocks(int B, int target_blocks = 0);  // slab rows neede
 void launch_oneshot_allreduce(float* buf, int count, int rank, int world, int max_count, float* const* peer_data,
                               uint32_t* const* peer_flags, uint32_t* seq, uint32_t* err, int nblk,
                               unsigned long long timeout_ticks, hipStream_t s, unsigned long long* stamps = nullptr);
-
-// LeNet conv parameters from the conv slab ([CONV_PARAMS][ld], column u = conv_bwd workgroup u, nslab columns):
-// grad[p] = scale * sum_u slab[p][u] for every conv parameter p -- one wave per parameter, fixed summation order;
-// launch_conv_update also applies SGD (+momentum), re-packs the conv operand images and optionally bumps the
-// step counters.  `skip`: as launch_sgd_pack.
-void launch_reduce_conv(const float* slab, int ld, int nslab, float scale, float* grad, hipStream_t s);
-void launch_conv_update(DType t, const float* slab, int ld, int nslab, float scale, float* params, float* grad,
-                        float* mom, void* pack, float lr, float momentum, int32_t* step_ptr, hipStream_t s);
 
 // grad[p] = scale * sum_s slab[s][p]  for p in [p0, p1)
 void launch_reduce(const float* slab, int slab_ld, int nslab, int p0, int p1, float scale, float* grad,

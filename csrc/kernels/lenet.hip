@@ -1440,10 +1440,8 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
   }
   stamp(14);
 
-  // ---- write this workgroup's partial gradients (slab column = unit: the conv update sums each parameter's
-  //      partials as one contiguous row, one wave per parameter -- optim.hip conv_update_kernel)
-  const int sld = cb.slab_ld;
-  auto out_at = [&](int q) -> float& { return cb.slab[(size_t)q * sld + unit]; };
+  // ---- write this workgroup's partial gradients (slab row = unit)
+  float* out = cb.slab + (size_t)unit * L::CONV_PARAMS;
 #pragma unroll
   for (int i = 0; i < NWT; ++i) {
     if (i >= nw) break;
@@ -1451,8 +1449,8 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = grp * 4 + r;
-      if (kcol < 150) out_at(L::CW2 + n * 150 + c * 25 + tap) = accW2[i][r];
-      else if (kcol == 150) out_at(L::CB2 + n) = accW2[i][r];
+      if (kcol < 150) out[L::CW2 + n * 150 + c * 25 + tap] = accW2[i][r];
+      else if (kcol == 150) out[L::CB2 + n] = accW2[i][r];
     }
   }
 #pragma unroll
@@ -1469,10 +1467,10 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
     const int r = C_AMAP[m] >> 3, n = C_AMAP[m] & 7, bj = C_BMAP[j];
     if (n < 6) {
       if (bj == 15) {
-        if (r == 0) out_at(L::CB1 + n) = v;
+        if (r == 0) out[L::CB1 + n] = v;
       } else {
         const int kh = 2 * (bj / 5) + r, kw = bj % 5;
-        if (kh <= 4) out_at(L::CW1 + n * 25 + kh * 5 + kw) = v;
+        if (kh <= 4) out[L::CW1 + n * 25 + kh * 5 + kw] = v;
       }
     }
   }
@@ -1526,8 +1524,6 @@ int lenet_conv_bwd_max_blocks(int B, int target) {
   // MAX_IPB caps the images per workgroup, so huge batches use more than `target` workgroups
   return std::max({1, std::min(B, target > 0 ? target : default_bwd_target()), (B + MAX_IPB - 1) / MAX_IPB});
 }
-
-int lenet_conv_slab_ld(int B) { return (std::max(1, lenet_conv_bwd_max_blocks(B, 0)) + 3) / 4 * 4; }
 
 void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetConvBuffers& cb, hipStream_t s) {
   if (br.B <= 0) return;

@@ -203,53 +203,6 @@ __global__ __launch_bounds__(256) void reduce_sgd_direct_kernel(const float* __r
   }
 }
 
-// LeNet conv update from the conv slab [CONV_PARAMS][ld] (column u = conv_bwd workgroup u): ONE wave per
-// parameter sums its contiguous row of nslab partials -- 16-byte loads, 643 four-wave blocks for the 2572
-// conv parameters, so every CU takes part (the row-per-workgroup slab was summed by 41 sixteen-wave blocks,
-// 4.6-5.5 us per step) -- in a fixed order: each lane its float4s in order, then the DPP row butterfly and the
-// fixed combine of the four rows (wave_sum).  SGD: + momentum / parameter / packed operand images, as
-// reduce_sgd_kernel.  Block 0 bumps the step counters when asked.
-template <class Model, typename T, bool SGD>
-__global__ __launch_bounds__(256) void conv_update_kernel(const float* __restrict__ slab, int ld, int nslab, int n,
-                                                          float scale, float* __restrict__ params,
-                                                          float* __restrict__ grad, float* __restrict__ mom,
-                                                          T* __restrict__ pack, float lr, float mu, int32_t* step_ptr) {
-  const int lane = threadIdx.x & 63, p = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (SGD && step_ptr && blockIdx.x == 0 && threadIdx.x == 0) {
-    step_ptr[0] += 1;
-    step_ptr[1] += 1;
-  }
-  if (p >= n) return;  // wave-uniform
-  float pv = 0.f, mv = 0.f;
-  if (SGD && lane == 0) {  // the update's operands, in flight with the slab loads
-    pv = params[p];
-    if (mom) mv = mom[p];
-  }
-  const float* row = slab + (size_t)p * ld;
-  const int nv = nslab >> 2;
-  float s = 0.f;
-  for (int j = lane; j < nv; j += 64) {
-    const f32x4 x = *reinterpret_cast<const f32x4*>(row + 4 * j);
-    s += (x[0] + x[1]) + (x[2] + x[3]);
-  }
-  if (lane < (nslab & 3)) s += row[4 * nv + lane];
-  s = wave_sum(s);
-  if (lane == 0) {
-    float g = s * scale;
-    grad[p] = g;
-    if constexpr (SGD) {
-      if (mom) {
-        const float b = mu * mv + g;
-        mom[p] = b;
-        g = b;
-      }
-      const float v = pv - lr * g;
-      params[p] = v;
-      Packer<Model, T>::pack(p, v, pack);
-    }
-  }
-}
-
 template <class Model, typename T>
 void reduce_sgd_t(const float* sa, int lda, int na, const float* sb, int ldb, int nb, int split, int p0, int n, float scale,
                   float* params, float* grad, float* mom, void* pack, float lr, float mu, int32_t* step_ptr,
@@ -292,24 +245,6 @@ __global__ __launch_bounds__(256) void gather_normalize_kernel(BatchRef br, T* o
 }
 
 }  // namespace
-
-void launch_reduce_conv(const float* slab, int ld, int nslab, float scale, float* grad, hipStream_t s) {
-  constexpr int n = LenetModel::CONV_PARAMS;
-  hipLaunchKernelGGL((conv_update_kernel<LenetModel, float, false>), dim3((n + 3) / 4), dim3(256), 0, s, slab, ld, nslab,
-                     n, scale, nullptr, grad, nullptr, nullptr, 0.f, 0.f, nullptr);
-}
-
-void launch_conv_update(DType t, const float* slab, int ld, int nslab, float scale, float* params, float* grad,
-                        float* mom, void* pack, float lr, float momentum, int32_t* step_ptr, hipStream_t s) {
-  constexpr int n = LenetModel::CONV_PARAMS;
-  float* mb = momentum != 0.f ? mom : nullptr;
-  if (t == DType::F32)
-    hipLaunchKernelGGL((conv_update_kernel<LenetModel, float, true>), dim3((n + 3) / 4), dim3(256), 0, s, slab, ld, nslab,
-                       n, scale, params, grad, mb, reinterpret_cast<float*>(pack), lr, momentum, step_ptr);
-  else
-    hipLaunchKernelGGL((conv_update_kernel<LenetModel, bf16, true>), dim3((n + 3) / 4), dim3(256), 0, s, slab, ld, nslab,
-                       n, scale, params, grad, mb, reinterpret_cast<bf16*>(pack), lr, momentum, step_ptr);
-}
 
 void launch_reduce(const float* slab, int slab_ld, int nslab, int p0, int p1, float scale, float* grad,
                    hipStream_t s) {

@@ -2,6 +2,7 @@
 
 #include "../kernels/launch.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -169,13 +170,16 @@ void RcclComm::all_reduce_max_f64(double* buf, size_t count, hipStream_t s) {
 }
 
 std::vector<float> RcclComm::time_all_reduce(float* buf, size_t count, int warmup, int iters, hipStream_t s,
-                                             double timeout_s) {
+                                             double timeout_s, int per_graph) {
   if (count == 0 || iters <= 0) return {};
   if (!comm_) throw std::runtime_error("RcclComm: communicator destroyed / aborted");
+  per_graph = std::max(1, per_graph);
   hipGraph_t g = nullptr;
   hipGraphExec_t ge = nullptr;
   HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeRelaxed));
-  ncclResult_t r = ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm_, s);
+  ncclResult_t r = ncclSuccess;
+  for (int i = 0; i < per_graph && (r == ncclSuccess || r == ncclInProgress); ++i)
+    r = ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm_, s);
   HIP_CHECK(hipStreamEndCapture(s, &g));
   if (r != ncclSuccess && r != ncclInProgress) {
     hipGraphDestroy(g);
@@ -195,7 +199,10 @@ std::vector<float> RcclComm::time_all_reduce(float* buf, size_t count, int warmu
   std::vector<float> out;
   if (err.empty()) {
     out.resize(iters);
-    for (int i = 0; i < iters; ++i) HIP_CHECK(hipEventElapsedTime(&out[i], ev[i], ev[i + 1]));
+    for (int i = 0; i < iters; ++i) {
+      HIP_CHECK(hipEventElapsedTime(&out[i], ev[i], ev[i + 1]));
+      out[i] /= float(per_graph);
+    }
   }
   if (err.empty()) {
     for (auto& e : ev) hipEventDestroy(e);

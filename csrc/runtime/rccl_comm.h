@@ -35,12 +35,13 @@ class RcclComm {
   void all_reduce_sum_f32(float* buf, size_t count, hipStream_t s);
   void broadcast_f32(float* buf, size_t count, int root, hipStream_t s);
   void all_reduce_max_f64(double* buf, size_t count, hipStream_t s);
-  // Latency of ONE sum all-reduce of `count` floats at `buf`, as the step graph issues it: the call is
-  // captured into its own hipGraph and replayed `warmup` + `iters` times back to back on `s`; returns the
-  // `iters` per-replay times in ms (events between replays).  Collective: every rank must call it with
-  // the same count, in the same order.  Waits through wait_stream (throws on an RCCL error / timeout).
+  // Latency of ONE sum all-reduce of `count` floats at `buf`, as the step graph issues it: `per_graph` calls are
+  // captured back to back into one hipGraph (so the host's graph-launch rate, ~10 us per replay, does not set the
+  // figure), replayed `warmup` + `iters` times on `s`; returns the `iters` per-call times in ms (events between
+  // replays / per_graph).  Collective: every rank must call it with the same count, in the same order.  Waits
+  // through wait_stream (throws on an RCCL error / timeout).
   std::vector<float> time_all_reduce(float* buf, size_t count, int warmup, int iters, hipStream_t s,
-                                     double timeout_s);
+                                     double timeout_s, int per_graph = 1);
   // Capture probe of the pattern the SPLIT plan was built to avoid (ROCm 7.0 segfaulted in hipStreamEndCapture on a
   // related form): inside ONE captured graph a side stream runs the all-reduce, a THIRD stream waits on an event
   // recorded behind it and runs a kernel, the capturing stream joins that stream; the graph is instantiated and

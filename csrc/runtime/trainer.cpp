@@ -95,7 +95,6 @@ Trainer::Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const
   if (ld_b < ((batch + 63) / 64) * 64) throw std::invalid_argument("ld_b must be >= batch rounded up to 64");
   nparam_ = model_nparam(model_);
   max_conv_slabs_ = model_ == ModelKind::LENET ? lenet_conv_bwd_max_blocks(batch_, 0) : 0;
-  conv_ld_ = model_ == ModelKind::LENET ? lenet_conv_slab_ld(batch_) : 0;
   concurrent_ = concurrent_mode() != 0;
   const int ps = model_phase_split(model_);  // default buckets: one per backward phase (see Plan)
   buckets_.push_back({ps, nparam_, 0});
@@ -223,7 +222,6 @@ LenetConvBuffers Trainer::conv_buffers(int B) const {
   cb.m2 = ptr<uint8_t>(p_.m2);
   cb.dp2 = ptr<const void>(p_.dp2);
   cb.slab = ptr<float>(p_.slab_conv);
-  cb.slab_ld = conv_ld_;
   cb.ablate = ablation_mask("MNIST_AMD_ABLATE");
   // stamps layout: launch.h STAMP_* (the conv kernels address their rows relative to STAMP_CONV_BWD)
   cb.stamps = p_.stamps ? ptr<unsigned long long>(p_.stamps) + STAMP_CONV_BWD * 16 : nullptr;
@@ -275,8 +273,7 @@ void Trainer::reduce_grads(int B, uintptr_t stream) {
   launch_reduce(ptr<const float>(p_.slab_fc), nparam_, splits, cp, nparam_, scale, ptr<float>(p_.grad), s);
   post_launch(s);
   if (cp > 0) {
-    launch_reduce_conv(ptr<const float>(p_.slab_conv), conv_ld_, lenet_conv_bwd_blocks(B, bwd_blocks_), scale,
-                       ptr<float>(p_.grad), s);
+    launch_reduce(ptr<const float>(p_.slab_conv), cp, lenet_conv_bwd_blocks(B, bwd_blocks_), 0, cp, scale, ptr<float>(p_.grad), s);
     post_launch(s);
   }
 }
@@ -403,7 +400,10 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     // kernel reads): with defer_join it follows conv_bwd directly, the join moves to the next head
     if (defer_join) aux_pending_ = true;
     else HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));
-    conv_update(nslab, scale, ptr<int32_t>(p_.step), s);
+    launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
+                      nparam_, splits, cp, 0, cp, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
+                      ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, ptr<int32_t>(p_.step), s);
+    post_launch(s);
     return;
   }
 
@@ -430,7 +430,10 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     // kernel before conv_bwd measured 31.0 vs 25.8 us per B = 128 step, profiles/r4_session2/NOTES.md)
     const int nslab = launch_lenet_conv_bwd_fc(dtype_, br, conv_buffers(B), hb, f, s, bwd_blocks_);
     post_launch(s);
-    conv_update(nslab, scale, ptr<int32_t>(p_.step), s);
+    launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
+                      nparam_, 1, cp, 0, cp, scale, ptr<float>(p_.params), ptr<float>(p_.grad), ptr<float>(p_.mom),
+                      ptr<void>(p_.pack), lr_, momentum_, ptr<int32_t>(p_.step), s);
+    post_launch(s);
     return;
   }
   const int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s, hrows);
@@ -440,18 +443,10 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     launch_lenet_conv_bwd(dtype_, br, conv_buffers(B), &nslab, s, bwd_blocks_);
     post_launch(s);
   }
-  // no communicator: fused reduce + SGD + pack (2 boundaries fewer than reduce -> sgd): LeNet's conv range from the
-  // conv slab, then the FC range (MLP: every parameter) in ONE kernel, which also bumps the step counters
-  if (cp > 0) conv_update(nslab, scale, nullptr, s);
-  launch_reduce_sgd(model_, dtype_, nullptr, 0, 0, ptr<const float>(p_.slab_fc), nparam_, splits, cp, cp, nparam_,
-                    scale, ptr<float>(p_.params), ptr<float>(p_.grad), ptr<float>(p_.mom), ptr<void>(p_.pack), lr_,
-                    momentum_, ptr<int32_t>(p_.step), s);
-  post_launch(s);
-}
-
-void Trainer::conv_update(int nslab, float scale, int32_t* step, hipStream_t s) {
-  launch_conv_update(dtype_, ptr<const float>(p_.slab_conv), conv_ld_, nslab, scale, ptr<float>(p_.params),
-                     ptr<float>(p_.grad), ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, step, s);
+  // no communicator: ONE fused reduce + SGD + pack kernel (2 boundaries fewer than reduce -> sgd)
+  launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
+                    nparam_, splits, cp, 0, nparam_, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
+                    ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, ptr<int32_t>(p_.step), s);
   post_launch(s);
 }
 
@@ -515,7 +510,7 @@ void Trainer::launch_lenet_comm_tail(int B, int nslab, int splits, hipStream_t s
   post_launch(aux_stream_);
   HIP_CHECK(hipEventRecord(events_[5], aux_stream_));
   if (plan_ == Plan::JOIN) {
-    launch_reduce_conv(ptr<const float>(p_.slab_conv), conv_ld_, nslab, scale, g, s);
+    launch_reduce(ptr<const float>(p_.slab_conv), cp, nslab, 0, cp, scale, g, s);
     post_launch(s);
     HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));
     all_reduce(coalesced_buckets(), -1, s);
@@ -532,7 +527,7 @@ void Trainer::launch_lenet_comm_tail(int B, int nslab, int splits, hipStream_t s
   trace("split: comm AR(FC) + update(FC)");
   comm_phase(0, events_[5], false);
   trace("split: reduce(conv)");
-  launch_reduce_conv(ptr<const float>(p_.slab_conv), conv_ld_, nslab, scale, g, s);
+  launch_reduce(ptr<const float>(p_.slab_conv), cp, nslab, 0, cp, scale, g, s);
   post_launch(s);
   HIP_CHECK(hipEventRecord(events_[1], s));
   trace("split: comm AR(conv) + update(conv)");
@@ -559,7 +554,7 @@ void Trainer::launch_lenet_overlap(int B, int nslab, hipStream_t s, const HeadBu
                         lr_, momentum_, gs, nullptr, aux_stream_, ov_fc_->err_word());
   post_launch(aux_stream_);
   HIP_CHECK(hipEventRecord(events_[5], aux_stream_));
-  launch_reduce_conv(ptr<const float>(p_.slab_conv), conv_ld_, nslab, scale, g, s);
+  launch_reduce(ptr<const float>(p_.slab_conv), cp, nslab, 0, cp, scale, g, s);
   post_launch(s);
   ov_conv_->all_reduce_sum_f32(g, size_t(cp), s);
   launch_sgd_pack_range(model_, dtype_, ptr<float>(p_.params), g, ptr<float>(p_.mom), ptr<void>(p_.pack), 0, cp, lr_,

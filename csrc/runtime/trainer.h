@@ -158,8 +158,6 @@ class Trainer {
   // bf16 X^T, unless the step's wgrad is the SGD-fused one (no LDS staging) or no row buffer was given
   // B > 0: the buffers of a training step of B rows (cb.xb set when conv_fwd_kernel writes batch-ordered rows)
   LenetConvBuffers conv_buffers(int B = 0) const;
-  // LeNet conv-range reduce + SGD + pack from the conv slab (launch_conv_update); `step`: bump the counters
-  void conv_update(int nslab, float scale, int32_t* step, hipStream_t s);
   // defer_join: (single GPU, concurrent schedule, inside a multi-step graph) leave the aux branch (FC
   // wgrad + FC update) un-joined at the end of the step; the NEXT step's head waits for it instead.
   void launch_step(int B, hipStream_t s, bool defer_join = false);
@@ -198,7 +196,6 @@ class Trainer {
   bool comm_enabled_ = true;
   hipStream_t last_stream_ = nullptr;  // stream of the last graph launch / capture (drained by invalidate)
   int bwd_blocks_ = 0;
-  int conv_ld_ = 0;         // row pitch of the conv slab [CONV_PARAMS][conv_ld_] (lenet_conv_slab_ld)
   int max_conv_slabs_ = 0;  // rows of the conv slab (lenet_conv_bwd_max_blocks(batch) at the default target)
   std::shared_ptr<RcclComm> comm_;
   std::shared_ptr<OneShotAllReduce> oneshot_;

@@ -33,6 +33,10 @@ from ..ops.native import require_gpu
 from ..parallel.comm import comm_timeout  # noqa: F401  (re-exported: watchdog deadline)
 
 PLANS = {"join": 0, "split": 1, "overlap": 2}
+# standalone collective latencies (comm_profile) are timed as graphs of this many back-to-back calls: one call per
+# graph measured the host's graph-launch rate (~15 us per replay) instead of the collective -- the one-shot kernel's
+# in-kernel span is ~4.5 us at world 1 (profiles/r5_session1/prof1/oneshot_lat.txt)
+STANDALONE_CALLS_PER_GRAPH = 8
 
 
 def resolve_plan(name: Optional[str]) -> Optional[str]:
@@ -75,8 +79,11 @@ def calib_blocks(avail: int, k: int, multi: bool):
     return bool(multi), blk, seg, per
 
 
-# single-GPU LeNet batches up to this size use the serial schedule without calibration (autotune_plan)
-SMALL_BATCH_SERIAL = int(os.environ.get("MNIST_AMD_SMALL_SERIAL", "1024"))
+# (Rounds 3-4 pinned the serial schedule for single-GPU LeNet batches <= 1024 because the calibration had timed
+#  it wrong at B = 128 (profiles/r3_session3/calib_probe_b128.txt).  Round 5, same box: the calibration now picks
+#  serial at B = 128 itself (bf16 0.0301 vs 0.0345 ms, fp32 0.0498 vs 0.0547) and concurrent at B = 1024, where
+#  the pinned serial schedule was 10 % slower (47.7 vs 52.4 us per step): profiles/r5_session1/calib_b128_auto.jsonl.
+#  The rule is gone; every single-GPU LeNet batch is calibrated.)
 
 
 class CollectiveError(RuntimeError):
@@ -152,11 +159,13 @@ class NativeTrainer:
         self.xT, self.h1T, self.h2T = z(K0P, self.ld_b), z(N1P, self.ld_b), z(N2P, self.ld_b)
         self.dy1T, self.dy2T, self.dy3T = z(N1P, self.ld_b), z(N2P, self.ld_b), z(16, self.ld_b)
         self.slab_fc = z(fc_splits, self.nparam, dt=torch.float32)
-        # conv slab [CONV_PARAMS][ld]: one column per conv_bwd workgroup, for any batch <= self.batch (a partial
-        # last batch can need more workgroups than a full one); the conv update sums each parameter's row
+        # rows for any batch <= self.batch (a partial last batch can need more workgroups than a full one).
+        # (Round 5 measured the transposed layout -- one slab column per workgroup, one wave per parameter in the
+        # conv update -- and reverted it: conv_bwd's scattered column stores cost 50.7 -> 54.4 us at B = 8192
+        # and the update did not get faster (5.5 -> 5.1 us; B = 128 4.6 -> 4.7 us): profiles/r5_session1/NOTES.md.)
+        conv_slabs = C.conv_bwd_max_blocks(self.batch) if model == "lenet5" else 0
         ncp = C.model_conv_params(mid)
-        conv_ld = C.conv_slab_ld(self.batch) if model == "lenet5" else 1
-        self.slab_conv = z(max(ncp, 1), conv_ld, dt=torch.float32)
+        self.slab_conv = z(max(conv_slabs, 1), max(ncp, 1), dt=torch.float32)
         if model == "lenet5":
             self.p1 = z(self.ld_b * 196 * 8)
             self.m1 = z(self.ld_b * 196 * 8, dt=torch.uint8)
@@ -523,15 +532,6 @@ class NativeTrainer:
                     candidates = {k: v for k, v in candidates.items() if v.get("plan", "join") == "join"}
                 if ovl:
                     candidates["overlap"] = dict(plan="overlap")
-            elif self.model_name == "lenet5" and self.batch <= SMALL_BATCH_SERIAL:
-                # Small LeNet batches: the serial schedule, not calibrated.  Round 3: run_steps measured serial
-                # 32.8 vs concurrent 35.0 us/step at B=128, but inside the calibration the serial graph timed
-                # 38.6 vs 35.0 -- the calibration picked the slower schedule (profiles/r3_session3/
-                # calib_probe_b128.txt).  Whether it still does with round 4's one-kernel conv_bwd + FC update
-                # (profiles/r4_session2/calib_diag_b128.txt times only the serial form) is measured with
-                # MNIST_AMD_SMALL_SERIAL=0, which turns this rule off (profiles/r5_*/calib_b128*).
-                self.apply_plan({"concurrent": False})
-                return {"chosen": "serial", "timings_ms": {}, "rule": f"batch <= {SMALL_BATCH_SERIAL}"}
             elif self.model_name == "lenet5":
                 candidates = local_plan_candidates(fwd_head=self.fwd_head_applies())
             else:
@@ -589,8 +589,9 @@ class NativeTrainer:
                 buf = torch.zeros(b - a, dtype=torch.float32, device=self.device)
                 self._sync_in()
                 try:
+                    # 8 calls per graph: the per-call figure, not the host's graph-launch rate
                     ts = self.comm.time_all_reduce(buf.data_ptr(), b - a, warmup, iters, self.stream.cuda_stream,
-                                                   comm_timeout())
+                                                   comm_timeout(), per_graph=STANDALONE_CALLS_PER_GRAPH)
                 except RuntimeError as e:
                     self.comm.abort()
                     raise CollectiveError(f"rank {self.comm.rank}: {e} (communicator aborted)") from e
@@ -602,7 +603,8 @@ class NativeTrainer:
                                                                   (self.overlap[0] if self.overlap else None))
             if os_ is not None:
                 from ..parallel.oneshot import time_oneshot
-                med = time_oneshot(os_, b - a, self.device, iters=iters, warmup=warmup)
+                med = time_oneshot(os_, b - a, self.device, iters=iters, warmup=warmup,
+                                   per_graph=STANDALONE_CALLS_PER_GRAPH)
                 med = reduce_max(med) if reduce_max is not None else med
                 row["oneshot_us"] = round(med * 1000.0, 2)
             colls.append(row)

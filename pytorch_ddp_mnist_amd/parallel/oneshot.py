@@ -67,15 +67,17 @@ def make_oneshot(ctx, max_count: int, nblk: int = 64, timeout_s: Optional[float]
     return o
 
 
-def time_oneshot(o, count: int, device, iters: int = 48, warmup: int = 8):
-    """Latency (ms) of ONE one-shot all-reduce of ``count`` floats, as the step graph issues it: captured into a
-    graph and replayed back to back (median; collective -- every rank calls it)."""
+def time_oneshot(o, count: int, device, iters: int = 48, warmup: int = 8, per_graph: int = 1):
+    """Latency (ms) of ONE one-shot all-reduce of ``count`` floats, as the step graph issues it: ``per_graph`` calls
+    captured back to back into a graph, replayed back to back (median per call; collective -- every rank calls it).
+    With one call per graph the figure is the host's graph-launch rate (~15 us), not the kernel."""
     buf = torch.zeros(count, dtype=torch.float32, device=device)
     s = torch.cuda.Stream(device=device)
     s.wait_stream(torch.cuda.current_stream(device))
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g, stream=s):
-        o.all_reduce_sum_f32(buf.data_ptr(), count, torch.cuda.current_stream(device).cuda_stream)
+        for _ in range(max(1, per_graph)):
+            o.all_reduce_sum_f32(buf.data_ptr(), count, torch.cuda.current_stream(device).cuda_stream)
     with torch.cuda.stream(s):
         for _ in range(warmup):
             g.replay()
@@ -88,7 +90,7 @@ def time_oneshot(o, count: int, device, iters: int = 48, warmup: int = 8):
     err = o.check()
     if err:
         raise RuntimeError(err)
-    ts = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(iters))
+    ts = sorted(ev[i].elapsed_time(ev[i + 1]) / max(1, per_graph) for i in range(iters))
     return ts[len(ts) // 2]
 
 

@@ -16,7 +16,8 @@ dev = torch.device("cuda", 0)
 for nblk in (8, 16, 64):
     o = C.OneShotAllReduce(0, 1, 0, 118272, nblk)
     for n in (2572, 59134, 118272):
-        ms = time_oneshot(o, n, dev, iters=200, warmup=20)
+        ms1 = time_oneshot(o, n, dev, iters=100, warmup=10)  # one call per graph: the host's launch rate
+        ms = time_oneshot(o, n, dev, iters=100, warmup=10, per_graph=8)
         # phase breakdown (direct launches, stamps on)
         o.enable_stamps(True)
         buf = torch.zeros(n, device=dev)
@@ -34,6 +35,17 @@ for nblk in (8, 16, 64):
             ph["span"].append(max(r[3] for r in rows) - t0)
         o.enable_stamps(False)
         med = {k: st.median(v) / 100.0 for k, v in ph.items()}  # 100 MHz ticks -> us
-        print(f"nblk {nblk:3d}  count {n:6d}  replay {ms * 1000:7.2f} us | in-kernel span {med['span']:6.2f}  "
+        print(f"nblk {nblk:3d}  count {n:6d}  per call {ms * 1000:6.2f} us (1/graph {ms1 * 1000:6.2f}) | in-kernel span {med['span']:6.2f}  "
               f"push {med['push']:5.2f}  flag {med['flag']:5.2f}  sum {med['sum']:5.2f} us", flush=True)
     assert o.check() == ""
+
+# RCCL at world 1 for comparison (its collective is a local copy there), same per-call method
+comm = C.RcclComm(C.RcclComm.make_unique_id(), 0, 1, 0)
+s = torch.cuda.Stream()
+for n in (2572, 59134, 118272):
+    buf = torch.zeros(n, device=dev)
+    s.wait_stream(torch.cuda.current_stream())
+    one = st.median(comm.time_all_reduce(buf.data_ptr(), n, 10, 100, s.cuda_stream, 60.0, per_graph=1))
+    per = st.median(comm.time_all_reduce(buf.data_ptr(), n, 10, 100, s.cuda_stream, 60.0, per_graph=8))
+    print(f"rccl world 1  count {n:6d}  per call {per * 1000:6.2f} us (1/graph {one * 1000:6.2f})", flush=True)
+assert comm.destroy(60.0) == ""
