@@ -96,6 +96,10 @@ Trainer::Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const
   nparam_ = model_nparam(model_);
   max_conv_slabs_ = model_ == ModelKind::LENET ? lenet_conv_bwd_max_blocks(batch_, 0) : 0;
   concurrent_ = concurrent_mode() != 0;
+  {  // MNIST_AMD_WGRAD_TAIL=0: the MLP weight gradient's separate reduce + SGD kernel instead of the tail update
+    const char* e = std::getenv("MNIST_AMD_WGRAD_TAIL");
+    wgrad_tail_ = !(e && *e == '0');
+  }
   const int ps = model_phase_split(model_);  // default buckets: one per backward phase (see Plan)
   buckets_.push_back({ps, nparam_, 0});
   buckets_.push_back({0, ps, 1});
@@ -105,6 +109,8 @@ Trainer::Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const
   for (auto& e : events_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_CHECK(hipMalloc(&zero_counter_, 2 * sizeof(int32_t)));
   HIP_CHECK(hipMemset(zero_counter_, 0, 2 * sizeof(int32_t)));
+  HIP_CHECK(hipMalloc(&tail_cnt_, TAIL_MAX_TILES * sizeof(int32_t)));  // wgrad tail arrival counters (MLP)
+  HIP_CHECK(hipMemset(tail_cnt_, 0, TAIL_MAX_TILES * sizeof(int32_t)));
 }
 
 Trainer::~Trainer() {
@@ -116,6 +122,7 @@ Trainer::~Trainer() {
   if (comm_stream_) hipStreamDestroy(comm_stream_);
   if (aux_stream_) hipStreamDestroy(aux_stream_);
   if (zero_counter_) hipFree(zero_counter_);
+  if (tail_cnt_) hipFree(tail_cnt_);
 }
 
 void Trainer::release() {
@@ -131,6 +138,15 @@ void Trainer::release() {
   ov_fc_.reset();
   ov_conv_.reset();
   if (plan_ == Plan::OVERLAP) plan_ = Plan::JOIN;
+}
+
+int Trainer::fc_splits_for(int B) const {
+  // the batch-split count launch_head_wgrad actually uses for B rows (wg::make_args)
+  const int KC = dtype_ == DType::BF16 ? 32 : 16;
+  const int Bp = (B + KC - 1) / KC * KC;
+  int splits = std::max(1, std::min(fc_splits_, Bp / KC));
+  const int rlen = ((Bp + splits - 1) / splits + KC - 1) / KC * KC;
+  return (Bp + rlen - 1) / rlen;
 }
 
 int Trainer::pack_size() const { return model_pack_size(model_); }
@@ -264,12 +280,7 @@ void Trainer::reduce_grads(int B, uintptr_t stream) {
   const int cp = model_conv_params(model_);
   const HeadBuffers hb = head_buffers(ptr<float>(p_.metrics));
   (void)hb;
-  // the split count actually used by launch_head_wgrad for this B
-  const int KC = dtype_ == DType::BF16 ? 32 : 16;
-  const int Bp = (B + KC - 1) / KC * KC;
-  int splits = std::max(1, std::min(fc_splits_, Bp / KC));
-  const int rlen = ((Bp + splits - 1) / splits + KC - 1) / KC * KC;
-  splits = (Bp + rlen - 1) / rlen;
+  const int splits = fc_splits_for(B);
   launch_reduce(ptr<const float>(p_.slab_fc), nparam_, splits, cp, nparam_, scale, ptr<float>(p_.grad), s);
   post_launch(s);
   if (cp > 0) {
@@ -417,6 +428,15 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
                     momentum_ != 0.f ? ptr<float>(p_.mom) : nullptr,  // as launch_reduce_sgd
                     ptr<void>(p_.pack), ptr<int32_t>(p_.step)};
     launch_head_wgrad(model_, dtype_, hb, B, 1, ptr<float>(p_.slab_fc), nparam_, s, hrows, &f);
+    post_launch(s);
+    return;
+  }
+  if (model_ == ModelKind::MLP && fuse_wgrad_sgd_ && wgrad_tail_ && fc_splits_for(B) % 8 == 0) {
+    // one GPU, several batch splits: each output tile's last-arriving split sums the tile's partials and applies
+    // the update (head.hip wgrad_tail) -- no reduce + SGD kernel, no boundary; bitwise equal to wgrad -> reduce_sgd
+    const SgdFuse f{scale, lr_, momentum_, ptr<float>(p_.params), ptr<float>(p_.grad),
+                    momentum_ != 0.f ? ptr<float>(p_.mom) : nullptr, ptr<void>(p_.pack), ptr<int32_t>(p_.step)};
+    launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s, hrows, &f, 7, tail_cnt_);
     post_launch(s);
     return;
   }

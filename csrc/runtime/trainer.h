@@ -158,6 +158,7 @@ class Trainer {
   // bf16 X^T, unless the step's wgrad is the SGD-fused one (no LDS staging) or no row buffer was given
   // B > 0: the buffers of a training step of B rows (cb.xb set when conv_fwd_kernel writes batch-ordered rows)
   LenetConvBuffers conv_buffers(int B = 0) const;
+  int fc_splits_for(int B) const;  // FC weight-gradient batch splits used for B rows
   // defer_join: (single GPU, concurrent schedule, inside a multi-step graph) leave the aux branch (FC
   // wgrad + FC update) un-joined at the end of the step; the NEXT step's head waits for it instead.
   void launch_step(int B, hipStream_t s, bool defer_join = false);
@@ -209,4 +210,6 @@ class Trainer {
   int multi_k_ = 0;
   int zero_step_dev_ = 0;
   int32_t* zero_counter_ = nullptr;  // device {0,0} for eval batch addressing
+  bool wgrad_tail_ = true;            // MLP single GPU, several splits: update by each tile's last arriver
+  int32_t* tail_cnt_ = nullptr;      // [TAIL_MAX_TILES] MLP wgrad tail arrival counters (zero between launches)
 };

@@ -34,9 +34,10 @@ ap.add_argument("--steps", type=int, default=4)
 ap.add_argument("--model", default="lenet5", choices=["lenet5", "mlp"])
 ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
 a = ap.parse_args()
-x, y = make_split(4096, seed=7)
+N = max(4096, a.batch * a.steps)  # (4096 for the default shapes: their digests are unchanged)
+x, y = make_split(N, seed=7)
 C = load_c()
-order = torch.randperm(4096, generator=torch.Generator().manual_seed(1)).to(torch.int32)
+order = torch.randperm(N, generator=torch.Generator().manual_seed(1)).to(torch.int32)
 
 for v in a.variants:
     m = re.fullmatch(r"(local_halflr|local|join|split|overlap)(?:_b(\d+))?(_w2)?(?:_k(\d+))?", v)

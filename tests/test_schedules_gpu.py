@@ -62,3 +62,14 @@ def test_mlp_schedules_bitwise_equal(native):
     for k in ("join", "split", "split_k4"):
         assert d[k] == d["local"], k
     assert d["join_w2"] == d["local_halflr"] and d["split_w2"] == d["local_halflr"]
+
+
+@pytest.mark.timeout(600)
+def test_mlp_wgrad_tail_bitwise_equal(native):
+    """MLP bf16 at B = 4096 (8 FC batch splits): the single-GPU step's update by each output tile's last-arriving
+    split (head.hip wgrad_tail) is bitwise the separate reduce + SGD kernel (MNIST_AMD_WGRAD_TAIL=0), the world-1
+    JOIN plan (reduce -> all-reduce -> SGD) and the 4-step graph."""
+    extra = ("--batch", "4096", "--dtype", "bf16")
+    tail = _digests({}, ["local", "join", "local_k4"], model="mlp", extra=extra)
+    sep = _digests({"MNIST_AMD_WGRAD_TAIL": "0"}, ["local"], model="mlp", extra=extra)
+    assert tail["local"] == sep["local"] == tail["join"] == tail["local_k4"], (tail, sep)
