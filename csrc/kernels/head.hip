@@ -1238,15 +1238,16 @@ DEV void wgrad_tail(const WgArgs<T>& a, const int j, const int tile) {
   const int ns = a.nsplit;
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(a.slab, (short)0, 0x7FFFFFFF, 0x00020000);
-  auto update = [&](int p, float sum) {  // reduce_sgd_direct_kernel's epilogue
+  auto update = [&](int p, float sum) {  // reduce_sgd_direct_kernel's epilogue, expression for expression
+    const float pv = f.params[p], mv = f.mom ? f.mom[p] : 0.f;
     float g = sum * f.scale;
     f.grad[p] = g;
     if (f.mom) {
-      const float b = f.momentum * f.mom[p] + g;
+      const float b = f.momentum * mv + g;
       f.mom[p] = b;
       g = b;
     }
-    const float v = f.params[p] - f.lr * g;
+    const float v = pv - f.lr * g;
     f.params[p] = v;
     Packer<Model, T>::pack(p, v, reinterpret_cast<T*>(f.pack));
   };
@@ -1272,18 +1273,9 @@ DEV void wgrad_tail(const WgArgs<T>& a, const int j, const int tile) {
       for (int i = 0; i < 8; ++i) acc[i] += v[i];
     }
     const f32x4 sum = zero4() + (((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7])));
-    // the update of the 4 consecutive parameters as vectors (reduce_sgd_direct_kernel's arithmetic per element)
-    f32x4 g = sum * f.scale;
-    *reinterpret_cast<f32x4*>(f.grad + p) = g;
-    if (f.mom) {
-      const f32x4 b = f.momentum * *reinterpret_cast<const f32x4*>(f.mom + p) + g;
-      *reinterpret_cast<f32x4*>(f.mom + p) = b;
-      g = b;
-    }
-    const f32x4 nv = *reinterpret_cast<const f32x4*>(f.params + p) - f.lr * g;
-    *reinterpret_cast<f32x4*>(f.params + p) = nv;
+    // the update, element by element in reduce_sgd_direct_kernel's exact expressions (the same contractions)
 #pragma unroll 1
-    for (int e = 0; e < 4; ++e) Packer<Model, T>::pack(p + e, nv[e], reinterpret_cast<T*>(f.pack));
+    for (int e = 0; e < 4; ++e) update(p + e, sum[e]);
   }
   if (J.bias && J.K >= kq && J.K < kq + 16) {  // the bias column of row n (only the tile that holds k == K)
     const int p = J.out_off + J.N * J.K + n;

@@ -33,6 +33,7 @@ ap.add_argument("--batch", type=int, default=512)
 ap.add_argument("--steps", type=int, default=4)
 ap.add_argument("--model", default="lenet5", choices=["lenet5", "mlp"])
 ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+ap.add_argument("--dump", default=None, help="also save each variant's parameters to DUMP.<variant>.pt")
 a = ap.parse_args()
 N = max(4096, a.batch * a.steps)  # (4096 for the default shapes: their digests are unchanged)
 x, y = make_split(N, seed=7)
@@ -66,3 +67,5 @@ for v in a.variants:
             tr.step(a.batch, use_graph=True)
     tr.synchronize()
     print("digest", v, hashlib.sha256(tr.params.cpu().numpy().tobytes()).hexdigest(), flush=True)
+    if a.dump:
+        torch.save(tr.params.cpu(), f"{a.dump}.{v}.pt")

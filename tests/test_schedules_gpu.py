@@ -22,9 +22,11 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _digests(env_extra, variants, model="lenet5", extra=()):
+def _digests(env_extra, variants, model="lenet5", extra=(), dump=None):
     env = dict(os.environ, PYTHONPATH=ROOT, **env_extra)
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "sched_equiv.py"), "--model", model, *extra] + variants,
+    dump_arg = ["--dump", str(dump)] if dump else []
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "sched_equiv.py"), "--model", model, *extra, *dump_arg]
+                       + variants,
                        env=env,
                        stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:]
@@ -65,11 +67,16 @@ def test_mlp_schedules_bitwise_equal(native):
 
 
 @pytest.mark.timeout(600)
-def test_mlp_wgrad_tail_bitwise_equal(native):
+def test_mlp_wgrad_tail_bitwise_equal(native, tmp_path):
     """MLP bf16 at B = 4096 (8 FC batch splits): the single-GPU step's update by each output tile's last-arriving
     split (head.hip wgrad_tail) is bitwise the separate reduce + SGD kernel (MNIST_AMD_WGRAD_TAIL=0), the world-1
     JOIN plan (reduce -> all-reduce -> SGD) and the 4-step graph."""
+    import torch
     extra = ("--batch", "4096", "--dtype", "bf16")
-    tail = _digests({}, ["local", "join", "local_k4"], model="mlp", extra=extra)
-    sep = _digests({"MNIST_AMD_WGRAD_TAIL": "0"}, ["local"], model="mlp", extra=extra)
-    assert tail["local"] == sep["local"] == tail["join"] == tail["local_k4"], (tail, sep)
+    tail = _digests({}, ["local", "join", "local_k4"], model="mlp", extra=extra, dump=tmp_path / "tail")
+    sep = _digests({"MNIST_AMD_WGRAD_TAIL": "0"}, ["local"], model="mlp", extra=extra, dump=tmp_path / "sep")
+    a, b = torch.load(tmp_path / "tail.local.pt"), torch.load(tmp_path / "sep.local.pt")
+    d = (a - b).abs()
+    # numerics first (a wrong hand-off shows as a large difference), then bit equality
+    assert float(d.max()) <= 1e-5 * float(b.abs().max()), (float(d.max()), int((d > 0).sum()))
+    assert tail["local"] == sep["local"] == tail["join"] == tail["local_k4"], (tail, sep, int((d > 0).sum()))
