@@ -72,6 +72,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("fwd_head_applies", [](int dtype, int B) { return lenet_fwd_head_applies(static_cast<DType>(dtype), B); },
         py::arg("dtype"), py::arg("B"));
   m.def("conv_bwd_max_blocks", &lenet_conv_bwd_max_blocks, py::arg("B"), py::arg("target_blocks") = 0);
+  m.def("fc_slab_ld", [](int model) { return fc_slab_ld(static_cast<ModelKind>(model)); });
   m.attr("L1_KSPLIT") = L1_KSPLIT;
   m.def("metric_rows", [](int B) { return metric_rows(B); });
   m.attr("L1_SPLIT_MAX_B") = L1_SPLIT_MAX_B;

@@ -1183,9 +1183,12 @@ DEV void wgrad_lds_body(const WgArgs<T>& a, const int j, const WgRows rows, cons
   if (!wave_live) return;
 
   float* out = a.slab + (size_t)split * a.slab_ld + J.out_off;
-  // tail mode: the partials are handed to the tile's last-arriving split (wgrad_tail) -- write-through (sc1)
-  // stores, so they are performed in memory, not left in this XCD's L2, when the arrival is counted
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0x7FFFFFFF, 0x00020000);
+  // tail mode: the partials are handed to the tile's last-arriving split (wgrad_tail) -- TILE-MAJOR (the tile's
+  // 64 x 64 block owns whole cache lines: in parameter order a line straddles two tiles, and one tile's tail
+  // reading it early would leave a stale copy in that XCD's L2 for the other tile's tail) and write-through
+  // (sc1) stores, so they are performed in memory, not held in this XCD's L2, when the arrival is counted
+  float* tb = a.slab + (size_t)split * a.slab_ld + (size_t)tile * 4096;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(tb, (short)0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -1196,7 +1199,9 @@ DEV void wgrad_lds_body(const WgArgs<T>& a, const int j, const WgRows rows, cons
         const int n = n0 + mi * 16 + grp * 4 + i;
         const int q = n >= J.N ? -1 : (k < J.K ? n * J.K + k : (k == J.K && J.bias ? J.N * J.K + n : -1));
         if (q >= 0) {
-          if (a.tail) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[mi][ni][i]), rs, q * 4, 0, 16);
+          if (a.tail)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[mi][ni][i]), rs,
+                                                  ((n - nb0) * 64 + (k - kb0)) * 4, 0, 16);
           else out[q] = acc[mi][ni][i];
         }
       }
@@ -1236,8 +1241,10 @@ DEV void wgrad_tail(const WgArgs<T>& a, const int j, const int tile) {
   const int tid = threadIdx.x, n = nb0 + (tid >> 2), kq = kb0 + (tid & 3) * 16;  // 16 tile columns per thread
   if (n >= J.N) return;
   const int ns = a.nsplit;
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc(a.slab, (short)0, 0x7FFFFFFF, 0x00020000);
+  // the tile's partials, tile-major: split s, tile row nl, tile column kl at s * slab_ld + tile * 4096 + nl * 64 + kl
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.slab + (size_t)tile * 4096, (short)0,
+                                                                      0x7FFFFFFF, 0x00020000);
+  const int lrow = (n - nb0) * 64;
   auto update = [&](int p, float sum) {  // reduce_sgd_direct_kernel's epilogue, expression for expression
     const float pv = f.params[p], mv = f.mom ? f.mom[p] : 0.f;
     float g = sum * f.scale;
@@ -1259,7 +1266,7 @@ DEV void wgrad_tail(const WgArgs<T>& a, const int j, const int tile) {
   for (int c = 0; c < 4; ++c) {
     const int k0 = kq + 4 * c;
     if (k0 >= J.K) break;  // K % 4 == 0 (784, 128): quads never straddle the bias column
-    const int p = J.out_off + n * J.K + k0;
+    const int p = J.out_off + n * J.K + k0, lo = lrow + (k0 - kb0);
     f32x4 acc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = zero4();
@@ -1268,7 +1275,7 @@ DEV void wgrad_tail(const WgArgs<T>& a, const int j, const int tile) {
       f32x4 v[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i)
-        v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((8 * h + i) * a.slab_ld + p) * 4, 0, 16));
+        v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((8 * h + i) * a.slab_ld + lo) * 4, 0, 16));
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] += v[i];
     }
@@ -1278,14 +1285,14 @@ DEV void wgrad_tail(const WgArgs<T>& a, const int j, const int tile) {
     for (int e = 0; e < 4; ++e) update(p + e, sum[e]);
   }
   if (J.bias && J.K >= kq && J.K < kq + 16) {  // the bias column of row n (only the tile that holds k == K)
-    const int p = J.out_off + J.N * J.K + n;
+    const int p = J.out_off + J.N * J.K + n, lo = lrow + (J.K - kb0);
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
     for (int h = 0; h < nchunk; ++h) {
       float v[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i)
-        v[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ((8 * h + i) * a.slab_ld + p) * 4, 0, 16));
+        v[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ((8 * h + i) * a.slab_ld + lo) * 4, 0, 16));
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] += v[i];
     }
@@ -1486,6 +1493,16 @@ int launch_head(ModelKind m, DType t, bool train, const BatchRef& br, const Head
   }
   if (t == DType::F32) return head_launch_t<float, LenetModel::Head>(train, br, hb, rows, s);
   return head_launch_t<bf16, LenetModel::Head>(train, br, hb, rows, s);
+}
+
+int fc_slab_ld(ModelKind m) {
+  // >= nparam (the parameter-order partials) and >= every tile's 64 x 64 tile-major block (the MLP tail mode)
+  int blk = 0, splits = 1;
+  HeadBuffers hb{};
+  hb.ldB = 64;
+  if (m == ModelKind::MLP) (void)wg::make_args<bf16, MlpModel::Head, MlpModel>(hb, 64, splits, nullptr, 0, nullptr, 7, &blk);
+  const int n = m == ModelKind::MLP ? MlpModel::NPARAM : LenetModel::NPARAM;
+  return rup(std::max(n, blk * 4096), 32);
 }
 
 int launch_head_wgrad(ModelKind m, DType t, const HeadBuffers& hb, int B, int splits, float* slab,

@@ -124,6 +124,8 @@ struct SgdFuse {
 // tail_cnt (MLP, with `fuse`, several splits): [TAIL_MAX_TILES] zeroed ints -- each output tile's LAST-arriving
 // split sums the tile's partials and applies the update (head.hip wgrad_tail; no reduce + SGD kernel).
 constexpr int TAIL_MAX_TILES = 64;
+// row pitch (floats) of the FC weight-gradient slab: >= nparam and >= tiles x 4096 (tail mode's tile-major partials)
+int fc_slab_ld(ModelKind m);
 int launch_head_wgrad(ModelKind m, DType t, const HeadBuffers& hb, int B, int splits, float* slab,
                        int slab_ld, hipStream_t s, int head_rows = 0, const SgdFuse* fuse = nullptr,
                        int job_mask = 7, int* tail_cnt = nullptr);

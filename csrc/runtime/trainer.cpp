@@ -436,7 +436,8 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     // the update (head.hip wgrad_tail) -- no reduce + SGD kernel, no boundary; bitwise equal to wgrad -> reduce_sgd
     const SgdFuse f{scale, lr_, momentum_, ptr<float>(p_.params), ptr<float>(p_.grad),
                     momentum_ != 0.f ? ptr<float>(p_.mom) : nullptr, ptr<void>(p_.pack), ptr<int32_t>(p_.step)};
-    launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s, hrows, &f, 7, tail_cnt_);
+    launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), fc_slab_ld(model_), s, hrows, &f, 7,
+                      tail_cnt_);
     post_launch(s);
     return;
   }
