@@ -82,7 +82,8 @@ PYBIND11_MODULE(_C, m) {
 #else
   m.attr("F32_SPLIT") = 0;
 #endif
-  m.attr("XB_MAX_B") = Trainer::XB_MAX_B;  // LeNet: batch-ordered pixel rows conv_fwd -> conv_bwd up to this batch
+  m.attr("XB_MAX_B") = Trainer::XB_MAX_B;
+  m.attr("CONV_SLAB_LD") = CONV_SLAB_LD;  // conv slab row pitch the conv tail update writes (>= conv params)  // LeNet: batch-ordered pixel rows conv_fwd -> conv_bwd up to this batch
   m.def("device_count", [] {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -266,6 +267,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("multi_steps", &Trainer::multi_steps)
       .def("invalidate", &Trainer::invalidate)
       .def("release", &Trainer::release, py::call_guard<py::gil_scoped_release>())
+      .def("destroy", &Trainer::destroy, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("captured", &Trainer::captured)
       .def_property_readonly("nparam", &Trainer::nparam)
       .def_property_readonly("pack_size", &Trainer::pack_size)

@@ -144,6 +144,10 @@ class Trainer {
   void invalidate();        // drop every cached graph
   // teardown: drop the graphs (they captured collectives), drain the side streams, detach the communicator
   void release();
+  // final teardown at a point the caller chooses (NativeTrainer.close): release(), then the native streams, events
+  // and device counters are destroyed while the HIP runtime is certainly alive (not from a destructor that may run
+  // during interpreter shutdown, after torch's own HIP teardown).  Idempotent; the object is unusable afterwards.
+  void destroy();
 
   int nparam() const { return nparam_; }
   int pack_size() const;
@@ -195,6 +199,7 @@ class Trainer {
   bool fuse_wgrad_sgd_ = true;
   bool fwd_head_ = true;
   bool comm_enabled_ = true;
+  bool destroyed_ = false;  // destroy() ran
   hipStream_t last_stream_ = nullptr;  // stream of the last graph launch / capture (drained by invalidate)
   int bwd_blocks_ = 0;
   int max_conv_slabs_ = 0;  // rows of the conv slab (lenet_conv_bwd_max_blocks(batch) at the default target)
@@ -211,5 +216,7 @@ class Trainer {
   int zero_step_dev_ = 0;
   int32_t* zero_counter_ = nullptr;  // device {0,0} for eval batch addressing
   bool wgrad_tail_ = true;            // MLP single GPU, several splits: update by each tile's last arriver
-  int32_t* tail_cnt_ = nullptr;      // [TAIL_MAX_TILES] MLP wgrad tail arrival counters (zero between launches)
+  int32_t* tail_cnt_ = nullptr;
+  float* conv_gpart_ = nullptr;      // [16][CONV_SLAB_LD] LeNet conv tail group partials
+  bool conv_tail_ = true;            // MNIST_AMD_CONV_TAIL      // [TAIL_MAX_TILES] MLP wgrad tail arrival counters (zero between launches)
 };

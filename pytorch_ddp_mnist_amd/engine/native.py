@@ -105,6 +105,26 @@ def _rup(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
 
+GUARD_BYTES = 4096   # per side of a guarded buffer (MNIST_AMD_GUARD)
+GUARD_FILL = 0xA5
+
+
+def _alloc(shape, dt, dev, guards):
+    """Zeroed device buffer; with a guard list, carved out of a larger allocation whose bytes before and after
+    the buffer hold GUARD_FILL (recorded in ``guards`` for NativeTrainer.check_guards)."""
+    if guards is None:
+        return torch.zeros(*shape, dtype=dt, device=dev)
+    n = 1
+    for d in shape:
+        n *= int(d)
+    nb = n * torch.empty((), dtype=dt).element_size()
+    raw = torch.full((2 * GUARD_BYTES + _rup(nb, 256),), GUARD_FILL, dtype=torch.uint8, device=dev)
+    body = raw[GUARD_BYTES:GUARD_BYTES + nb]
+    body.zero_()
+    guards.append((raw, nb))
+    return body.view(dt).view(*shape)
+
+
 @dataclass
 class EpochStats:
     loss_sum: float
@@ -144,7 +164,10 @@ class NativeTrainer:
         if fc_splits is None:
             fc_splits = int(os.environ.get("MNIST_AMD_FC_SPLITS", "0")) or max(1, min(16, _rup(self.batch, KC) // 512))
         K0P, N1P, N2P = HEAD_DIMS[model]
-        z = lambda *s, dt=tdt: torch.zeros(*s, dtype=dt, device=dev)  # noqa: E731
+        # MNIST_AMD_GUARD=1: every buffer the kernels address sits between two guard regions of a known byte
+        # pattern; check_guards() names the buffers whose guards a launch wrote (an out-of-bounds store)
+        self._guards = [] if os.environ.get("MNIST_AMD_GUARD", "0") not in ("", "0") else None
+        z = lambda *s, dt=tdt: _alloc(s, dt, dev, self._guards)  # noqa: E731
         self.params = z(self.nparam, dt=torch.float32)
         self.grad = z(self.nparam, dt=torch.float32)
         self.mom = z(self.nparam, dt=torch.float32)
@@ -167,7 +190,9 @@ class NativeTrainer:
         # and the update did not get faster (5.5 -> 5.1 us; B = 128 4.6 -> 4.7 us): profiles/r5_session1/NOTES.md.)
         conv_slabs = C.conv_bwd_max_blocks(self.batch) if model == "lenet5" else 0
         ncp = C.model_conv_params(mid)
-        self.slab_conv = z(max(conv_slabs, 1), max(ncp, 1), dt=torch.float32)
+        # (pitch CONV_SLAB_LD: whole cache lines per row, as the small-batch conv tail update writes them; the other
+        # paths use pitch = conv params inside the same rows)
+        self.slab_conv = z(max(conv_slabs, 1), max(C.CONV_SLAB_LD if ncp else 0, 1), dt=torch.float32)
         if model == "lenet5":
             self.p1 = z(self.ld_b * 196 * 8)
             self.m1 = z(self.ld_b * 196 * 8, dt=torch.uint8)
@@ -625,9 +650,40 @@ class NativeTrainer:
                 "step_plan_ms": round(plan_ms, 4), "step_local_ms": round(local_ms, 4),
                 "exposed_comm_us": round((plan_ms - local_ms) * 1000.0, 2)}
 
+    def close(self) -> None:
+        """Final teardown (DistContext.finalize): :meth:`release`, then the native runtime's streams, events and
+        device counters are destroyed here, while HIP is certainly up -- not by the pybind destructor, which can run
+        during interpreter shutdown after torch's HIP teardown (verdict r4, weak #1).  The trainer is unusable
+        afterwards; a second call does nothing."""
+        if self.rt is None:
+            return
+        self.release()
+        self.rt.destroy()
+        self.rt = None
+
+    def check_guards(self) -> list:
+        """MNIST_AMD_GUARD=1 runs: the buffers (attribute names) whose guard bytes no longer hold the fill
+        pattern after the queued work drained -- a kernel stored outside them.  [] when none, or no guards."""
+        if self._guards is None:
+            return []
+        self.synchronize()
+        names = {}
+        for k, v in vars(self).items():
+            if isinstance(v, torch.Tensor) and v.is_cuda:
+                names.setdefault(v.data_ptr(), k)
+        bad = []
+        for raw, nb in self._guards:
+            lo = raw[:GUARD_BYTES]
+            hi = raw[GUARD_BYTES + nb:]
+            if bool((lo != GUARD_FILL).any()) or bool((hi != GUARD_FILL).any()):
+                bad.append(names.get(raw.data_ptr() + GUARD_BYTES, f"buffer@{raw.data_ptr() + GUARD_BYTES:#x}"))
+        return bad
+
     def release(self) -> None:
         """Teardown (before the communicator is destroyed): drain the streams, drop every cached graph --
         they captured collectives -- and detach the communicator.  The trainer can still run local steps."""
+        if self.rt is None:
+            return
         try:
             if self.comm is not None and not self.comm.aborted:
                 self.synchronize()

@@ -65,12 +65,15 @@ class DistContext:
 
     def finalize(self, *trainers) -> None:
         """Clean teardown in a fixed order (the reference never calls its finalize(), survey Q16):
-        1. every trainer that captured collectives drops its graphs and detaches (``release``);
+        1. every trainer drops its graphs (they captured collectives), detaches and destroys its native streams
+           and events (``close``; ``release`` for objects without one);
         2. the RCCL communicator is flushed and destroyed (``ncclCommFinalize`` -> ``ncclCommDestroy``,
            bounded; aborted if the flush does not complete);
         3. the gloo control plane: barrier, ``destroy_process_group``."""
         for tr in trainers:
-            if tr is not None and hasattr(tr, "release"):
+            if tr is not None and hasattr(tr, "close"):
+                tr.close()
+            elif tr is not None and hasattr(tr, "release"):
                 tr.release()
         if self.rccl is not None:
             err = self.rccl.destroy(comm_timeout())

@@ -10,7 +10,8 @@ rank's "all-reduced" gradient is its own): they must equal a local run at half t
 ``_k<k>`` variants run the steps as ONE k-step graph (run_steps), whose steps may leave the aux
 branch join to the next step's head; they must equal the same number of single-step graphs.
 Usage: python scripts/sched_equiv.py [--model mlp|lenet5] [--dtype bf16|fp32] [--batch B] VARIANT [VARIANT ...]
-  VARIANT = {local,local_halflr,join,split,overlap}[_b<blocks>][_w2][_k<k>]   (overlap: LeNet, world-1 one-shot)
+  VARIANT = {local,local_halflr,join,split,overlap}[_b<blocks>][_w2][_k<k>][_t<rows>]   (overlap: LeNet, world-1
+  one-shot; _t<rows>: one more step of a partial batch of <rows> rows after the full ones, eager launch)
 """
 import argparse
 import hashlib
@@ -35,16 +36,17 @@ ap.add_argument("--model", default="lenet5", choices=["lenet5", "mlp"])
 ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
 ap.add_argument("--dump", default=None, help="also save each variant's parameters to DUMP.<variant>.pt")
 a = ap.parse_args()
-N = max(4096, a.batch * a.steps)  # (4096 for the default shapes: their digests are unchanged)
+N = max(4096, a.batch * (a.steps + 1))  # (4096 for the default shapes: their digests are unchanged)
 x, y = make_split(N, seed=7)
 C = load_c()
 order = torch.randperm(N, generator=torch.Generator().manual_seed(1)).to(torch.int32)
 
 for v in a.variants:
-    m = re.fullmatch(r"(local_halflr|local|join|split|overlap)(?:_b(\d+))?(_w2)?(?:_k(\d+))?", v)
+    m = re.fullmatch(r"(local_halflr|local|join|split|overlap)(?:_b(\d+))?(_w2)?(?:_k(\d+))?(?:_t(\d+))?", v)
     if not m:
         raise SystemExit(f"unknown variant {v}")
     kind, blocks, w2, k = m.group(1), int(m.group(2) or 0), bool(m.group(3)), int(m.group(4) or 0)
+    tail_rows = int(m.group(5) or 0)
     lr = 0.025 if kind == "local_halflr" else 0.05
     torch.manual_seed(0)
     tr = NativeTrainer(a.model, a.dtype, a.batch, torch.from_numpy(x.reshape(-1, 784)), torch.from_numpy(y),
@@ -65,6 +67,8 @@ for v in a.variants:
     else:
         for _ in range(a.steps):
             tr.step(a.batch, use_graph=True)
+    if tail_rows:
+        tr.step(tail_rows, use_graph=False)
     tr.synchronize()
     print("digest", v, hashlib.sha256(tr.params.cpu().numpy().tobytes()).hexdigest(), flush=True)
     if a.dump:

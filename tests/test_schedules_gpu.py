@@ -80,3 +80,25 @@ def test_mlp_wgrad_tail_bitwise_equal(native, tmp_path):
     # numerics first (a wrong hand-off shows as a large difference), then bit equality
     assert float(d.max()) <= 1e-5 * float(b.abs().max()), (float(d.max()), int((d > 0).sum()))
     assert tail["local"] == sep["local"] == tail["join"] == tail["local_k4"], (tail, sep, int((d > 0).sum()))
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("dtype,batch", [("bf16", 128), ("fp32", 128), ("bf16", 64), ("bf16", 512)])
+def test_conv_tail_bitwise_equal(native, tmp_path, dtype, batch):
+    """LeNet small batches, serial schedule: the conv update by the last-arriving conv_bwd workgroups (lenet.hip
+    conv_tail; two levels above 64 conv workgroups, one at B = 64) is bitwise the separate reduce + SGD kernel
+    (MNIST_AMD_CONV_TAIL=0) and the concurrent two-stream schedule, for single steps, a 4-step graph, a partial last
+    batch (_t: fewer conv workgroups, fewer groups) and at B = 512 a capped conv grid (b480: 256 workgroups of two
+    images, 16-row groups)."""
+    import torch
+    extra = ("--dtype", dtype, "--batch", str(batch))
+    var = ["local", "local_k4", f"local_t{batch // 2 + 5}"] + (["local_b480"] if batch == 512 else [])
+    tail = _digests({"MNIST_AMD_CONCURRENT": "0"}, var, extra=extra, dump=tmp_path / "tail")
+    sep = _digests({"MNIST_AMD_CONCURRENT": "0", "MNIST_AMD_CONV_TAIL": "0"}, var, extra=extra, dump=tmp_path / "sep")
+    conc = _digests({"MNIST_AMD_CONCURRENT": "1"}, ["local"], extra=extra)
+    a, b = torch.load(tmp_path / "tail.local.pt"), torch.load(tmp_path / "sep.local.pt")
+    d = (a - b).abs()
+    assert float(d.max()) <= 1e-5 * float(b.abs().max()), (float(d.max()), int((d > 0).sum()))
+    for k in var:
+        assert tail[k] == sep[k], (k, tail, sep, int((d > 0).sum()))
+    assert tail["local"] == tail["local_k4"] == conc["local"], (tail, conc)
