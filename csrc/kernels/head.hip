@@ -1199,8 +1199,11 @@ DEV void wgrad_lds_body(const WgArgs<T>& a, const int j, const WgRows rows, cons
         const int n = n0 + mi * 16 + grp * 4 + i;
         const int q = n >= J.N ? -1 : (k < J.K ? n * J.K + k : (k == J.K && J.bias ? J.N * J.K + n : -1));
         if (q >= 0) {
+          // (__float_as_uint, not __builtin_bit_cast: hipcc (ROCm 7.2) bit-casts an ext-vector ELEMENT from the
+          // vector's address, i.e. always element 0 -- every lane stored acc[mi][ni][0] four times;
+          // scripts/diag/tail_diag.py found it, profiles/r5_session1/NOTES.md)
           if (a.tail)
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc[mi][ni][i]), rs,
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[mi][ni][i]), rs,
                                                   ((n - nb0) * 64 + (k - kb0)) * 4, 0, 16);
           else out[q] = acc[mi][ni][i];
         }
