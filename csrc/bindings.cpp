@@ -72,7 +72,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("fwd_head_applies", [](int dtype, int B) { return lenet_fwd_head_applies(static_cast<DType>(dtype), B); },
         py::arg("dtype"), py::arg("B"));
   m.def("conv_bwd_max_blocks", &lenet_conv_bwd_max_blocks, py::arg("B"), py::arg("target_blocks") = 0);
-  m.def("fc_slab_ld", [](int model) { return fc_slab_ld(static_cast<ModelKind>(model)); });
   m.attr("L1_KSPLIT") = L1_KSPLIT;
   m.def("metric_rows", [](int B) { return metric_rows(B); });
   m.attr("L1_SPLIT_MAX_B") = L1_SPLIT_MAX_B;
@@ -82,8 +81,7 @@ PYBIND11_MODULE(_C, m) {
 #else
   m.attr("F32_SPLIT") = 0;
 #endif
-  m.attr("XB_MAX_B") = Trainer::XB_MAX_B;
-  m.attr("CONV_SLAB_LD") = CONV_SLAB_LD;  // conv slab row pitch the conv tail update writes (>= conv params)  // LeNet: batch-ordered pixel rows conv_fwd -> conv_bwd up to this batch
+  m.attr("XB_MAX_B") = Trainer::XB_MAX_B;  // LeNet: batch-ordered pixel rows conv_fwd -> conv_bwd up to this batch
   m.def("device_count", [] {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;

@@ -1183,12 +1183,6 @@ DEV void wgrad_lds_body(const WgArgs<T>& a, const int j, const WgRows rows, cons
   if (!wave_live) return;
 
   float* out = a.slab + (size_t)split * a.slab_ld + J.out_off;
-  // tail mode: the partials are handed to the tile's last-arriving split (wgrad_tail) -- TILE-MAJOR (the tile's
-  // 64 x 64 block owns whole cache lines: in parameter order a line straddles two tiles, and one tile's tail
-  // reading it early would leave a stale copy in that XCD's L2 for the other tile's tail) and write-through
-  // (sc1) stores, so they are performed in memory, not held in this XCD's L2, when the arrival is counted
-  float* tb = a.slab + (size_t)split * a.slab_ld + (size_t)tile * 4096;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(tb, (short)0, 0x7FFFFFFF, 0x00020000);
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -1198,113 +1192,13 @@ DEV void wgrad_lds_body(const WgArgs<T>& a, const int j, const WgRows rows, cons
       for (int i = 0; i < 4; ++i) {
         const int n = n0 + mi * 16 + grp * 4 + i;
         const int q = n >= J.N ? -1 : (k < J.K ? n * J.K + k : (k == J.K && J.bias ? J.N * J.K + n : -1));
-        if (q >= 0) {
-          // (__float_as_uint, not __builtin_bit_cast: hipcc (ROCm 7.2) bit-casts an ext-vector ELEMENT from the
-          // vector's address, i.e. always element 0 -- every lane stored acc[mi][ni][0] four times;
-          // scripts/diag/tail_diag.py found it, profiles/r5_session1/NOTES.md)
-          if (a.tail)
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[mi][ni][i]), rs,
-                                                  ((n - nb0) * 64 + (k - kb0)) * 4, 0, 16);
-          else out[q] = acc[mi][ni][i];
-        }
+        if (q >= 0) out[q] = acc[mi][ni][i];
       }
     }
 }
 
-// Tail of the MLP weight gradient with several batch splits (WgArgs::tail): each split's workgroup counts its
-// arrival on its output tile once its partial is performed; the LAST arriver of the tile sums the tile's nsplit
-// partials -- the same fixed tree as reduce_sgd_direct_kernel (optim.hip slab_sum_direct), so the parameters are
-// bitwise those of wgrad -> reduce_sgd -- and applies SGD (+momentum), the grad store and the operand re-pack.
-// Hand-off (MI355X_MICROARCH.md, visibility, Valid forms, first table row): every partial stored write-through
-// (sc1) and drained by each storing wave (s_waitcnt vmcnt(0)), a workgroup barrier, ONE lane's agent-scope
-// atomic add; the workgroup whose add returned the last count reads every partial with sc1 loads after a
-// barrier.  Nothing waits or spins: no workgroup depends on another being resident.
-template <typename T, class Model>
-DEV void wgrad_tail(const WgArgs<T>& a, const int j, const int tile) {
-  __shared__ int s_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's partial stores are performed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(a.tile_cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = old == a.nsplit - 1;
-    if (last) __hip_atomic_store(a.tile_cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-    s_last = last;
-  }
-  __syncthreads();
-  if (!s_last) return;  // block-uniform
-  const SgdFuse& f = a.sgd;
-  if (tile == 0 && threadIdx.x == 0 && f.step_ptr) {  // the step counters move once per step (as reduce_sgd)
-    f.step_ptr[0] += 1;
-    f.step_ptr[1] += 1;
-  }
-  // (selected, not indexed: a runtime index into the by-value argument array made a private copy in scratch)
-  const WgJob<T> J = j == 0 ? a.job[0] : (j == 1 ? a.job[1] : a.job[2]);
-  const int lb = tile - J.blk_begin, bn = lb / J.nblk_k, bk = lb % J.nblk_k;
-  const int nb0 = bn * 64, kb0 = bk * 64;
-  const int tid = threadIdx.x, n = nb0 + (tid >> 2), kq = kb0 + (tid & 3) * 16;  // 16 tile columns per thread
-  if (n >= J.N) return;
-  const int ns = a.nsplit;
-  // the tile's partials, tile-major: split s, tile row nl, tile column kl at s * slab_ld + tile * 4096 + nl * 64 + kl
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.slab + (size_t)tile * 4096, (short)0,
-                                                                      0x7FFFFFFF, 0x00020000);
-  const int lrow = (n - nb0) * 64;
-  auto update = [&](int p, float sum) {  // reduce_sgd_direct_kernel's epilogue, expression for expression
-    const float pv = f.params[p], mv = f.mom ? f.mom[p] : 0.f;
-    float g = sum * f.scale;
-    f.grad[p] = g;
-    if (f.mom) {
-      const float b = f.momentum * mv + g;
-      f.mom[p] = b;
-      g = b;
-    }
-    const float v = pv - f.lr * g;
-    f.params[p] = v;
-    Packer<Model, T>::pack(p, v, reinterpret_cast<T*>(f.pack));
-  };
-  // slab_sum_direct's tree over the ns (<= 16) partials of 4 consecutive parameters at once
-  // one quad of weights per pass, its partials in groups of 8 (the tree's chunks; ns is a multiple of 8, host
-  // check) -- 8 16-byte loads in flight per thread, so the tail stays within the main loop's register budget
-  const int nchunk = ns >> 3;
-#pragma unroll 1
-  for (int c = 0; c < 4; ++c) {
-    const int k0 = kq + 4 * c;
-    if (k0 >= J.K) break;  // K % 4 == 0 (784, 128): quads never straddle the bias column
-    const int p = J.out_off + n * J.K + k0, lo = lrow + (k0 - kb0);
-    f32x4 acc[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = zero4();
-#pragma unroll 1
-    for (int h = 0; h < nchunk; ++h) {
-      f32x4 v[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        v[i] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((8 * h + i) * a.slab_ld + lo) * 4, 0, 16));
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] += v[i];
-    }
-    const f32x4 sum = zero4() + (((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7])));
-    // the update, element by element in reduce_sgd_direct_kernel's exact expressions (the same contractions)
-#pragma unroll 1
-    for (int e = 0; e < 4; ++e) update(p + e, sum[e]);
-  }
-  if (J.bias && J.K >= kq && J.K < kq + 16) {  // the bias column of row n (only the tile that holds k == K)
-    const int p = J.out_off + J.N * J.K + n, lo = lrow + (J.K - kb0);
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int h = 0; h < nchunk; ++h) {
-      float v[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-        v[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, ((8 * h + i) * a.slab_ld + lo) * 4, 0, 16));
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] += v[i];
-    }
-    update(p, 0.f + (((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]))));
-  }
-}
-
-template <typename T, int SUB, class Model, bool TAIL = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAIL ? 5 : 1))) void wgrad_lds_kernel(WgArgs<T> a) {
+template <typename T, int SUB>
+__global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
   constexpr int KC = Mma<T>::KC;
   constexpr int TILE = 64 * ((SUB * 64 + 32) / (int)sizeof(T));
   __shared__ __attribute__((aligned(16))) T lds[2][TILE];  // [A = dY^T, B = X^T]
@@ -1334,7 +1228,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(TAIL ? 5 : 
   int j = 0;
   while (j + 1 < a.njobs && tile >= a.job[j + 1].blk_begin) ++j;
   wgrad_lds_body<T, SUB>(a, j, rows, nsteps, tile, split, lds[0], lds[1]);
-  if constexpr (TAIL) wgrad_tail<T, Model>(a, j, tile);
   if (a.stamps && threadIdx.x == 0 && lin < 512) a.stamps[(STAMP_WGRAD + lin) * 16 + 1] = wall_clock64();
 }
 
@@ -1358,31 +1251,24 @@ constexpr int WGRAD_SUB = MNIST_AMD_WGRAD_SUB;  // wgrad_lds_kernel: 32-row K-st
 
 template <typename T, class H, class Model>
 int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab_ld, int xcd_ch, hipStream_t s,
-                 const SgdFuse* fuse, int job_mask, int* tail_cnt) {
+                 const SgdFuse* fuse, int job_mask) {
   int blk = 0;
-  WgArgs<T> a = wg::make_args<T, H, Model>(hb, B, splits, slab, slab_ld, fuse, job_mask, &blk, tail_cnt);
+  WgArgs<T> a = wg::make_args<T, H, Model>(hb, B, splits, slab, slab_ld, fuse, job_mask, &blk);
   constexpr int KC = Mma<T>::KC;
-  constexpr bool lds_stage = std::is_same<Model, MlpModel>::value;
-  if (a.tail && blk > TAIL_MAX_TILES) throw std::invalid_argument("wgrad tail update: more tiles than counters");
+  const bool lds_stage = std::is_same<Model, MlpModel>::value;
   // XCD-aware mapping when the head's row tiling is known and the split count divides over 8 XCDs
-  if ((!fuse || a.tail) && xcd_ch > 0 && xcd_ch % KC == 0 && splits % 8 == 0) {
+  if (!fuse && xcd_ch > 0 && xcd_ch % KC == 0 && splits % 8 == 0) {
     a.xcd_ch = xcd_ch;
     a.nch = (a.Bp + xcd_ch - 1) / xcd_ch;
     a.sx = splits / 8;
     const int head_grid = (rup(B, 32) + xcd_ch - 1) / xcd_ch;  // head_launch_mtw's grid
     a.contig = hb.xcd && head_grid % 8 == 0 && a.nch == head_grid;
-    if constexpr (lds_stage) {
-      if (a.tail) hipLaunchKernelGGL((wgrad_lds_kernel<T, WGRAD_SUB, Model, true>), dim3(blk * splits), dim3(256), 0, s, a);
-      else hipLaunchKernelGGL((wgrad_lds_kernel<T, WGRAD_SUB, Model>), dim3(blk * splits), dim3(256), 0, s, a);
-    }
+    if (lds_stage) hipLaunchKernelGGL((wgrad_lds_kernel<T, WGRAD_SUB>), dim3(blk * splits), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((wgrad_kernel<T, WGRAD_DEPTH>), dim3(blk * splits), dim3(256), 0, s, a);
   } else if (a.fuse) {
     hipLaunchKernelGGL((wgrad_sgd_kernel<T, Model>), dim3(blk), dim3(256), 0, s, a);
   } else {
-    if constexpr (lds_stage) {
-      if (a.tail) hipLaunchKernelGGL((wgrad_lds_kernel<T, WGRAD_SUB, Model, true>), dim3(blk, splits), dim3(256), 0, s, a);
-      else hipLaunchKernelGGL((wgrad_lds_kernel<T, WGRAD_SUB, Model>), dim3(blk, splits), dim3(256), 0, s, a);
-    }
+    if (lds_stage) hipLaunchKernelGGL((wgrad_lds_kernel<T, WGRAD_SUB>), dim3(blk, splits), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((wgrad_kernel<T, WGRAD_DEPTH>), dim3(blk, splits), dim3(256), 0, s, a);
   }
   return splits;
@@ -1498,30 +1384,15 @@ int launch_head(ModelKind m, DType t, bool train, const BatchRef& br, const Head
   return head_launch_t<bf16, LenetModel::Head>(train, br, hb, rows, s);
 }
 
-int fc_slab_ld(ModelKind m) {
-  // >= nparam (the parameter-order partials) and >= every tile's 64 x 64 tile-major block (the MLP tail mode)
-  int blk = 0, splits = 1;
-  HeadBuffers hb{};
-  hb.ldB = 64;
-  if (m == ModelKind::MLP) (void)wg::make_args<bf16, MlpModel::Head, MlpModel>(hb, 64, splits, nullptr, 0, nullptr, 7, &blk);
-  const int n = m == ModelKind::MLP ? MlpModel::NPARAM : LenetModel::NPARAM;
-  return rup(std::max(n, blk * 4096), 32);
-}
-
 int launch_head_wgrad(ModelKind m, DType t, const HeadBuffers& hb, int B, int splits, float* slab,
-                      int slab_ld, hipStream_t s, int head_rows, const SgdFuse* fuse, int job_mask, int* tail_cnt) {
+                      int slab_ld, hipStream_t s, int head_rows, const SgdFuse* fuse, int job_mask) {
   // head_rows: batch rows per head workgroup for this B (0 = unknown: contiguous split mapping)
   if (m == ModelKind::MLP) {
     if (t == DType::F32)
-      return wgrad_launch<float, MlpModel::Head, MlpModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse, job_mask,
-                                                           tail_cnt);
-    return wgrad_launch<bf16, MlpModel::Head, MlpModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse, job_mask,
-                                                        tail_cnt);
+      return wgrad_launch<float, MlpModel::Head, MlpModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse, job_mask);
+    return wgrad_launch<bf16, MlpModel::Head, MlpModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse, job_mask);
   }
-  if (tail_cnt) throw std::invalid_argument("wgrad tail update: MLP only");
   if (t == DType::F32)
-    return wgrad_launch<float, LenetModel::Head, LenetModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse, job_mask,
-                                                             nullptr);
-  return wgrad_launch<bf16, LenetModel::Head, LenetModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse, job_mask,
-                                                          nullptr);
+    return wgrad_launch<float, LenetModel::Head, LenetModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse, job_mask);
+  return wgrad_launch<bf16, LenetModel::Head, LenetModel>(hb, B, splits, slab, slab_ld, head_rows, s, fuse, job_mask);
 }

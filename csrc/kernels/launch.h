@@ -54,19 +54,6 @@ struct HeadBuffers {
   const uint8_t* yb = nullptr;  // LeNet head16: this step's labels in batch order (LenetConvBuffers::yb) or null
 };
 
-// Optional SGD epilogue of the weight-gradient GEMM (one GPU, ONE batch split: each output element is
-// the whole gradient): g = scale * dW, momentum, parameter, packed operand images and the device step
-// counters updated in place -- the separate reduce + SGD kernel and its boundary disappear.  Bitwise
-// equal to the wgrad -> reduce_sgd pair (a one-slab reduce is scale * dW).
-struct SgdFuse {
-  float scale, lr, momentum;
-  float* params;
-  float* grad;
-  float* mom;
-  void* pack;
-  int32_t* step_ptr;
-};
-
 struct LenetConvBuffers {
   const float* params;
   const void* pack;
@@ -83,18 +70,7 @@ struct LenetConvBuffers {
   uint8_t* yb = nullptr;  // [B] u8: the labels in batch order, written with xb (read by the head16 head)
   int ablate = 0;        // diagnostics only: bitmask of phases to skip (timing ablation, wrong results)
   unsigned long long* stamps = nullptr;  // optional phase timestamps (profiling): fwd [block][16], bwd [block][16]
-  // conv update as the tail of conv_bwd (small-batch single-GPU kernel launch_lenet_conv_bwd_fc, lenet.hip
-  // conv_tail): slab rows at pitch CONV_SLAB_LD (whole cache lines per row), 16 group-partial rows in gpart, and
-  // counters tail_cnt[17] (zero between launches); the update's operands in tail_sgd.  Null: no tail.
-  float* gpart = nullptr;
-  int* tail_cnt = nullptr;
-  SgdFuse tail_sgd{};
 };
-// row pitch of the conv slab in conv-tail mode: CONV_PARAMS (2572) rounded up to whole 128-byte lines
-constexpr int CONV_SLAB_LD = 2592;
-// conv-tail mode: at most 16 groups of this many slab rows (conv workgroups), i.e. 512 workgroups
-constexpr int CONV_TAIL_MAX_PER = 32;
-constexpr int CONV_TAIL_COUNTERS = 17;  // 16 groups + the final stage (within TAIL_MAX_TILES)
 
 // Timing-ablation switches (MNIST_AMD_ABLATE / MNIST_AMD_HEAD_ABLATE: skip kernel phases, WRONG results).
 // Compiled in only by an ablation build (-DMNIST_AMD_ABLATION_BUILD, scripts/ablate.sh); in the normal
@@ -130,17 +106,24 @@ int launch_head(ModelKind m, DType t, bool train, const BatchRef& br, const Head
                  int rows_per_block, hipStream_t s);
 
 // Grouped weight-gradient GEMM over the batch (split-K over rows): writes S slabs, returns S.
+// Optional SGD epilogue of the weight-gradient GEMM (one GPU, ONE batch split: each output element is
+// the whole gradient): g = scale * dW, momentum, parameter, packed operand images and the device step
+// counters updated in place -- the separate reduce + SGD kernel and its boundary disappear.  Bitwise
+// equal to the wgrad -> reduce_sgd pair (a one-slab reduce is scale * dW).
+struct SgdFuse {
+  float scale, lr, momentum;
+  float* params;
+  float* grad;
+  float* mom;
+  void* pack;
+  int32_t* step_ptr;
+};
 
 // job_mask: which layers' weight gradients to compute (bit l = layer l+1; 7 = all three).  A subset
 // writes only those layers' slab columns (the MLP's SPLIT plan sends layers 2+3 while layer 1 computes).
-// tail_cnt (MLP, with `fuse`, several splits): [TAIL_MAX_TILES] zeroed ints -- each output tile's LAST-arriving
-// split sums the tile's partials and applies the update (head.hip wgrad_tail; no reduce + SGD kernel).
-constexpr int TAIL_MAX_TILES = 64;
-// row pitch (floats) of the FC weight-gradient slab: >= nparam and >= tiles x 4096 (tail mode's tile-major partials)
-int fc_slab_ld(ModelKind m);
 int launch_head_wgrad(ModelKind m, DType t, const HeadBuffers& hb, int B, int splits, float* slab,
                        int slab_ld, hipStream_t s, int head_rows = 0, const SgdFuse* fuse = nullptr,
-                       int job_mask = 7, int* tail_cnt = nullptr);
+                       int job_mask = 7);
 
 void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetConvBuffers& cb,
                            hipStream_t s);

@@ -951,9 +951,8 @@ struct BwdRoles {
 #define MNIST_AMD_BWD_PD 2
 #endif
 constexpr int BWD_PD = MNIST_AMD_BWD_PD;
-// One conv_bwd workgroup: block `blk` of `nblk` (the conv_bwd part of the grid).  TAIL: the slab row goes out at
-// pitch CONV_SLAB_LD with write-through (sc1) stores, for the conv update by the last arrivers (conv_tail).
-template <typename T, int NW, bool TAIL = false>
+// One conv_bwd workgroup: block `blk` of `nblk` (the conv_bwd part of the grid).
+template <typename T, int NW>
 DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int ipb, const int blk, const int nblk) {
   using M = Mma<T>;
   using Frag = typename M::Frag;
@@ -1442,12 +1441,7 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
   stamp(14);
 
   // ---- write this workgroup's partial gradients (slab row = unit)
-  float* out = cb.slab + (size_t)unit * (TAIL ? CONV_SLAB_LD : L::CONV_PARAMS);
-  const __amdgpu_buffer_rsrc_t ors = __builtin_amdgcn_make_buffer_rsrc(out, (short)0, 0x7FFFFFFF, 0x00020000);
-  auto put = [&](int q, float v) {
-    if constexpr (TAIL) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), ors, q * 4, 0, 16);
-    else out[q] = v;
-  };
+  float* out = cb.slab + (size_t)unit * L::CONV_PARAMS;
 #pragma unroll
   for (int i = 0; i < NWT; ++i) {
     if (i >= nw) break;
@@ -1455,8 +1449,8 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = grp * 4 + r;
-      if (kcol < 150) put(L::CW2 + n * 150 + c * 25 + tap, accW2[i][r]);
-      else if (kcol == 150) put(L::CB2 + n, accW2[i][r]);
+      if (kcol < 150) out[L::CW2 + n * 150 + c * 25 + tap] = accW2[i][r];
+      else if (kcol == 150) out[L::CB2 + n] = accW2[i][r];
     }
   }
 #pragma unroll
@@ -1473,10 +1467,10 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
     const int r = C_AMAP[m] >> 3, n = C_AMAP[m] & 7, bj = C_BMAP[j];
     if (n < 6) {
       if (bj == 15) {
-        if (r == 0) put(L::CB1 + n, v);
+        if (r == 0) out[L::CB1 + n] = v;
       } else {
         const int kh = 2 * (bj / 5) + r, kw = bj % 5;
-        if (kh <= 4) put(L::CW1 + n * 25 + kh * 5 + kw, v);
+        if (kh <= 4) out[L::CW1 + n * 25 + kh * 5 + kw] = v;
       }
     }
   }
@@ -1492,129 +1486,17 @@ void conv_bwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
   conv_bwd_block<T, NW>(br, cb, ipb, blockIdx.x, gridDim.x);
 }
 
-// The conv update as the tail of conv_bwd_fc_kernel (TAIL: small batches, one GPU) -- the last-arriving workgroups
-// do the work of reduce_sgd_kernel<RNW = 16> (optim.hip) over the conv parameters, bitwise: that kernel's wave w sums
-// slab rows [w * per, (w + 1) * per) (slab_partial's tree), then lane-sequential over the 16 wave partials.  Here
-// group w = the conv workgroups whose slab rows fall in that range; the group's LAST arriver computes the group
-// partial of every conv parameter (same tree) into gpart row w; the last of the 16 group arrivals sums gpart rows
-// 0..15 in order, applies SGD (+momentum), stores grad / params / mom, re-packs the operand images and moves the step
-// counters.  Slab counts <= 64 (reduce_sgd_direct's one-lane tree): one level, the last of all workgroups sums every
-// row.  Hand-off as head.hip wgrad_tail (MI355X_MICROARCH.md, visibility, valid forms): write-through stores drained
-// per wave, barrier, one agent-scope atomic add per workgroup; the last arriver reads with sc1 loads.  Slab and gpart
-// rows are whole 128-byte lines (pitch CONV_SLAB_LD), so no XCD's L2 holds a line read before all of it was written.
-// Nothing waits: the other workgroups simply exit.
-constexpr int CONV_TAIL_FINAL = 16;  // counter index of the final stage (0..15: the groups)
-constexpr int CONV_DIRECT_MAX = 64;  // optim.hip DIRECT_MAX
-template <typename T, int NT>
-DEV void conv_tail(const LenetConvBuffers& cb, const int unit, const int nslab) {
-  __shared__ int s_last;
-  const int tid = threadIdx.x;
-  const bool direct = nslab <= CONV_DIRECT_MAX;
-  const int per = (nslab + 15) / 16;
-  const int grp = direct ? CONV_TAIL_FINAL : unit / per;
-  const int gb = direct ? 0 : grp * per, gn = direct ? nslab : min(nslab, gb + per) - gb;  // the group's rows
-  auto arrive = [&](int ctr, int n) {  // true in every thread of the workgroup whose add completed `ctr`
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's stores are performed
-    __syncthreads();
-    if (tid == 0) {
-      const int old = __hip_atomic_fetch_add(cb.tail_cnt + ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = old == n - 1;
-      if (last) __hip_atomic_store(cb.tail_cnt + ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-      s_last = last;
-    }
-    __syncthreads();
-    return s_last != 0;
-  };
-  if (!arrive(grp, gn)) return;
-  constexpr int NQ = L::CONV_PARAMS / 4;  // 643 quads (CONV_PARAMS % 4 == 0)
-  static_assert(L::CONV_PARAMS % 4 == 0 && CONV_SLAB_LD % 32 == 0 && CONV_SLAB_LD >= L::CONV_PARAMS, "conv slab pitch");
-  const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(cb.slab, (short)0, 0x7FFFFFFF, 0x00020000);
-  const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(cb.gpart, (short)0, 0x7FFFFFFF, 0x00020000);
-  auto ld4 = [](const __amdgpu_buffer_rsrc_t& rs, int off) {
-    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off * 4, 0, 16));
-  };
-  // the tree of slab_partial / slab_sum_direct over rows [gb, gb + gn): chunks of 8 into acc[0..7] (in order), the
-  // remainder into acc[0], then ((0+1)+(2+3))+((4+5)+(6+7))
-  auto rows_tree = [&](int q) {
-    f32x4 acc[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = zero4();
-    int k = gb;
-#pragma unroll 1
-    for (; k + 8 <= gb + gn; k += 8) {
-      f32x4 v[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = ld4(srs, (k + i) * CONV_SLAB_LD + 4 * q);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] += v[i];
-    }
-#pragma unroll 1
-    for (; k < gb + gn; ++k) acc[0] += ld4(srs, k * CONV_SLAB_LD + 4 * q);
-    return ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-  };
-  const SgdFuse& f = cb.tail_sgd;
-  T* pack = reinterpret_cast<T*>(f.pack);
-  auto update = [&](int p, float pv, float mv, float g) {  // reduce_sgd_kernel's epilogue, expression for expression
-    g *= f.scale;
-    f.grad[p] = g;
-    if (f.mom) {
-      const float b = f.momentum * mv + g;
-      f.mom[p] = b;
-      g = b;
-    }
-    const float v = pv - f.lr * g;
-    f.params[p] = v;
-    Packer<L, T>::pack(p, v, pack);
-  };
-  if (direct) {  // reduce_sgd_direct_kernel: g = (0 + tree) * scale
-#pragma unroll 1
-    for (int q = tid; q < NQ; q += NT) {
-      const f32x4 pv = *reinterpret_cast<const f32x4*>(f.params + 4 * q);
-      const f32x4 mv = f.mom ? *reinterpret_cast<const f32x4*>(f.mom + 4 * q) : zero4();
-      const f32x4 t = zero4() + rows_tree(q);
-#pragma unroll 1
-      for (int e = 0; e < 4; ++e) update(4 * q + e, pv[e], mv[e], t[e]);
-    }
-  } else {
-#pragma unroll 1
-    for (int q = tid; q < NQ; q += NT) {
-      const f32x4 t = rows_tree(q);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, t), grs, (grp * CONV_SLAB_LD + 4 * q) * 4, 0, 16);
-    }
-    if (!arrive(CONV_TAIL_FINAL, (nslab + per - 1) / per)) return;
-#pragma unroll 1
-    for (int q = tid; q < NQ; q += NT) {
-      const f32x4 pv = *reinterpret_cast<const f32x4*>(f.params + 4 * q);
-      const f32x4 mv = f.mom ? *reinterpret_cast<const f32x4*>(f.mom + 4 * q) : zero4();
-      const int ng = (nslab + per - 1) / per;
-      f32x4 v[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = i < ng ? ld4(grs, i * CONV_SLAB_LD + 4 * q) : zero4();
-      f32x4 t = zero4();
-#pragma unroll
-      for (int i = 0; i < 16; ++i) t += v[i];  // reduce_sgd_kernel: g = 0; g += part[i] for i < 16
-#pragma unroll 1
-      for (int e = 0; e < 4; ++e) update(4 * q + e, pv[e], mv[e], t[e]);
-    }
-  }
-  if (tid == 0 && f.step_ptr) {
-    f.step_ptr[0] += 1;
-    f.step_ptr[1] += 1;
-  }
-}
-
 // Small batches, one GPU, one FC batch split: conv_bwd and the FC weight gradient + SGD update (wg::
 // wgrad_sgd_tile, the wgrad_sgd_kernel body) in ONE launch -- workgroups [0, nconv) are conv_bwd's, the rest
 // one 32x32 FC output tile each (waves 4.. of a wider workgroup idle).  The two touch disjoint data (FC
 // operands and FC parameters / images vs the conv ones), as in the concurrent two-stream schedule, so this is
 // that schedule without the fork / join: the serial small-batch chain loses a kernel boundary and the FC
 // update runs in conv_bwd's shadow.  The step counters are bumped by the conv update that follows.
-template <typename T, int NW, bool TAIL = false>
+template <typename T, int NW>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(NW == 8 ? 4 : 1)))
 void conv_bwd_fc_kernel(BatchRef br, LenetConvBuffers cb, int ipb, int nconv, wg::WgArgs<T> fa) {
   if ((int)blockIdx.x < nconv) {
-    conv_bwd_block<T, NW, TAIL>(br, cb, ipb, blockIdx.x, nconv);
-    if constexpr (TAIL) conv_tail<T, NW * 64>(cb, xcd_unit(blockIdx.x, nconv, br.xcd), nconv);
+    conv_bwd_block<T, NW>(br, cb, ipb, blockIdx.x, nconv);
   } else if (threadIdx.x < 256) {
     wg::wgrad_sgd_tile<T, LenetModel>(fa, (int)blockIdx.x - nconv);
   }
@@ -1695,17 +1577,12 @@ int launch_lenet_conv_bwd_fc(DType t, const BatchRef& br, const LenetConvBuffers
   const int ipb = bwd_ipb(br.B, target_blocks), nconv = (br.B + ipb - 1) / ipb;
   if (br.B <= 0) return nconv;
   int splits = 1, nfc = 0;
-  const bool tail = cb.tail_cnt != nullptr;
-  if (tail && (!cb.gpart || nconv > 16 * CONV_TAIL_MAX_PER))
-    throw std::invalid_argument("conv tail update: no group-partial buffer, or more conv workgroups than it covers");
   if (t == DType::F32) {
     const auto fa = wg::make_args<float, LenetModel::Head, LenetModel>(hb, br.B, splits, nullptr, 0, &fuse, 7, &nfc);
-    if (tail) hipLaunchKernelGGL((conv_bwd_fc_kernel<float, 8, true>), dim3(nconv + nfc), dim3(512), 0, s, br, cb, ipb, nconv, fa);
-    else hipLaunchKernelGGL((conv_bwd_fc_kernel<float, 8>), dim3(nconv + nfc), dim3(512), 0, s, br, cb, ipb, nconv, fa);
+    hipLaunchKernelGGL((conv_bwd_fc_kernel<float, 8>), dim3(nconv + nfc), dim3(512), 0, s, br, cb, ipb, nconv, fa);
   } else {
     const auto fa = wg::make_args<bf16, LenetModel::Head, LenetModel>(hb, br.B, splits, nullptr, 0, &fuse, 7, &nfc);
-    if (tail) hipLaunchKernelGGL((conv_bwd_fc_kernel<bf16, 4, true>), dim3(nconv + nfc), dim3(256), 0, s, br, cb, ipb, nconv, fa);
-    else hipLaunchKernelGGL((conv_bwd_fc_kernel<bf16, 4>), dim3(nconv + nfc), dim3(256), 0, s, br, cb, ipb, nconv, fa);
+    hipLaunchKernelGGL((conv_bwd_fc_kernel<bf16, 4>), dim3(nconv + nfc), dim3(256), 0, s, br, cb, ipb, nconv, fa);
   }
   return nconv;
 }

@@ -35,14 +35,9 @@ struct WgArgs {
   // [x * nch / 8, (x + 1) * nch / 8) instead of x, x + 8, ...
   int xcd_ch, nch, sx, contig;  // chunk rows, chunk count, splits per XCD
   float* slab;
-  SgdFuse sgd;          // used when fuse != 0 (then splits == 1) or tail != 0
+  SgdFuse sgd;          // used when fuse != 0 (then splits == 1)
   int fuse;
   unsigned long long* stamps;  // optional phase stamps (MNIST_AMD_STAMPS): slots [STAMP_WGRAD + block][16]
-  // tail != 0 (MLP, one GPU, several batch splits; head.hip wgrad_tail): every split of an output tile adds to
-  // tile_cnt[tile] after its partial is performed, and the LAST one sums the tile's nsplit partials and applies the
-  // SGD update (sgd) -- the separate reduce + SGD kernel and its boundary disappear
-  int tail, nsplit;
-  int* tile_cnt;        // [tiles] zero before the first launch; each tile's last arriver re-zeroes its own
 };
 
 // Weight-gradient GEMM + SGD update for one GPU and ONE batch split (small batches), one 32x32 output tile
@@ -137,10 +132,9 @@ DEV void wgrad_sgd_tile(const WgArgs<T>& a, int tile) {
 // tiles of BT x BT (BT = 32 with the SGD epilogue, else 64), *splits = batch splits actually used.
 template <typename T, class H, class Model>
 WgArgs<T> make_args(const HeadBuffers& hb, int B, int& splits, float* slab, int slab_ld, const SgdFuse* fuse,
-                    int job_mask, int* blocks, int* tail_cnt = nullptr) {
+                    int job_mask, int* blocks) {
   WgArgs<T> a{};
-  const bool tail = fuse && tail_cnt;  // several splits, the update by each tile's last arriver
-  const int BT = fuse && !tail ? 32 : 64;
+  const int BT = fuse ? 32 : 64;
   int nj = 0;
   auto mk = [&](int layer, const void* dy, const void* x, int N, int K, int NP, bool bias, int off, int& blk) {
     if (!(job_mask >> layer & 1)) return;
@@ -164,14 +158,7 @@ WgArgs<T> make_args(const HeadBuffers& hb, int B, int& splits, float* slab, int 
   splits = std::max(1, std::min(splits, a.Bp / KC));
   a.rlen = rup((a.Bp + splits - 1) / splits, KC);
   splits = (a.Bp + a.rlen - 1) / a.rlen;
-  if (tail) {
-    if (!std::is_same<Model, MlpModel>::value || splits % 8 != 0)
-      throw std::invalid_argument("wgrad tail update: MLP LDS-staged weight gradient, a multiple of 8 batch splits");
-    a.sgd = *fuse;
-    a.tail = 1;
-    a.nsplit = splits;
-    a.tile_cnt = tail_cnt;
-  } else if (fuse) {
+  if (fuse) {
     if (splits != 1) throw std::invalid_argument("wgrad with the SGD epilogue needs one batch split");
     a.sgd = *fuse;
     a.fuse = 1;

@@ -96,13 +96,6 @@ Trainer::Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const
   nparam_ = model_nparam(model_);
   max_conv_slabs_ = model_ == ModelKind::LENET ? lenet_conv_bwd_max_blocks(batch_, 0) : 0;
   concurrent_ = concurrent_mode() != 0;
-  {  // MNIST_AMD_WGRAD_TAIL=0: the MLP weight gradient's separate reduce + SGD kernel instead of the tail update
-    const char* e = std::getenv("MNIST_AMD_WGRAD_TAIL");
-    wgrad_tail_ = !(e && *e == '0');
-    // MNIST_AMD_CONV_TAIL=0: the LeNet small-batch conv update as its own reduce + SGD kernel after conv_bwd_fc
-    const char* c = std::getenv("MNIST_AMD_CONV_TAIL");
-    conv_tail_ = !(c && *c == '0');
-  }
   const int ps = model_phase_split(model_);  // default buckets: one per backward phase (see Plan)
   buckets_.push_back({ps, nparam_, 0});
   buckets_.push_back({0, ps, 1});
@@ -112,10 +105,6 @@ Trainer::Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const
   for (auto& e : events_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_CHECK(hipMalloc(&zero_counter_, 2 * sizeof(int32_t)));
   HIP_CHECK(hipMemset(zero_counter_, 0, 2 * sizeof(int32_t)));
-  HIP_CHECK(hipMalloc(&tail_cnt_, TAIL_MAX_TILES * sizeof(int32_t)));  // wgrad tail arrival counters (MLP)
-  HIP_CHECK(hipMemset(tail_cnt_, 0, TAIL_MAX_TILES * sizeof(int32_t)));
-  if (model_ == ModelKind::LENET)  // conv tail update: the 16 group partials (lenet.hip conv_tail)
-    HIP_CHECK(hipMalloc(&conv_gpart_, 16 * (size_t)CONV_SLAB_LD * sizeof(float)));
 }
 
 Trainer::~Trainer() { destroy(); }
@@ -132,11 +121,8 @@ void Trainer::destroy() {
   if (comm_stream_) hipStreamDestroy(comm_stream_);
   if (aux_stream_) hipStreamDestroy(aux_stream_);
   if (zero_counter_) hipFree(zero_counter_);
-  if (tail_cnt_) hipFree(tail_cnt_);
-  if (conv_gpart_) hipFree(conv_gpart_);
-  conv_gpart_ = nullptr;
   comm_stream_ = aux_stream_ = last_stream_ = nullptr;
-  zero_counter_ = tail_cnt_ = nullptr;
+  zero_counter_ = nullptr;
   comm_.reset();
   oneshot_.reset();
   ov_fc_.reset();
@@ -450,16 +436,6 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     post_launch(s);
     return;
   }
-  if (model_ == ModelKind::MLP && fuse_wgrad_sgd_ && wgrad_tail_ && fc_splits_for(B) % 8 == 0) {
-    // one GPU, several batch splits: each output tile's last-arriving split sums the tile's partials and applies
-    // the update (head.hip wgrad_tail) -- no reduce + SGD kernel, no boundary; bitwise equal to wgrad -> reduce_sgd
-    const SgdFuse f{scale, lr_, momentum_, ptr<float>(p_.params), ptr<float>(p_.grad),
-                    momentum_ != 0.f ? ptr<float>(p_.mom) : nullptr, ptr<void>(p_.pack), ptr<int32_t>(p_.step)};
-    launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), fc_slab_ld(model_), s, hrows, &f, 7,
-                      tail_cnt_);
-    post_launch(s);
-    return;
-  }
   if (model_ == ModelKind::LENET && fc_splits_ == 1 && fuse_wgrad_sgd_) {
     // serial single-GPU schedule, one FC batch split (small batches): the FC update is the wgrad kernel's
     // epilogue (it touches only FC parameters / operand images, which conv_bwd does not read), and the closing
@@ -468,18 +444,6 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
                     momentum_ != 0.f ? ptr<float>(p_.mom) : nullptr, ptr<void>(p_.pack), nullptr};
     // ... as extra workgroups of the conv_bwd launch (one kernel instead of two; the FC wgrad + update as its own
     // kernel before conv_bwd measured 31.0 vs 25.8 us per B = 128 step, profiles/r4_session2/NOTES.md)
-    if (conv_tail_ && lenet_conv_bwd_blocks(B, bwd_blocks_) <= 16 * CONV_TAIL_MAX_PER) {
-      // ... and the conv update by the last-arriving conv workgroups (lenet.hip conv_tail; bitwise the reduce +
-      // SGD kernel below): the step is one kernel after the head
-      LenetConvBuffers cb = conv_buffers(B);
-      cb.gpart = conv_gpart_;
-      cb.tail_cnt = tail_cnt_;
-      cb.tail_sgd = SgdFuse{scale, lr_, momentum_, ptr<float>(p_.params), ptr<float>(p_.grad),
-                            momentum_ != 0.f ? ptr<float>(p_.mom) : nullptr, ptr<void>(p_.pack), ptr<int32_t>(p_.step)};
-      launch_lenet_conv_bwd_fc(dtype_, br, cb, hb, f, s, bwd_blocks_);
-      post_launch(s);
-      return;
-    }
     const int nslab = launch_lenet_conv_bwd_fc(dtype_, br, conv_buffers(B), hb, f, s, bwd_blocks_);
     post_launch(s);
     launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),

@@ -215,8 +215,4 @@ class Trainer {
   int multi_k_ = 0;
   int zero_step_dev_ = 0;
   int32_t* zero_counter_ = nullptr;  // device {0,0} for eval batch addressing
-  bool wgrad_tail_ = true;            // MLP single GPU, several splits: update by each tile's last arriver
-  int32_t* tail_cnt_ = nullptr;
-  float* conv_gpart_ = nullptr;      // [16][CONV_SLAB_LD] LeNet conv tail group partials
-  bool conv_tail_ = true;            // MNIST_AMD_CONV_TAIL      // [TAIL_MAX_TILES] MLP wgrad tail arrival counters (zero between launches)
 };

@@ -181,18 +181,14 @@ class NativeTrainer:
         self.eval_metrics = z(C.metric_rows(self.batch), 4, dt=torch.float32)
         self.xT, self.h1T, self.h2T = z(K0P, self.ld_b), z(N1P, self.ld_b), z(N2P, self.ld_b)
         self.dy1T, self.dy2T, self.dy3T = z(N1P, self.ld_b), z(N2P, self.ld_b), z(16, self.ld_b)
-        # FC weight-gradient partials: one row per batch split, pitch >= nparam (parameter order) and >= the MLP
-        # tail mode's tile-major blocks (csrc/kernels/head.hip wgrad_tail)
-        self.slab_fc = z(fc_splits, C.fc_slab_ld(mid), dt=torch.float32)
+        self.slab_fc = z(fc_splits, self.nparam, dt=torch.float32)
         # rows for any batch <= self.batch (a partial last batch can need more workgroups than a full one).
         # (Round 5 measured the transposed layout -- one slab column per workgroup, one wave per parameter in the
         # conv update -- and reverted it: conv_bwd's scattered column stores cost 50.7 -> 54.4 us at B = 8192
         # and the update did not get faster (5.5 -> 5.1 us; B = 128 4.6 -> 4.7 us): profiles/r5_session1/NOTES.md.)
         conv_slabs = C.conv_bwd_max_blocks(self.batch) if model == "lenet5" else 0
         ncp = C.model_conv_params(mid)
-        # (pitch CONV_SLAB_LD: whole cache lines per row, as the small-batch conv tail update writes them; the other
-        # paths use pitch = conv params inside the same rows)
-        self.slab_conv = z(max(conv_slabs, 1), max(C.CONV_SLAB_LD if ncp else 0, 1), dt=torch.float32)
+        self.slab_conv = z(max(conv_slabs, 1), max(ncp, 1), dt=torch.float32)
         if model == "lenet5":
             self.p1 = z(self.ld_b * 196 * 8)
             self.m1 = z(self.ld_b * 196 * 8, dt=torch.uint8)

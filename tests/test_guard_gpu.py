@@ -19,7 +19,7 @@ CASES = [
     ("mlp", "fp32", 128, "eager"),     # the shared-GPU test's path: phase API, host all-reduce
     ("mlp", "fp32", 128, "graph"),
     ("mlp", "bf16", 128, "graph"),
-    ("mlp", "bf16", 4096, "graph"),    # the weight-gradient tail update (8 batch splits)
+    ("mlp", "bf16", 4096, "graph"),    # 8 FC batch splits
     ("mlp", "fp32", 8192, "graph"),
     ("lenet5", "bf16", 128, "graph"),  # conv_bwd + FC wgrad/SGD in one kernel
     ("lenet5", "fp32", 128, "eager"),
