@@ -1066,13 +1066,13 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
   //  shuttle accumulators VGPR<->AGPR around every MFMA -- the B operand is read from LDS)
 
   // ---- once per workgroup: zero every padded image, stage C2d
-  zero_lds<T>(xs, S::ONES);
+  zero_lds<T>(xs, S::ONES, tid, NT);
   for (int e = tid; e < S::ONES_N; e += NT) xs[S::ONES + e] = to_t<T>(1.f);
-  zero_lds<T>(dy1t - S::D1PRE, S::D1PRE + 8 * S::D1P);
-  zero_lds<T>(dys, 18 * 18 * 16);
-  zero_lds<T>(p1t, 31 * S::P1P);
+  zero_lds<T>(dy1t - S::D1PRE, S::D1PRE + 8 * S::D1P, tid, NT);
+  zero_lds<T>(dys, 18 * 18 * 16, tid, NT);
+  zero_lds<T>(p1t, 31 * S::P1P, tid, NT);
   for (int e = tid; e < S::P1P; e += NT) p1t[31 * S::P1P + e] = to_t<T>(1.f);
-  if constexpr (S::DY2) zero_lds<T>(dy2t, 16 * S::D2P);
+  if constexpr (S::DY2) zero_lds<T>(dy2t, 16 * S::D2P, tid, NT);
   // conv2 dgrad, two output rows per tile: out (Y = y + r, x, c) = sum over kh' in [-1, 4], kw, n of
   // dY2[y - kh'][x - kw][n] * W2[n][c][kh' + r][kw]  ->  B[(kh'+1)*5 + kw, n][(r, c)], zero where
   // kh' + r is outside 0..4.  N = (r, c) holds 12 live columns of 16 (was 6 with one row per tile).
@@ -1486,6 +1486,107 @@ void conv_bwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
   conv_bwd_block<T, NW>(br, cb, ipb, blockIdx.x, gridDim.x);
 }
 
+// The FC weight gradient on two SPARE waves of every conv_bwd workgroup (conv_bwd_wg_kernel): wgrad_kernel's wave
+// jobs (wg::wave_job, bit for bit the same partials), one or a few 32-row K-steps per barrier interval of conv_bwd,
+// the wave executing exactly conv_bwd's barrier count (NB = 2 + 3 * ipb: setup, three per image, the final
+// reduction) so the two roles share the workgroup's s_barrier.  What this replaces is the concurrent schedule's
+// fork / join: the FC wgrad on an aux stream beside conv_bwd cost ~5 us of idle time at the fork and ~6 us at the
+// join per step (rocprofv3 kernel trace, LeNet bf16 B=8192, profiles/r5_session1/NOTES.md) -- a captured graph's
+// cross-stream edge, not the kernels.  Jobs are dealt XCD-locally when both grids divide by 8 (job workgroup L ran
+// on XCD L % 8 in wgrad_kernel, where the head wrote its rows); a job of a sub-tile with no K-steps stores zeros
+// (as wgrad_kernel does); any step left after the last barrier is finished without one.
+template <typename T>
+DEV void fc_wgrad_lockstep(const wg::WgArgs<T>& a, const int nblk_tiles, const int nblocks, const int wave, const int NB) {
+  using M = Mma<T>;
+  using Frag = typename M::Frag;
+  constexpr int KV = M::KV, KC = M::KC;
+  const int g = blockIdx.x, G = gridDim.x;
+  const bool local = (G & 7) == 0 && (nblocks & 7) == 0;
+  const int x = g & 7;
+  const int r0 = local ? (g >> 3) * 2 + wave : g * 2 + wave;  // this wave's first job (XCD-local / global index)
+  const int rstep = local ? (G >> 3) * 2 : G * 2;
+  const int rend = local ? (nblocks >> 3) * 4 : nblocks * 4;
+  auto job_of = [&](int r, wg::WaveJob<T>& o) {
+    const int L = local ? x + 8 * (r >> 2) : (r >> 2);
+    return wg::wave_job(a, nblk_tiles, L, r & 3, o);
+  };
+  int S = 0;  // this wave's K-steps over all its jobs
+  for (int r = r0; r < rend; r += rstep) {
+    wg::WaveJob<T> o;
+    if (job_of(r, o)) S += o.nsteps;
+  }
+  const int per = max(1, (S + NB - 1) / NB);  // K-steps per barrier interval
+  Frag ones;
+#pragma unroll
+  for (int q = 0; q < KV; ++q) M::set(ones, q, 1.f);
+  const Frag zf = M::zero();
+  wg::WaveJob<T> o;
+  f32x4 acc[2][2];
+  Frag c0, c1, c2, c3;  // the current step's A0, A1, B0, B1
+  int r = r0 - rstep, st = 0;
+  bool live = false;
+  auto load = [&](int s, Frag& x0, Frag& x1, Frag& x2, Frag& x3) {
+    const int rc = o.rows(s, KC);
+    x0 = M::load(o.ap0 + rc);
+    x1 = o.nv1 ? M::load(o.ap1 + rc) : zf;
+    x2 = M::load(o.bp0 + rc);
+    x3 = M::load(o.bp1 + rc);
+  };
+  auto zero_acc = [&] {
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = zero4();
+  };
+  auto next_job = [&] {  // the next job with K-steps (jobs without any store their zero partial at once)
+    live = false;
+    for (r += rstep; r < rend; r += rstep) {
+      if (!job_of(r, o)) continue;
+      zero_acc();
+      if (o.nsteps == 0) {
+        wg::wave_job_store(a, o, acc);
+        continue;
+      }
+      st = 0;
+      load(0, c0, c1, c2, c3);
+      live = true;
+      return;
+    }
+  };
+  auto step = [&] {  // one K-step of the live job (wgrad_kernel's MFMA order), then the next step's fragments
+    Frag n0 = c0, n1 = c1, n2 = c2, n3 = c3;
+    const bool more = st + 1 < o.nsteps;
+    if (more) load(st + 1, n0, n1, n2, n3);
+    const Frag b0 = o.sel0 == 0 ? c2 : (o.sel0 == 1 ? ones : zf);
+    const Frag b1 = o.sel1 == 0 ? c3 : (o.sel1 == 1 ? ones : zf);
+    M::mma(acc[0][0], c0, b0);
+    M::mma(acc[0][1], c0, b1);
+    M::mma(acc[1][0], c1, b0);
+    M::mma(acc[1][1], c1, b1);
+    if (more) {
+      c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+      ++st;
+    } else {
+      wg::wave_job_store(a, o, acc);
+      next_job();
+    }
+  };
+  next_job();
+  for (int b = 0; b < NB; ++b) {
+    for (int p = 0; p < per && live; ++p) step();
+    __syncthreads();  // conv_bwd's b-th barrier
+  }
+  while (live) step();
+}
+
+template <typename T, int NW>
+__global__ __launch_bounds__((NW + 2) * 64) __attribute__((amdgpu_waves_per_eu(1)))
+void conv_bwd_wg_kernel(BatchRef br, LenetConvBuffers cb, int ipb, wg::WgArgs<T> fa, int nblk_tiles, int nblocks) {
+  const int w = wave_id();
+  if (w < NW) conv_bwd_block<T, NW>(br, cb, ipb, blockIdx.x, gridDim.x);
+  else fc_wgrad_lockstep<T>(fa, nblk_tiles, nblocks, w - NW, 2 + 3 * ipb);
+}
+
 // Small batches, one GPU, one FC batch split: conv_bwd and the FC weight gradient + SGD update (wg::
 // wgrad_sgd_tile, the wgrad_sgd_kernel body) in ONE launch -- workgroups [0, nconv) are conv_bwd's, the rest
 // one 32x32 FC output tile each (waves 4.. of a wider workgroup idle).  The two touch disjoint data (FC
@@ -1511,6 +1612,20 @@ static int default_bwd_target() { return 512; }
 static int bwd_ipb(int B, int target) {
   const int div = target > 0 ? target : default_bwd_target();
   return std::min(MAX_IPB, std::max(1, (B + div - 1) / div));
+}
+
+int launch_lenet_conv_bwd_wg(DType t, const BatchRef& br, const LenetConvBuffers& cb, const HeadBuffers& hb,
+                             int splits, float* slab_fc, int slab_ld, int head_rows, int* nslab_out, hipStream_t s,
+                             int target_blocks) {
+  if (t != DType::BF16) throw std::invalid_argument("conv_bwd + FC wgrad in one kernel: bf16 only");
+  const int ipb = bwd_ipb(br.B, target_blocks), grid = (br.B + ipb - 1) / ipb;
+  if (nslab_out) *nslab_out = grid;
+  int blk = 0;
+  wg::WgArgs<bf16> a = wg::make_args<bf16, LenetModel::Head, LenetModel>(hb, br.B, splits, slab_fc, slab_ld, nullptr, 7, &blk);
+  wg::configure_xcd(a, hb, br.B, splits, head_rows);
+  if (br.B <= 0) return splits;
+  hipLaunchKernelGGL((conv_bwd_wg_kernel<bf16, 4>), dim3(grid), dim3(6 * 64), 0, s, br, cb, ipb, a, blk, blk * splits);
+  return splits;
 }
 
 int lenet_conv_bwd_blocks(int B, int target) {
