@@ -1495,11 +1495,12 @@ void conv_bwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
 // cross-stream edge, not the kernels.  Jobs are dealt XCD-locally when both grids divide by 8 (job workgroup L ran
 // on XCD L % 8 in wgrad_kernel, where the head wrote its rows); a job of a sub-tile with no K-steps stores zeros
 // (as wgrad_kernel does); any step left after the last barrier is finished without one.
+constexpr int WGW_JOBS = 2;  // wave jobs with K-steps per spare wave (launch_lenet_conv_bwd_wg checks)
 template <typename T>
 DEV void fc_wgrad_lockstep(const wg::WgArgs<T>& a, const int nblk_tiles, const int nblocks, const int wave, const int NB) {
   using M = Mma<T>;
   using Frag = typename M::Frag;
-  constexpr int KV = M::KV, KC = M::KC;
+  constexpr int KV = M::KV, KC = M::KC, D = 3;  // K-steps of fragments in flight ahead of the MFMAs
   const int g = blockIdx.x, G = gridDim.x;
   const bool local = (G & 7) == 0 && (nblocks & 7) == 0;
   const int x = g & 7;
@@ -1516,67 +1517,123 @@ DEV void fc_wgrad_lockstep(const wg::WgArgs<T>& a, const int nblk_tiles, const i
     if (job_of(r, o)) S += o.nsteps;
   }
   const int per = max(1, (S + NB - 1) / NB);  // K-steps per barrier interval
+  const int GS = per * NB;                     // step slots: a barrier after every `per`
   Frag ones;
 #pragma unroll
   for (int q = 0; q < KV; ++q) M::set(ones, q, 1.f);
   const Frag zf = M::zero();
-  wg::WaveJob<T> o;
-  f32x4 acc[2][2];
-  Frag c0, c1, c2, c3;  // the current step's A0, A1, B0, B1
-  int r = r0 - rstep, st = 0;
-  bool live = false;
-  auto load = [&](int s, Frag& x0, Frag& x1, Frag& x2, Frag& x3) {
-    const int rc = o.rows(s, KC);
-    x0 = M::load(o.ap0 + rc);
-    x1 = o.nv1 ? M::load(o.ap1 + rc) : zf;
-    x2 = M::load(o.bp0 + rc);
-    x3 = M::load(o.bp1 + rc);
-  };
-  auto zero_acc = [&] {
+  f32x4 acc[2][2], done[2][2];
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
+  for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = zero4();
+    for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = done[mi][ni] = zero4();
+  // Two cursors over the jobs that have K-steps: `ld` issues fragments D steps ahead, `cp` computes.  Nothing but
+  // the four fragment loads per step touches memory inside the loop (the partials are stored after the last
+  // barrier; a wave has at most WGW_JOBS jobs with K-steps, the first one's sums parked in `done`), and an exhausted
+  // `ld` re-issues its last step's loads, so the compiler's vmcnt wait before a step's MFMAs counts the 2 x 4 loads
+  // issued after that step's own.
+  struct Cur {
+    int r, st;
+    wg::WaveJob<T> o;
   };
-  auto next_job = [&] {  // the next job with K-steps (jobs without any store their zero partial at once)
-    live = false;
-    for (r += rstep; r < rend; r += rstep) {
-      if (!job_of(r, o)) continue;
-      zero_acc();
-      if (o.nsteps == 0) {
-        wg::wave_job_store(a, o, acc);
-        continue;
-      }
-      st = 0;
-      load(0, c0, c1, c2, c3);
-      live = true;
-      return;
-    }
+  auto seek = [&](Cur& c) {  // from c.r (inclusive) to the next job with K-steps (r = rend: none)
+    for (; c.r < rend; c.r += rstep)
+      if (job_of(c.r, c.o) && c.o.nsteps > 0) break;
+    c.st = 0;
   };
-  auto step = [&] {  // one K-step of the live job (wgrad_kernel's MFMA order), then the next step's fragments
-    Frag n0 = c0, n1 = c1, n2 = c2, n3 = c3;
-    const bool more = st + 1 < o.nsteps;
-    if (more) load(st + 1, n0, n1, n2, n3);
-    const Frag b0 = o.sel0 == 0 ? c2 : (o.sel0 == 1 ? ones : zf);
-    const Frag b1 = o.sel1 == 0 ? c3 : (o.sel1 == 1 ? ones : zf);
-    M::mma(acc[0][0], c0, b0);
-    M::mma(acc[0][1], c0, b1);
-    M::mma(acc[1][0], c1, b0);
-    M::mma(acc[1][1], c1, b1);
-    if (more) {
-      c0 = n0; c1 = n1; c2 = n2; c3 = n3;
-      ++st;
+  auto advance = [&](Cur& c) {
+    if (c.st + 1 < c.o.nsteps) {
+      ++c.st;
     } else {
-      wg::wave_job_store(a, o, acc);
-      next_job();
+      Cur n = c;
+      n.r += rstep;
+      seek(n);
+      if (n.r < rend) c = n;  // exhausted: stays on its last step (its loads are re-issued, never used)
     }
   };
-  next_job();
-  for (int b = 0; b < NB; ++b) {
-    for (int p = 0; p < per && live; ++p) step();
-    __syncthreads();  // conv_bwd's b-th barrier
+  Frag f[D][4];  // f[slot][A0, A1, B0, B1]: step k's fragments in slot k % D (constant indices: unrolled by D)
+  Cur ld{r0, 0, {}}, cp{r0, 0, {}};
+  if (S > 0) {
+    seek(ld);
+    seek(cp);
   }
-  while (live) step();
+  auto load = [&](int slot) {
+    const wg::WaveJob<T>& o = ld.o;
+    const int rc = o.rows(ld.st, KC);
+    // A1 of a sub-tile whose second 16 rows are padding: row 0's fragment instead (every step issues the same four
+    // loads), replaced by zeros at use as in wgrad_kernel
+    f[slot][0] = M::load(o.ap0 + rc);
+    f[slot][1] = M::load(o.nv1 ? o.ap1 + rc : o.ap0 + rc);
+    f[slot][2] = M::load(o.bp0 + rc);
+    f[slot][3] = M::load(o.bp1 + rc);
+    advance(ld);
+  };
+  int jd = 0;  // jobs completed
+  auto compute = [&](int slot) {
+    const wg::WaveJob<T>& o = cp.o;
+    const Frag a0 = f[slot][0], a1 = o.nv1 ? f[slot][1] : zf;
+    const Frag b0 = o.sel0 == 0 ? f[slot][2] : (o.sel0 == 1 ? ones : zf);
+    const Frag b1 = o.sel1 == 0 ? f[slot][3] : (o.sel1 == 1 ? ones : zf);
+    M::mma(acc[0][0], a0, b0);
+    M::mma(acc[0][1], a0, b1);
+    M::mma(acc[1][0], a1, b0);
+    M::mma(acc[1][1], a1, b1);
+    if (cp.st + 1 == o.nsteps) {
+      if (jd == 0) {
+#pragma unroll
+        for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 2; ++ni) {
+            done[mi][ni] = acc[mi][ni];
+            acc[mi][ni] = zero4();
+          }
+      }
+      ++jd;
+    }
+    advance(cp);
+  };
+  if (S > 0) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) load(d);
+  }
+  int k = 0;
+  if (S > 0) {
+    for (; k + D <= GS; k += D) {
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        if (k + d < S) compute(d);
+        load(d);  // step k + d + D's fragments (or a re-issue past the end)
+        if ((k + d + 1) % per == 0) __syncthreads();  // conv_bwd's barriers: NB in all
+      }
+    }
+  }
+  for (; k < GS; ++k) {  // the last < D step slots (a step here has had its fragments since the prologue / loop)
+    if (k < S) {
+      const int d = k % D;
+      if (d == 0) compute(0);
+      else if (d == 1) compute(1);
+      else compute(2);
+    }
+    if ((k + 1) % per == 0) __syncthreads();
+  }
+  // the partials, after conv_bwd's last barrier: every job of this wave in order (a job without K-steps stores its
+  // zero partial, as wgrad_kernel's waves do)
+  int jn = 0;
+  for (int r = r0; r < rend; r += rstep) {
+    wg::WaveJob<T> o;
+    if (!job_of(r, o)) continue;
+    if (o.nsteps == 0) {
+      f32x4 z[2][2];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) z[mi][ni] = zero4();
+      wg::wave_job_store(a, o, z);
+    } else {
+      wg::wave_job_store(a, o, jn == 0 ? done : acc);
+      ++jn;
+    }
+  }
 }
 
 template <typename T, int NW>
@@ -1623,6 +1680,11 @@ int launch_lenet_conv_bwd_wg(DType t, const BatchRef& br, const LenetConvBuffers
   int blk = 0;
   wg::WgArgs<bf16> a = wg::make_args<bf16, LenetModel::Head, LenetModel>(hb, br.B, splits, slab_fc, slab_ld, nullptr, 7, &blk);
   wg::configure_xcd(a, hb, br.B, splits, head_rows);
+  // every spare wave gets at most WGW_JOBS wave jobs (the job list of fc_wgrad_lockstep, dealt XCD-locally)
+  const bool local = grid % 8 == 0 && (blk * splits) % 8 == 0;
+  const int jobs = local ? (blk * splits) / 8 * 4 : blk * splits * 4, waves = local ? grid / 8 * 2 : grid * 2;
+  if ((jobs + waves - 1) / waves > WGW_JOBS)
+    throw std::invalid_argument("conv_bwd + FC wgrad in one kernel: more wave jobs than the spare waves hold");
   if (br.B <= 0) return splits;
   hipLaunchKernelGGL((conv_bwd_wg_kernel<bf16, 4>), dim3(grid), dim3(6 * 64), 0, s, br, cb, ipb, a, blk, blk * splits);
   return splits;
