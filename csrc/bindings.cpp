@@ -237,9 +237,6 @@ PYBIND11_MODULE(_C, m) {
       .def("set_plan", &Trainer::set_plan)
       .def_property_readonly("plan", &Trainer::plan)
       .def("set_concurrent", &Trainer::set_concurrent)
-      .def("set_bwd_wg", &Trainer::set_bwd_wg)
-      .def_property_readonly("bwd_wg", &Trainer::bwd_wg)
-      .def("bwd_wg_applies", &Trainer::bwd_wg_applies, py::arg("B"))
       .def("set_fwd_head", &Trainer::set_fwd_head)
       .def_property_readonly("fwd_head", &Trainer::fwd_head)
       .def_property_readonly("concurrent", &Trainer::concurrent)

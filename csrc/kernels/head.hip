@@ -28,7 +28,6 @@
 namespace {
 using wg::WgArgs;
 using wg::WgJob;
-using wg::WgRows;
 using wg::wgrad_sgd_tile;
 
 template <typename T, class H, int MT, bool PRE = false>
@@ -1058,6 +1057,15 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
   if (a.stamps && threadIdx.x == 0 && lin < 512) a.stamps[(STAMP_WGRAD + lin) * 16 + 1] = wall_clock64();
 }
 
+// Batch rows of a wgrad workgroup's K-steps (wgrad_kernel's split / XCD-aware mapping, see WgArgs).
+struct WgRows {
+  int xcd_ch, rs, m0, spc, x, contig, nch;
+  DEV int operator()(int st, int KC) const {  // first batch row of step st (monotonic in st)
+    if (xcd_ch == 0) return rs + st * KC;
+    const int m = m0 + st / spc;
+    return (contig ? x * (nch / 8) + m : x + 8 * m) * xcd_ch + (st % spc) * KC;
+  }
+};
 
 // LDS-staged variant of wgrad_kernel (same tiles, splits, step order and slab layout; every output element
 // is the same MFMA chain, so the results are bitwise those of wgrad_kernel): the workgroup stages the 64-row
@@ -1248,9 +1256,13 @@ int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab
   WgArgs<T> a = wg::make_args<T, H, Model>(hb, B, splits, slab, slab_ld, fuse, job_mask, &blk);
   constexpr int KC = Mma<T>::KC;
   const bool lds_stage = std::is_same<Model, MlpModel>::value;
-  (void)KC;
   // XCD-aware mapping when the head's row tiling is known and the split count divides over 8 XCDs
-  if (!fuse && wg::configure_xcd(a, hb, B, splits, xcd_ch)) {
+  if (!fuse && xcd_ch > 0 && xcd_ch % KC == 0 && splits % 8 == 0) {
+    a.xcd_ch = xcd_ch;
+    a.nch = (a.Bp + xcd_ch - 1) / xcd_ch;
+    a.sx = splits / 8;
+    const int head_grid = (rup(B, 32) + xcd_ch - 1) / xcd_ch;  // head_launch_mtw's grid
+    a.contig = hb.xcd && head_grid % 8 == 0 && a.nch == head_grid;
     if (lds_stage) hipLaunchKernelGGL((wgrad_lds_kernel<T, WGRAD_SUB>), dim3(blk * splits), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((wgrad_kernel<T, WGRAD_DEPTH>), dim3(blk * splits), dim3(256), 0, s, a);
   } else if (a.fuse) {

@@ -147,12 +147,6 @@ void launch_lenet_conv_bwd(DType t, const BatchRef& br, const LenetConvBuffers& 
 // launch_head_wgrad with `fuse`) in ONE kernel; returns the conv slab count (the conv update follows).
 int launch_lenet_conv_bwd_fc(DType t, const BatchRef& br, const LenetConvBuffers& cb, const HeadBuffers& hb,
                              const SgdFuse& fuse, hipStream_t s, int target_blocks = 0);
-// conv_bwd with the FC weight gradient on two spare waves of each workgroup (lenet.hip conv_bwd_wg_kernel; bf16):
-// conv slab as launch_lenet_conv_bwd (*nslab_out rows), FC partials as launch_head_wgrad(hb, B, splits, slab_fc,
-// slab_ld, head_rows) -- bit for bit.  Returns the FC split count.
-int launch_lenet_conv_bwd_wg(DType t, const BatchRef& br, const LenetConvBuffers& cb, const HeadBuffers& hb,
-                             int splits, float* slab_fc, int slab_ld, int head_rows, int* nslab_out, hipStream_t s,
-                             int target_blocks = 0);
 int lenet_conv_bwd_blocks(int B, int target_blocks = 0);
 int lenet_conv_bwd_max_blocks(int B, int target_blocks = 0);  // slab rows needed for any batch <= B
 

@@ -1066,13 +1066,13 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
   //  shuttle accumulators VGPR<->AGPR around every MFMA -- the B operand is read from LDS)
 
   // ---- once per workgroup: zero every padded image, stage C2d
-  zero_lds<T>(xs, S::ONES, tid, NT);
+  zero_lds<T>(xs, S::ONES);
   for (int e = tid; e < S::ONES_N; e += NT) xs[S::ONES + e] = to_t<T>(1.f);
-  zero_lds<T>(dy1t - S::D1PRE, S::D1PRE + 8 * S::D1P, tid, NT);
-  zero_lds<T>(dys, 18 * 18 * 16, tid, NT);
-  zero_lds<T>(p1t, 31 * S::P1P, tid, NT);
+  zero_lds<T>(dy1t - S::D1PRE, S::D1PRE + 8 * S::D1P);
+  zero_lds<T>(dys, 18 * 18 * 16);
+  zero_lds<T>(p1t, 31 * S::P1P);
   for (int e = tid; e < S::P1P; e += NT) p1t[31 * S::P1P + e] = to_t<T>(1.f);
-  if constexpr (S::DY2) zero_lds<T>(dy2t, 16 * S::D2P, tid, NT);
+  if constexpr (S::DY2) zero_lds<T>(dy2t, 16 * S::D2P);
   // conv2 dgrad, two output rows per tile: out (Y = y + r, x, c) = sum over kh' in [-1, 4], kw, n of
   // dY2[y - kh'][x - kw][n] * W2[n][c][kh' + r][kw]  ->  B[(kh'+1)*5 + kw, n][(r, c)], zero where
   // kh' + r is outside 0..4.  N = (r, c) holds 12 live columns of 16 (was 6 with one row per tile).
@@ -1486,164 +1486,6 @@ void conv_bwd_kernel(BatchRef br, LenetConvBuffers cb, int ipb) {
   conv_bwd_block<T, NW>(br, cb, ipb, blockIdx.x, gridDim.x);
 }
 
-// The FC weight gradient on two SPARE waves of every conv_bwd workgroup (conv_bwd_wg_kernel): wgrad_kernel's wave
-// jobs (wg::wave_job, bit for bit the same partials), one or a few 32-row K-steps per barrier interval of conv_bwd,
-// the wave executing exactly conv_bwd's barrier count (NB = 2 + 3 * ipb: setup, three per image, the final
-// reduction) so the two roles share the workgroup's s_barrier.  What this replaces is the concurrent schedule's
-// fork / join: the FC wgrad on an aux stream beside conv_bwd cost ~5 us of idle time at the fork and ~6 us at the
-// join per step (rocprofv3 kernel trace, LeNet bf16 B=8192, profiles/r5_session1/NOTES.md) -- a captured graph's
-// cross-stream edge, not the kernels.  Jobs are dealt XCD-locally when both grids divide by 8 (job workgroup L ran
-// on XCD L % 8 in wgrad_kernel, where the head wrote its rows); a job of a sub-tile with no K-steps stores zeros
-// (as wgrad_kernel does); any step left after the last barrier is finished without one.
-constexpr int WGW_JOBS = 2;  // wave jobs with K-steps per spare wave (launch_lenet_conv_bwd_wg checks)
-template <typename T>
-DEV void fc_wgrad_lockstep(const wg::WgArgs<T>& a, const int nblk_tiles, const int nblocks, const int wave, const int NB) {
-  using M = Mma<T>;
-  using Frag = typename M::Frag;
-  constexpr int KV = M::KV, KC = M::KC, D = 3;  // K-steps of fragments in flight ahead of the MFMAs
-  const int g = blockIdx.x, G = gridDim.x;
-  const bool local = (G & 7) == 0 && (nblocks & 7) == 0;
-  const int x = g & 7;
-  const int r0 = local ? (g >> 3) * 2 + wave : g * 2 + wave;  // this wave's first job (XCD-local / global index)
-  const int rstep = local ? (G >> 3) * 2 : G * 2;
-  const int rend = local ? (nblocks >> 3) * 4 : nblocks * 4;
-  auto job_of = [&](int r, wg::WaveJob<T>& o) {
-    const int L = local ? x + 8 * (r >> 2) : (r >> 2);
-    return wg::wave_job(a, nblk_tiles, L, r & 3, o);
-  };
-  int S = 0;  // this wave's K-steps over all its jobs
-  for (int r = r0; r < rend; r += rstep) {
-    wg::WaveJob<T> o;
-    if (job_of(r, o)) S += o.nsteps;
-  }
-  const int per = max(1, (S + NB - 1) / NB);  // K-steps per barrier interval
-  const int GS = per * NB;                     // step slots: a barrier after every `per`
-  Frag ones;
-#pragma unroll
-  for (int q = 0; q < KV; ++q) M::set(ones, q, 1.f);
-  const Frag zf = M::zero();
-  f32x4 acc[2][2], done[2][2];
-#pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = done[mi][ni] = zero4();
-  // Two cursors over the jobs that have K-steps: `ld` issues fragments D steps ahead, `cp` computes.  Nothing but
-  // the four fragment loads per step touches memory inside the loop (the partials are stored after the last
-  // barrier; a wave has at most WGW_JOBS jobs with K-steps, the first one's sums parked in `done`), and an exhausted
-  // `ld` re-issues its last step's loads, so the compiler's vmcnt wait before a step's MFMAs counts the 2 x 4 loads
-  // issued after that step's own.
-  struct Cur {
-    int r, st;
-    wg::WaveJob<T> o;
-  };
-  auto seek = [&](Cur& c) {  // from c.r (inclusive) to the next job with K-steps (r = rend: none)
-    for (; c.r < rend; c.r += rstep)
-      if (job_of(c.r, c.o) && c.o.nsteps > 0) break;
-    c.st = 0;
-  };
-  auto advance = [&](Cur& c) {
-    if (c.st + 1 < c.o.nsteps) {
-      ++c.st;
-    } else {
-      Cur n = c;
-      n.r += rstep;
-      seek(n);
-      if (n.r < rend) c = n;  // exhausted: stays on its last step (its loads are re-issued, never used)
-    }
-  };
-  Frag f[D][4];  // f[slot][A0, A1, B0, B1]: step k's fragments in slot k % D (constant indices: unrolled by D)
-  Cur ld{r0, 0, {}}, cp{r0, 0, {}};
-  if (S > 0) {
-    seek(ld);
-    seek(cp);
-  }
-  auto load = [&](int slot) {
-    const wg::WaveJob<T>& o = ld.o;
-    const int rc = o.rows(ld.st, KC);
-    // A1 of a sub-tile whose second 16 rows are padding: row 0's fragment instead (every step issues the same four
-    // loads), replaced by zeros at use as in wgrad_kernel
-    f[slot][0] = M::load(o.ap0 + rc);
-    f[slot][1] = M::load(o.nv1 ? o.ap1 + rc : o.ap0 + rc);
-    f[slot][2] = M::load(o.bp0 + rc);
-    f[slot][3] = M::load(o.bp1 + rc);
-    advance(ld);
-  };
-  int jd = 0;  // jobs completed
-  auto compute = [&](int slot) {
-    const wg::WaveJob<T>& o = cp.o;
-    const Frag a0 = f[slot][0], a1 = o.nv1 ? f[slot][1] : zf;
-    const Frag b0 = o.sel0 == 0 ? f[slot][2] : (o.sel0 == 1 ? ones : zf);
-    const Frag b1 = o.sel1 == 0 ? f[slot][3] : (o.sel1 == 1 ? ones : zf);
-    M::mma(acc[0][0], a0, b0);
-    M::mma(acc[0][1], a0, b1);
-    M::mma(acc[1][0], a1, b0);
-    M::mma(acc[1][1], a1, b1);
-    if (cp.st + 1 == o.nsteps) {
-      if (jd == 0) {
-#pragma unroll
-        for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < 2; ++ni) {
-            done[mi][ni] = acc[mi][ni];
-            acc[mi][ni] = zero4();
-          }
-      }
-      ++jd;
-    }
-    advance(cp);
-  };
-  if (S > 0) {
-#pragma unroll
-    for (int d = 0; d < D; ++d) load(d);
-  }
-  int k = 0;
-  if (S > 0) {
-    for (; k + D <= GS; k += D) {
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        if (k + d < S) compute(d);
-        load(d);  // step k + d + D's fragments (or a re-issue past the end)
-        if ((k + d + 1) % per == 0) __syncthreads();  // conv_bwd's barriers: NB in all
-      }
-    }
-  }
-  for (; k < GS; ++k) {  // the last < D step slots (a step here has had its fragments since the prologue / loop)
-    if (k < S) {
-      const int d = k % D;
-      if (d == 0) compute(0);
-      else if (d == 1) compute(1);
-      else compute(2);
-    }
-    if ((k + 1) % per == 0) __syncthreads();
-  }
-  // the partials, after conv_bwd's last barrier: every job of this wave in order (a job without K-steps stores its
-  // zero partial, as wgrad_kernel's waves do)
-  int jn = 0;
-  for (int r = r0; r < rend; r += rstep) {
-    wg::WaveJob<T> o;
-    if (!job_of(r, o)) continue;
-    if (o.nsteps == 0) {
-      f32x4 z[2][2];
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) z[mi][ni] = zero4();
-      wg::wave_job_store(a, o, z);
-    } else {
-      wg::wave_job_store(a, o, jn == 0 ? done : acc);
-      ++jn;
-    }
-  }
-}
-
-template <typename T, int NW>
-__global__ __launch_bounds__((NW + 2) * 64) __attribute__((amdgpu_waves_per_eu(1)))
-void conv_bwd_wg_kernel(BatchRef br, LenetConvBuffers cb, int ipb, wg::WgArgs<T> fa, int nblk_tiles, int nblocks) {
-  const int w = wave_id();
-  if (w < NW) conv_bwd_block<T, NW>(br, cb, ipb, blockIdx.x, gridDim.x);
-  else fc_wgrad_lockstep<T>(fa, nblk_tiles, nblocks, w - NW, 2 + 3 * ipb);
-}
-
 // Small batches, one GPU, one FC batch split: conv_bwd and the FC weight gradient + SGD update (wg::
 // wgrad_sgd_tile, the wgrad_sgd_kernel body) in ONE launch -- workgroups [0, nconv) are conv_bwd's, the rest
 // one 32x32 FC output tile each (waves 4.. of a wider workgroup idle).  The two touch disjoint data (FC
@@ -1669,25 +1511,6 @@ static int default_bwd_target() { return 512; }
 static int bwd_ipb(int B, int target) {
   const int div = target > 0 ? target : default_bwd_target();
   return std::min(MAX_IPB, std::max(1, (B + div - 1) / div));
-}
-
-int launch_lenet_conv_bwd_wg(DType t, const BatchRef& br, const LenetConvBuffers& cb, const HeadBuffers& hb,
-                             int splits, float* slab_fc, int slab_ld, int head_rows, int* nslab_out, hipStream_t s,
-                             int target_blocks) {
-  if (t != DType::BF16) throw std::invalid_argument("conv_bwd + FC wgrad in one kernel: bf16 only");
-  const int ipb = bwd_ipb(br.B, target_blocks), grid = (br.B + ipb - 1) / ipb;
-  if (nslab_out) *nslab_out = grid;
-  int blk = 0;
-  wg::WgArgs<bf16> a = wg::make_args<bf16, LenetModel::Head, LenetModel>(hb, br.B, splits, slab_fc, slab_ld, nullptr, 7, &blk);
-  wg::configure_xcd(a, hb, br.B, splits, head_rows);
-  // every spare wave gets at most WGW_JOBS wave jobs (the job list of fc_wgrad_lockstep, dealt XCD-locally)
-  const bool local = grid % 8 == 0 && (blk * splits) % 8 == 0;
-  const int jobs = local ? (blk * splits) / 8 * 4 : blk * splits * 4, waves = local ? grid / 8 * 2 : grid * 2;
-  if ((jobs + waves - 1) / waves > WGW_JOBS)
-    throw std::invalid_argument("conv_bwd + FC wgrad in one kernel: more wave jobs than the spare waves hold");
-  if (br.B <= 0) return splits;
-  hipLaunchKernelGGL((conv_bwd_wg_kernel<bf16, 4>), dim3(grid), dim3(6 * 64), 0, s, br, cb, ipb, a, blk, blk * splits);
-  return splits;
 }
 
 int lenet_conv_bwd_blocks(int B, int target) {

@@ -40,16 +40,6 @@ struct WgArgs {
   unsigned long long* stamps;  // optional phase stamps (MNIST_AMD_STAMPS): slots [STAMP_WGRAD + block][16]
 };
 
-// Batch rows of a wgrad workgroup's K-steps (wgrad_kernel's split / XCD-aware mapping, see WgArgs).
-struct WgRows {
-  int xcd_ch, rs, m0, spc, x, contig, nch;
-  DEV int operator()(int st, int KC) const {  // first batch row of step st (monotonic in st)
-    if (xcd_ch == 0) return rs + st * KC;
-    const int m = m0 + st / spc;
-    return (contig ? x * (nch / 8) + m : x + 8 * m) * xcd_ch + (st % spc) * KC;
-  }
-};
-
 // Weight-gradient GEMM + SGD update for one GPU and ONE batch split (small batches), one 32x32 output tile
 // (`tile`) per 4-wave workgroup (waves >= 4 of a larger workgroup idle): every output
 // element is the whole gradient, so the update is the epilogue -- g = scale * dW, momentum, parameter,
@@ -179,96 +169,6 @@ WgArgs<T> make_args(const HeadBuffers& hb, int B, int& splits, float* slab, int 
   a.xcd_ch = 0;
   *blocks = blk;
   return a;
-}
-
-// XCD-aware row mapping (WgArgs::xcd_ch) when the head's row tiling (xcd_ch rows per head workgroup) is known and
-// the split count divides over 8 XCDs: then the grid is 1-D, workgroup L on XCD L % 8.  Returns whether it applies.
-template <typename T>
-bool configure_xcd(WgArgs<T>& a, const HeadBuffers& hb, int B, int splits, int xcd_ch) {
-  constexpr int KC = Mma<T>::KC;
-  if (!(xcd_ch > 0 && xcd_ch % KC == 0 && splits % 8 == 0)) return false;
-  a.xcd_ch = xcd_ch;
-  a.nch = (a.Bp + xcd_ch - 1) / xcd_ch;
-  a.sx = splits / 8;
-  const int head_grid = (rup(B, 32) + xcd_ch - 1) / xcd_ch;  // head_launch_mtw's grid
-  a.contig = hb.xcd && head_grid % 8 == 0 && a.nch == head_grid;
-  return true;
-}
-
-// ONE wave's share of wgrad_kernel (head.hip): wave w (a 32x32 sub-tile) of workgroup L of its grid -- the same
-// operands, the same K-steps in the same order, the same MFMA chain per output element, the same slab stores -- so
-// a kernel that runs these jobs on spare waves (lenet.hip conv_bwd_wg_kernel) produces wgrad_kernel's partials
-// bit for bit.  nblocks: workgroups of wgrad_kernel's grid (tiles x splits).
-template <typename T>
-struct WaveJob {
-  const T *ap0, *ap1, *bp0, *bp1;
-  int sel0, sel1, nv1, nsteps, n0, k0, j, split;
-  WgRows rows;
-};
-template <typename T>
-DEV bool wave_job(const WgArgs<T>& a, int nblk_tiles, int L, int w, WaveJob<T>& o) {
-  constexpr int KV = Mma<T>::KV, KC = Mma<T>::KC;
-  const int lane = threadIdx.x & 63, row = lane & 15, grp = lane >> 4;
-  int tile, split, nsteps;
-  WgRows rows{a.xcd_ch, 0, 0, 1, 0, a.contig, a.nch};
-  if (a.xcd_ch == 0) {  // wgrad_kernel's 2-D grid: blockIdx.x = tile, blockIdx.y = split
-    tile = L % nblk_tiles;
-    split = L / nblk_tiles;
-    rows.rs = split * a.rlen;
-    nsteps = (min(rows.rs + a.rlen, a.Bp) - rows.rs + KC - 1) / KC;
-  } else {
-    const int q = L >> 3;
-    rows.x = L & 7;
-    tile = q / a.sx;
-    const int sub = q % a.sx;
-    split = rows.x * a.sx + sub;
-    const int mx = a.contig ? a.nch / 8 : (rows.x < a.nch ? (a.nch - rows.x + 7) / 8 : 0);
-    rows.m0 = sub * mx / a.sx;
-    const int m1 = (sub + 1) * mx / a.sx;
-    rows.spc = a.xcd_ch / KC;
-    nsteps = (m1 - rows.m0) * rows.spc;
-  }
-  while (nsteps > 0 && rows(nsteps - 1, KC) >= a.Bp) --nsteps;  // steps past the (padded) batch
-  int j = 0;
-  while (j + 1 < a.njobs && tile >= a.job[j + 1].blk_begin) ++j;
-  const WgJob<T> J = j == 0 ? a.job[0] : (j == 1 ? a.job[1] : a.job[2]);
-  const int lb = tile - J.blk_begin, bn = lb / J.nblk_k, bk = lb % J.nblk_k;
-  o.n0 = bn * 64 + (w >> 1) * 32;
-  o.k0 = bk * 64 + (w & 1) * 32;
-  if (o.n0 >= J.N || o.k0 >= J.K + (J.bias ? 1 : 0)) return false;
-  o.nv1 = o.n0 + 16 < J.NP;
-  o.ap0 = J.dyT + (size_t)(o.n0 + row) * a.ldB + grp * KV;
-  o.ap1 = J.dyT + (size_t)(o.n0 + 16 + row) * a.ldB + grp * KV;
-  const int kk0 = o.k0 + row, kk1 = o.k0 + 16 + row;
-  o.bp0 = J.xT + (size_t)min(kk0, J.K > 0 ? J.K - 1 : 0) * a.ldB + grp * KV;
-  o.bp1 = J.xT + (size_t)min(kk1, J.K > 0 ? J.K - 1 : 0) * a.ldB + grp * KV;
-  o.sel0 = kk0 < J.K ? 0 : (kk0 == J.K && J.bias ? 1 : 2);
-  o.sel1 = kk1 < J.K ? 0 : (kk1 == J.K && J.bias ? 1 : 2);
-  o.nsteps = nsteps;
-  o.j = j;
-  o.split = split;
-  o.rows = rows;
-  return true;
-}
-
-// wgrad_kernel's epilogue for one wave job: the 32x32 partial into the split's slab row (parameter order)
-template <typename T>
-DEV void wave_job_store(const WgArgs<T>& a, const WaveJob<T>& o, const f32x4 (&acc)[2][2]) {
-  const int lane = threadIdx.x & 63, row = lane & 15, grp = lane >> 4;
-  const WgJob<T> J = o.j == 0 ? a.job[0] : (o.j == 1 ? a.job[1] : a.job[2]);
-  float* out = a.slab + (size_t)o.split * a.slab_ld + J.out_off;
-#pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < 2; ++ni) {
-      const int k = o.k0 + ni * 16 + row;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int n = o.n0 + mi * 16 + grp * 4 + i;
-        const int q = n >= J.N ? -1 : (k < J.K ? n * J.K + k : (k == J.K && J.bias ? J.N * J.K + n : -1));
-        if (q >= 0) out[q] = acc[mi][ni][i];
-      }
-    }
 }
 
 }  // namespace wg

@@ -96,10 +96,6 @@ Trainer::Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const
   nparam_ = model_nparam(model_);
   max_conv_slabs_ = model_ == ModelKind::LENET ? lenet_conv_bwd_max_blocks(batch_, 0) : 0;
   concurrent_ = concurrent_mode() != 0;
-  {  // MNIST_AMD_WGWAVES=1: start with the FC wgrad on conv_bwd's spare waves (the calibration may change it)
-    const char* e = std::getenv("MNIST_AMD_WGWAVES");
-    bwd_wg_ = e && *e == '1';
-  }
   const int ps = model_phase_split(model_);  // default buckets: one per backward phase (see Plan)
   buckets_.push_back({ps, nparam_, 0});
   buckets_.push_back({0, ps, 1});
@@ -156,10 +152,6 @@ int Trainer::fc_splits_for(int B) const {
   int splits = std::max(1, std::min(fc_splits_, Bp / KC));
   const int rlen = ((Bp + splits - 1) / splits + KC - 1) / KC * KC;
   return (Bp + rlen - 1) / rlen;
-}
-
-bool Trainer::bwd_wg_applies(int B) const {
-  return model_ == ModelKind::LENET && dtype_ == DType::BF16 && fc_splits_for(B) > 1;
 }
 
 int Trainer::pack_size() const { return model_pack_size(model_); }
@@ -378,19 +370,6 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     post_launch(s);
   }
 
-  if (model_ == ModelKind::LENET && !comm && bwd_wg_ && bwd_wg_applies(B)) {
-    // one stream: conv_bwd with the FC weight gradient on its spare waves, then ONE reduce + SGD over every
-    // parameter (bitwise the serial and concurrent schedules: the same partials, the same reduction)
-    int nslab = 0;
-    const int splits = launch_lenet_conv_bwd_wg(dtype_, br, conv_buffers(B), hb, fc_splits_, ptr<float>(p_.slab_fc),
-                                                nparam_, hrows, &nslab, s, bwd_blocks_);
-    post_launch(s);
-    launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
-                      nparam_, splits, cp, 0, nparam_, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
-                      ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, ptr<int32_t>(p_.step), s);
-    post_launch(s);
-    return;
-  }
   if (model_ == ModelKind::LENET && (comm || concurrent_)) {
     // fork: conv_bwd on the main stream (enqueued first, so its one-round grid is dispatched whole:
     // measured wgrad-first 0.1692 ms/step, conv_bwd-first 0.1565, serial 0.1671), the FC wgrad (no LDS,
@@ -673,7 +652,7 @@ void Trainer::drop(GraphSlot& g) {
 // replays back to back; anything that changes the kernels' arguments clears the cache (invalidate).
 uint64_t Trainer::schedule_key(int nsteps) const {
   return (static_cast<uint64_t>(nsteps) << 40) | (static_cast<uint64_t>(bwd_blocks_) << 8) |
-         (static_cast<uint64_t>(bwd_wg_) << 5) | (static_cast<uint64_t>(fwd_head_) << 4) | (static_cast<uint64_t>(comm_enabled_) << 3) | (static_cast<uint64_t>(concurrent_) << 2) |
+         (static_cast<uint64_t>(fwd_head_) << 4) | (static_cast<uint64_t>(comm_enabled_) << 3) | (static_cast<uint64_t>(concurrent_) << 2) |
          static_cast<uint64_t>(plan_);
 }
 

@@ -88,12 +88,6 @@ class Trainer {
   // single-GPU LeNet schedule: FC wgrad + FC update on the aux stream beside conv_bwd (true) or serial
   void set_concurrent(bool on) { concurrent_ = on; }
   bool concurrent() const { return concurrent_; }
-  // single-GPU LeNet bf16, several FC batch splits: the FC weight gradient on spare waves of the conv_bwd workgroups
-  // (launch_lenet_conv_bwd_wg) instead of an aux-stream branch -- one stream, no fork / join; the closing reduce +
-  // SGD covers every parameter.  Part of the graph-cache key; applies when bwd_wg_applies(B).
-  void set_bwd_wg(bool on) { bwd_wg_ = on; }
-  bool bwd_wg() const { return bwd_wg_; }
-  bool bwd_wg_applies(int B) const;
   // MLP, one GPU, one FC batch split: SGD as the wgrad kernel's epilogue (true) or wgrad + reduce_sgd
   void set_fuse_wgrad_sgd(bool on) { fuse_wgrad_sgd_ = on; invalidate(); }
   // LeNet bf16 (large batches): conv_fwd + FC head as ONE kernel (fwd_head_kernel, true) or the two
@@ -202,7 +196,6 @@ class Trainer {
   int world_ = 1;
   Plan plan_ = Plan::JOIN;
   bool concurrent_ = true;
-  bool bwd_wg_ = false;
   bool fuse_wgrad_sgd_ = true;
   bool fwd_head_ = true;
   bool comm_enabled_ = true;

@@ -387,18 +387,15 @@ class NativeTrainer:
     def current_schedule(self) -> dict:
         """The installed schedule as a complete :meth:`apply_plan` candidate."""
         return {"plan": self.plan, "bwd_blocks": int(self.rt.bwd_blocks) if self.model_name == "lenet5" else 0,
-                "concurrent": bool(self.rt.concurrent), "fwd_head": bool(self.rt.fwd_head),
-                "bwd_wg": bool(self.rt.bwd_wg)}
+                "concurrent": bool(self.rt.concurrent), "fwd_head": bool(self.rt.fwd_head)}
 
     def apply_plan(self, cfg: dict) -> None:
-        """Install one candidate of :meth:`autotune_plan` ({plan, bwd_blocks, concurrent, fwd_head, bwd_wg, comm}).
+        """Install one candidate of :meth:`autotune_plan` ({plan, bwd_blocks, concurrent, fwd_head, comm}).
         Keys a candidate leaves out take their defaults (join, default conv_bwd grid, concurrent, fused
-        forward + head kernel, FC wgrad not on conv_bwd's waves, comm on), so a candidate names ONE cached graph
-        whatever was installed before it.  ``comm: False`` (timing only) runs the local schedule without
-        collectives."""
+        forward + head kernel, comm on), so a candidate names ONE cached graph whatever was installed
+        before it.  ``comm: False`` (timing only) runs the local schedule without collectives."""
         self.rt.comm_enabled = bool(cfg.get("comm", True))
         self.rt.set_concurrent(bool(cfg.get("concurrent", True)))
-        self.rt.set_bwd_wg(bool(cfg.get("bwd_wg", False)))
         self.rt.set_fwd_head(bool(cfg.get("fwd_head", True)))
         self.set_plan(cfg.get("plan", "join"), int(cfg.get("bwd_blocks", 0)))
 
@@ -559,8 +556,7 @@ class NativeTrainer:
                 if ovl:
                     candidates["overlap"] = dict(plan="overlap")
             elif self.model_name == "lenet5":
-                candidates = local_plan_candidates(fwd_head=self.fwd_head_applies(),
-                                                   bwd_wg=bool(self.rt.bwd_wg_applies(self.batch)))
+                candidates = local_plan_candidates(fwd_head=self.fwd_head_applies())
             else:
                 return {"chosen": "local", "timings_ms": {}}
         prefer = "join" if dp else "concurrent"

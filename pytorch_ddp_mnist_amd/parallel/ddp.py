@@ -81,19 +81,14 @@ def mlp_plan_candidates() -> Dict[str, dict]:
     return {"join": dict(plan="join"), "split": dict(plan="split")}
 
 
-def local_plan_candidates(fwd_head: bool = False, bwd_wg: bool = False) -> Dict[str, dict]:
+def local_plan_candidates(fwd_head: bool = False) -> Dict[str, dict]:
     """Single-GPU LeNet schedules: the FC weight gradient + FC update on an aux stream beside
     conv_bwd (``concurrent``, the default) or after it (``serial``).  ``fwd_head`` (bf16, large
     batches: the fused forward + FC head kernel applies): also the same schedule with the two separate
-    kernels (``separate``), so the calibration measures what the fusion is worth on this box.
-    ``bwd_wg`` (bf16, several FC batch splits): also the one-stream schedule with the FC weight gradient on
-    spare waves of the conv_bwd workgroups (``wgwaves``: no fork / join, csrc/kernels/lenet.hip
-    conv_bwd_wg_kernel)."""
+    kernels (``separate``), so the calibration measures what the fusion is worth on this box."""
     c = {"concurrent": dict(concurrent=True), "serial": dict(concurrent=False)}
     if fwd_head:
         c["separate"] = dict(concurrent=True, fwd_head=False)
-    if bwd_wg:
-        c["wgwaves"] = dict(concurrent=False, bwd_wg=True)
     return c
 
 

@@ -10,9 +10,8 @@ rank's "all-reduced" gradient is its own): they must equal a local run at half t
 ``_k<k>`` variants run the steps as ONE k-step graph (run_steps), whose steps may leave the aux
 branch join to the next step's head; they must equal the same number of single-step graphs.
 Usage: python scripts/sched_equiv.py [--model mlp|lenet5] [--dtype bf16|fp32] [--batch B] VARIANT [VARIANT ...]
-  VARIANT = {local,local_halflr,join,split,overlap,wgw}[_b<blocks>][_w2][_k<k>][_t<rows>]   (overlap: LeNet, world-1
-  one-shot; wgw: the FC wgrad on conv_bwd's spare waves; _t<rows>: one more step of a partial batch of <rows> rows
-  after the full ones, eager launch)
+  VARIANT = {local,local_halflr,join,split,overlap}[_b<blocks>][_w2][_k<k>][_t<rows>]   (overlap: LeNet, world-1
+  one-shot; _t<rows>: one more step of a partial batch of <rows> rows after the full ones, eager launch)
 """
 import argparse
 import hashlib
@@ -43,7 +42,7 @@ C = load_c()
 order = torch.randperm(N, generator=torch.Generator().manual_seed(1)).to(torch.int32)
 
 for v in a.variants:
-    m = re.fullmatch(r"(local_halflr|local|join|split|overlap|wgw)(?:_b(\d+))?(_w2)?(?:_k(\d+))?(?:_t(\d+))?", v)
+    m = re.fullmatch(r"(local_halflr|local|join|split|overlap)(?:_b(\d+))?(_w2)?(?:_k(\d+))?(?:_t(\d+))?", v)
     if not m:
         raise SystemExit(f"unknown variant {v}")
     kind, blocks, w2, k = m.group(1), int(m.group(2) or 0), bool(m.group(3)), int(m.group(4) or 0)
@@ -60,8 +59,6 @@ for v in a.variants:
         fc, conv = C.OneShotAllReduce(0, 1, 0, tr.nparam), C.OneShotAllReduce(0, 1, 0, int(tr.rt.conv_params))
         tr.attach_overlap(fc, conv, 2 if w2 else 1)
         tr.set_plan("overlap", blocks)
-    elif kind == "wgw":  # one stream, the FC wgrad on conv_bwd's spare waves (LeNet bf16, several FC splits)
-        tr.apply_plan(dict(concurrent=False, bwd_wg=True, bwd_blocks=blocks))
     elif blocks:
         tr.rt.set_bwd_blocks(blocks)
     tr.set_epoch_indices(order)

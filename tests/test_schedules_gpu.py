@@ -66,19 +66,3 @@ def test_mlp_schedules_bitwise_equal(native):
         assert d[k] == d["local"], k
     assert d["join_w2"] == d["local_halflr"] and d["split_w2"] == d["local_halflr"]
 
-
-
-@pytest.mark.timeout(900)
-@pytest.mark.parametrize("batch", [8192, 2048])
-def test_wgwaves_bitwise_equal(native, batch):
-    """LeNet bf16, several FC batch splits: the one-stream schedule with the FC weight gradient on spare waves of the
-    conv_bwd workgroups (lenet.hip conv_bwd_wg_kernel; XCD-aware wave jobs at B = 8192, the 2-D split grid at
-    B = 2048) is bitwise the serial and the concurrent schedules, for single steps, a 4-step graph and a partial
-    last batch."""
-    extra = ("--batch", str(batch), "--steps", "3")
-    t = f"_t{batch // 2 + 37}"
-    wgw = _digests({"MNIST_AMD_CONCURRENT": "0"}, ["wgw", "wgw_k3", "wgw" + t], extra=extra)
-    ser = _digests({"MNIST_AMD_CONCURRENT": "0"}, ["local", "local" + t], extra=extra)
-    conc = _digests({"MNIST_AMD_CONCURRENT": "1"}, ["local"], extra=extra)
-    assert wgw["wgw"] == ser["local"] == conc["local"] == wgw["wgw_k3"], (wgw, ser, conc)
-    assert wgw["wgw" + t] == ser["local" + t], (wgw, ser)
