@@ -1,7 +1,6 @@
 #!/bin/bash
 # Round-5 measurement pass (one gpurun call):  scripts/gpu_r5_prof.sh TAG
-# benches of every BASELINE-relevant config, kernel-time profiles, the small-batch calibration check
-# (MNIST_AMD_SMALL_SERIAL=0: the calibration decides at B=128) and the one-shot latency breakdown.
+# benches of every BASELINE-relevant config, kernel-time profiles and the one-shot latency breakdown.
 # Every GPU step has its own limit; the chain stops at the first failure.
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -23,11 +22,8 @@ $B --model mlp --dtype fp32 --batch 128 --steps 2000 --warmup 50 >> $J 2>> $E &&
 $B --batch 128 --steps 2000 --warmup 50 >> $J 2>> $E &&
 $B --batch 128 --dtype fp32 --steps 2000 --warmup 50 >> $J 2>> $E &&
 $B --dtype fp32 --steps 200 --warmup 10 >> $J 2>> $E &&
-echo "calibration at B=128 with the small-batch rule off" &&
-MNIST_AMD_SMALL_SERIAL=0 $B --batch 128 --steps 2000 --warmup 50 > "$OUT/calib_b128_auto.jsonl" 2>> $E &&
-MNIST_AMD_SMALL_SERIAL=0 $B --batch 128 --dtype fp32 --steps 2000 --warmup 50 >> "$OUT/calib_b128_auto.jsonl" 2>> $E &&
-MNIST_AMD_SMALL_SERIAL=0 $B --batch 1024 --steps 1000 --warmup 50 >> "$OUT/calib_b128_auto.jsonl" 2>> $E &&
-$B --batch 1024 --steps 1000 --warmup 50 >> "$OUT/calib_b128_auto.jsonl" 2>> $E &&
+$B --batch 1024 --steps 1000 --warmup 50 >> $J 2>> $E &&
+$B --model mlp --dtype fp32 --batch 8192 --steps 500 --warmup 20 >> $J 2>> $E &&
 echo "one-shot latency" &&
 timeout -k 10 180 python scripts/diag/oneshot_lat.py > "$OUT/oneshot_lat.txt" 2>&1 &&
 echo "kernel profiles" &&
