@@ -21,6 +21,8 @@ typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
 typedef __bf16 bf16;
 
 #define DEV __device__ __forceinline__
@@ -93,6 +95,13 @@ template <> struct Mma<bf16> {
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc, 0, 0, 0);
   }
   static DEV Frag load(const bf16* p) { Frag f; f.v = *reinterpret_cast<const bf16x8*>(p); return f; }
+  // a fragment at an 8-byte (not 16-byte) aligned address: two 8-byte reads (a 16-byte read would be under-aligned)
+  static DEV Frag load8(const bf16* p) {
+    const u32x2 lo = *reinterpret_cast<const u32x2*>(p), hi = *reinterpret_cast<const u32x2*>(p + 4);
+    Frag f;
+    f.v = __builtin_bit_cast(bf16x8, u32x4{lo[0], lo[1], hi[0], hi[1]});
+    return f;
+  }
   static DEV Frag zero() {
     Frag f;
     for (int j = 0; j < 8; ++j) f.v[j] = (bf16)0.f;
@@ -105,8 +114,6 @@ template <> struct Mma<bf16> {
 // Streaming (non-temporal) global stores for kernel outputs that only a LATER kernel reads: they are not
 // kept dirty in this XCD's L2, so the end-of-kernel L2 write-back (cross-XCD coherence at the kernel
 // boundary) has less to flush before the next kernel may start.
-typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
-typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
 #ifndef MNIST_NT_STORES
 #define MNIST_NT_STORES 1
 #endif

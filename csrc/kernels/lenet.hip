@@ -82,9 +82,13 @@ DEV typename Mma<T>::Frag ones_frag() {
 template <typename T>
 struct FwdSmem {
   static constexpr int XP = 1048;  // plane pitch (32x32 + pad): 2-way worst-case conflicts (was 8-way at 1024)
-  static constexpr int OFF_XS = 0;                                        // [8][XP] T
-  static constexpr int XTAIL = 64;  // zeroed tail: conv1's all-zero kernel row kh' = 7 reads 1 row past plane 7
-  static constexpr int OFF_P1 = rup((8 * XP + XTAIL) * (int)sizeof(T), 16);  // [196][8] T   pool1 output (conv2 im2col)
+  // shifted planes: fp32, 8 (a 4-float run at any column is a 16-byte aligned read of plane x & 7); bf16, 4 -- an
+  // 8-tap run starting at column x is at column x & ~3 of plane x & 3, an 8-byte aligned pair of 8-byte reads
+  // (Mma::load8) -- so the fused forward + head workgroup fits three per CU (52 KB of LDS instead of 69 KB)
+  static constexpr int NPL = sizeof(T) == 2 ? 4 : 8;
+  static constexpr int OFF_XS = 0;                                        // [NPL][XP] T
+  static constexpr int XTAIL = 64;  // zeroed tail: conv1's all-zero kernel row kh' = 7 reads 1 row past the last plane
+  static constexpr int OFF_P1 = rup((NPL * XP + XTAIL) * (int)sizeof(T), 16);  // [196][8] T   pool1 output (conv2 im2col)
   static constexpr int OFF_P1C = rup(OFF_P1 + 196 * 8 * (int)sizeof(T), 16);  // [6][P1CP] T pool1, CHW16 (-> HBM)
   static constexpr int OFF_M1 = rup(OFF_P1C + P1IMG * (int)sizeof(T), 16);    // [6][M1CP] u8 pool1 codes, CHW16
   static constexpr int OFF_P2 = rup(OFF_M1 + M1IMG, 16);                  // [400] T      pool2 output (NCHW)
@@ -220,10 +224,14 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
     for (int kc = 0; kc < C1CH; ++kc) {
       const int k0 = kc * KC + grp * KV;
       const int khp = k0 >> 3, xx = xt + (k0 & 7);
-      c1base[kc] = (xx & 7) * S::XP + ((e >> 1) + khp) * 32 + 8 * wc + (xx & ~7);
+      c1base[kc] = (xx & (S::NPL - 1)) * S::XP + ((e >> 1) + khp) * 32 + 8 * wc + (xx & ~(S::NPL - 1));
     }
   }
   const bool c1valid = 4 * wc + grp < 14;  // column group 3, lane groups 2-3: padding columns 14, 15
+  auto c1_load = [&](int off) {  // conv1 A fragment (bf16: 8-byte aligned, see FwdSmem::NPL)
+    if constexpr (sizeof(T) == 2) return M::load8(xs + off);
+    else return M::load(xs + off);
+  };
   // Branch-free epilogues: a lane without an output (padding column / channel) stores into the junk area.  Each
   // store address is a per-lane base (real or junk, chosen ONCE) plus a per-tile immediate offset, so the 7
   // tiles' stores need 3 address registers, not 21, and no exec-masked branch breaks the lgkmcnt counting.
@@ -307,7 +315,7 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
     }
   };
 
-  zero_lds<T>(xs, 8 * S::XP + S::XTAIL, tid, NT);
+  zero_lds<T>(xs, S::NPL * S::XP + S::XTAIL, tid, NT);
   if (TRAIN) {
     zero_lds<T>(p1c, P1IMG, tid, NT);
     zero_lds<uint8_t>(m1s, M1IMG, tid, NT);
@@ -351,20 +359,16 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
           D[k] = __builtin_bit_cast(uint32_t, p2v);
         }
         const uint32_t msk = 0u - (uint32_t)sh;  // bit blend: a ?: select here becomes scratch-indexed D
+        // 4 planes: this thread writes planes 2 sh, 2 sh + 1 (window E = D shifted by sh dwords = 2 sh taps)
 #pragma unroll
-        for (int j = 0; j < 6; ++j) E[j] = (D[j] & ~msk) | (D[j + 2] & msk);
+        for (int j = 0; j < 5; ++j) E[j] = (D[j] & ~msk) | (D[j + 1] & msk);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < 2; ++q) {
           uint4 o;
           uint32_t* ov = reinterpret_cast<uint32_t*>(&o);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            if (q == 0) ov[j] = E[j];
-            else if (q == 1) ov[j] = __builtin_amdgcn_alignbyte(E[j + 1], E[j], 2);
-            else if (q == 2) ov[j] = E[j + 1];
-            else ov[j] = __builtin_amdgcn_alignbyte(E[j + 2], E[j + 1], 2);
-          }
-          *reinterpret_cast<uint4*>(dst + (4 * sh + q) * S::XP) = o;
+          for (int j = 0; j < 4; ++j) ov[j] = q == 0 ? E[j] : __builtin_amdgcn_alignbyte(E[j + 1], E[j], 2);
+          *reinterpret_cast<uint4*>(dst + (2 * sh + q) * S::XP) = o;
         }
       } else {
         // bit blend instead of `sh ? f[i + 4 + q] : f[i + q]`: hipcc turned that select into a lane-indexed
@@ -403,7 +407,7 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
         constexpr int T0 = decltype(t0c)::value, T1 = decltype(t1c)::value;
         Frag fa[C1CH];
 #pragma unroll
-        for (int kc = 0; kc < C1CH; ++kc) fa[kc] = M::load(xs + c1base[kc] + T0 * 128);
+        for (int kc = 0; kc < C1CH; ++kc) fa[kc] = c1_load(c1base[kc] + T0 * 128);
         f32x4 prev = zero4();
 #pragma unroll
         for (int t = T0; t < T1; ++t) {
@@ -414,7 +418,7 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
 #pragma unroll
             for (int kc = 0; kc < HC; ++kc) fa[kc] = fa[kc + HC];
 #pragma unroll
-            for (int kc = HC; kc < C1CH; ++kc) fa[kc] = M::load(xs + c1base[kc] + (t + 1) * 128);
+            for (int kc = HC; kc < C1CH; ++kc) fa[kc] = c1_load(c1base[kc] + (t + 1) * 128);
           }
           if (t > T0) c1_epi(t - 1, prev);
           prev = acc;
