@@ -82,10 +82,10 @@ DEV typename Mma<T>::Frag ones_frag() {
 template <typename T>
 struct FwdSmem {
   static constexpr int XP = 1048;  // plane pitch (32x32 + pad): 2-way worst-case conflicts (was 8-way at 1024)
-  // shifted planes: fp32, 8 (a 4-float run at any column is a 16-byte aligned read of plane x & 7); bf16, 4 -- an
-  // 8-tap run starting at column x is at column x & ~3 of plane x & 3, an 8-byte aligned pair of 8-byte reads
-  // (Mma::load8) -- so the fused forward + head workgroup fits three per CU (52 KB of LDS instead of 69 KB)
-  static constexpr int NPL = sizeof(T) == 2 ? 4 : 8;
+  // 4 shifted planes: a K-chunk run of taps starting at column x is at column x & ~3 of plane x & 3 -- fp32 (4 taps
+  // = 16 bytes) one aligned 16-byte read; bf16 (8 taps) an 8-byte aligned pair of 8-byte reads (Mma::load8).
+  // (Was 8 planes, every bf16 read 16-byte aligned: 8.4 KB more LDS and twice the staging stores per image.)
+  static constexpr int NPL = 4;
   static constexpr int OFF_XS = 0;                                        // [NPL][XP] T
   static constexpr int XTAIL = 64;  // zeroed tail: conv1's all-zero kernel row kh' = 7 reads 1 row past the last plane
   static constexpr int OFF_P1 = rup((NPL * XP + XTAIL) * (int)sizeof(T), 16);  // [196][8] T   pool1 output (conv2 im2col)
@@ -371,17 +371,17 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
           *reinterpret_cast<uint4*>(dst + (2 * sh + q) * S::XP) = o;
         }
       } else {
-        // bit blend instead of `sh ? f[i + 4 + q] : f[i + q]`: hipcc turned that select into a lane-indexed
-        // load of f[] from scratch memory (80 B/lane of scratch traffic per image)
+        // bit blend instead of `sh ? f[i + 2 + q] : f[i + q]`: hipcc turned that select into a lane-indexed
+        // load of f[] from scratch memory (80 B/lane of scratch traffic per image); planes 2 sh, 2 sh + 1
         const uint32_t msk = 0u - (uint32_t)sh;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < 2; ++q) {
           float o[8];
 #pragma unroll
           for (int i = 0; i < 8; ++i)
             o[i] = __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, f[i + q]) & ~msk) |
-                                                 (__builtin_bit_cast(uint32_t, f[i + 4 + q]) & msk));
-          float* d = reinterpret_cast<float*>(dst) + (4 * sh + q) * S::XP;
+                                                 (__builtin_bit_cast(uint32_t, f[i + 2 + q]) & msk));
+          float* d = reinterpret_cast<float*>(dst) + (2 * sh + q) * S::XP;
           *reinterpret_cast<f32x4*>(d) = f32x4{o[0], o[1], o[2], o[3]};
           *reinterpret_cast<f32x4*>(d + 4) = f32x4{o[4], o[5], o[6], o[7]};
         }
