@@ -82,10 +82,11 @@ DEV typename Mma<T>::Frag ones_frag() {
 template <typename T>
 struct FwdSmem {
   static constexpr int XP = 1048;  // plane pitch (32x32 + pad): 2-way worst-case conflicts (was 8-way at 1024)
-  // 4 shifted planes: a K-chunk run of taps starting at column x is at column x & ~3 of plane x & 3 -- fp32 (4 taps
-  // = 16 bytes) one aligned 16-byte read; bf16 (8 taps) an 8-byte aligned pair of 8-byte reads (Mma::load8).
-  // (Was 8 planes, every bf16 read 16-byte aligned: 8.4 KB more LDS and twice the staging stores per image.)
-  static constexpr int NPL = 4;
+  // shifted planes: a K-chunk run of taps starting at column x is at column x & ~(NPL-1) of plane x & (NPL-1) --
+  // bf16, 4 planes: 8 taps = an 8-byte aligned pair of 8-byte reads (Mma::load8); fp32, 2 planes: 4 taps = an
+  // 8-byte aligned pair of 8-byte reads.  (Was 8 planes with every read 16-byte aligned: more LDS and staging
+  // stores per image.  bf16 with 2 planes -- 4-byte reads -- measured 3.8 % slower at B=1024, neutral at 8192.)
+  static constexpr int NPL = sizeof(T) == 2 ? 4 : 2;
   static constexpr int OFF_XS = 0;                                        // [NPL][XP] T
   static constexpr int XTAIL = 64;  // zeroed tail: conv1's all-zero kernel row kh' = 7 reads 1 row past the last plane
   static constexpr int OFF_P1 = rup((NPL * XP + XTAIL) * (int)sizeof(T), 16);  // [196][8] T   pool1 output (conv2 im2col)
@@ -228,9 +229,15 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
     }
   }
   const bool c1valid = 4 * wc + grp < 14;  // column group 3, lane groups 2-3: padding columns 14, 15
-  auto c1_load = [&](int off) {  // conv1 A fragment (bf16: 8-byte aligned, see FwdSmem::NPL)
-    if constexpr (sizeof(T) == 2) return M::load8(xs + off);
-    else return M::load(xs + off);
+  auto c1_load = [&](int off) {  // conv1 A fragment at an 8-byte aligned address (FwdSmem::NPL): two 8-byte reads
+    if constexpr (sizeof(T) == 2) {
+      return M::load8(xs + off);
+    } else {
+      typename M::Frag f;
+      const u32x2 lo = *reinterpret_cast<const u32x2*>(xs + off), hi = *reinterpret_cast<const u32x2*>(xs + off + 2);
+      f.v = __builtin_bit_cast(f32x4, u32x4{lo[0], lo[1], hi[0], hi[1]});
+      return f;
+    }
   };
   // Branch-free epilogues: a lane without an output (padding column / channel) stores into the junk area.  Each
   // store address is a per-lane base (real or junk, chosen ONCE) plus a per-tile immediate offset, so the 7
@@ -371,17 +378,17 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
           *reinterpret_cast<uint4*>(dst + (2 * sh + q) * S::XP) = o;
         }
       } else {
-        // bit blend instead of `sh ? f[i + 2 + q] : f[i + q]`: hipcc turned that select into a lane-indexed
-        // load of f[] from scratch memory (80 B/lane of scratch traffic per image); planes 2 sh, 2 sh + 1
+        // bit blend instead of `sh ? f[i + 1] : f[i]`: hipcc turned that select into a lane-indexed
+        // load of f[] from scratch memory (80 B/lane of scratch traffic per image); plane sh
         const uint32_t msk = 0u - (uint32_t)sh;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        {
+          constexpr int q = 0;
           float o[8];
 #pragma unroll
           for (int i = 0; i < 8; ++i)
             o[i] = __builtin_bit_cast(float, (__builtin_bit_cast(uint32_t, f[i + q]) & ~msk) |
-                                                 (__builtin_bit_cast(uint32_t, f[i + 2 + q]) & msk));
-          float* d = reinterpret_cast<float*>(dst) + (2 * sh + q) * S::XP;
+                                                 (__builtin_bit_cast(uint32_t, f[i + 1 + q]) & msk));
+          float* d = reinterpret_cast<float*>(dst) + sh * S::XP;
           *reinterpret_cast<f32x4*>(d) = f32x4{o[0], o[1], o[2], o[3]};
           *reinterpret_cast<f32x4*>(d + 4) = f32x4{o[4], o[5], o[6], o[7]};
         }
