@@ -266,6 +266,7 @@ PYBIND11_MODULE(_C, m) {
       .def("invalidate", &Trainer::invalidate)
       .def("release", &Trainer::release, py::call_guard<py::gil_scoped_release>())
       .def("destroy", &Trainer::destroy, py::call_guard<py::gil_scoped_release>())
+      .def("graph_nodes", &Trainer::graph_nodes)
       .def_property_readonly("captured", &Trainer::captured)
       .def_property_readonly("nparam", &Trainer::nparam)
       .def_property_readonly("pack_size", &Trainer::pack_size)

@@ -154,6 +154,37 @@ int Trainer::fc_splits_for(int B) const {
   return (Bp + rlen - 1) / rlen;
 }
 
+std::vector<std::string> Trainer::graph_nodes() const {
+  std::vector<std::string> out;
+  const GraphSlot* g = find_graph(1);
+  if (!g || !g->graph) return out;
+  size_t n = 0;
+  HIP_CHECK(hipGraphGetNodes(g->graph, nullptr, &n));
+  std::vector<hipGraphNode_t> nodes(n);
+  HIP_CHECK(hipGraphGetNodes(g->graph, nodes.data(), &n));
+  for (size_t i = 0; i < n; ++i) {
+    hipGraphNodeType t;
+    HIP_CHECK(hipGraphNodeGetType(nodes[i], &t));
+    size_t nd = 0;
+    HIP_CHECK(hipGraphNodeGetDependencies(nodes[i], nullptr, &nd));
+    std::vector<hipGraphNode_t> deps(nd);
+    if (nd) HIP_CHECK(hipGraphNodeGetDependencies(nodes[i], deps.data(), &nd));
+    std::string line = std::to_string(i) + " type=" + std::to_string(static_cast<int>(t));
+    if (t == hipGraphNodeTypeKernel) {
+      hipKernelNodeParams kp{};
+      if (hipGraphKernelNodeGetParams(nodes[i], &kp) == hipSuccess)
+        line += " grid=" + std::to_string(kp.gridDim.x) + "x" + std::to_string(kp.gridDim.y) + " block=" +
+                std::to_string(kp.blockDim.x);
+    }
+    line += " deps=";
+    for (size_t d = 0; d < nd; ++d)
+      for (size_t j = 0; j < n; ++j)
+        if (nodes[j] == deps[d]) line += std::to_string(j) + ",";
+    out.push_back(line);
+  }
+  return out;
+}
+
 int Trainer::pack_size() const { return model_pack_size(model_); }
 int Trainer::phase_split() const { return model_phase_split(model_); }
 int Trainer::conv_params() const { return model_conv_params(model_); }

@@ -144,6 +144,9 @@ class Trainer {
   void invalidate();        // drop every cached graph
   // teardown: drop the graphs (they captured collectives), drain the side streams, detach the communicator
   void release();
+  // the cached single-step graph of the current schedule, one line per node: "index type deps" (diagnostics:
+  // what the captured step looks like to the runtime -- kernel / event / memset / empty nodes and their edges)
+  std::vector<std::string> graph_nodes() const;
   // final teardown at a point the caller chooses (NativeTrainer.close): release(), then the native streams, events
   // and device counters are destroyed while the HIP runtime is certainly alive (not from a destructor that may run
   // during interpreter shutdown, after torch's own HIP teardown).  Idempotent; the object is unusable afterwards.
