@@ -77,7 +77,7 @@ PYBIND11_MODULE(_C, m) {
   m.attr("L1_SPLIT_MAX_B") = L1_SPLIT_MAX_B;
   m.attr("STAMP_ROWS") = STAMP_ROWS;
 #ifdef MNIST_AMD_F32_SPLIT
-  m.attr("F32_SPLIT") = 3;  // fp32 products as 3-part bf16 MFMAs (common.h Mma<float>, opt-in build)
+  m.attr("F32_SPLIT") = 3;  // fp32 products as exact 3-part bf16 splits on 16x16x32 MFMAs (common.h Mma<float>, opt-in build)
 #else
   m.attr("F32_SPLIT") = 0;
 #endif

@@ -43,42 +43,38 @@ template <> struct Mma<float> {
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[3], b.v[3], acc, 0, 0, 0);
   }
 #else
-  // Opt-in build (-DMNIST_AMD_F32_SPLIT): fp32 operands as 3 bf16 parts (hi = x rounded to bf16, then each exact
-  // remainder rounded to bf16), the six products of weight >= 2^-16 of (hi + mid + lo)^2 on
-  // v_mfma_f32_16x16x16_bf16, whose lane layout (4 contiguous k per lane, K = 16) is this chunk's: ~2^-24 relative
-  // error (fp32-like; passes the fp32 tolerances) but 40 % SLOWER than the exact fp32 MFMAs, because the split is
-  // VALU work paid per fragment use (profiles/r4_session2/NOTES.md).  Pre-split LDS operand images would remove that
-  // cost but need 1.5x the fp32 images' LDS (conv_bwd fp32 already uses 150 KB of the 160 KB); not built.  (The
-  // 2-part / truncated 3-term forms failed the tolerances and were removed in round 5.)
-  typedef __attribute__((ext_vector_type(4))) short s16x4;
-  // (whole vectors are bit-cast: hipcc (ROCm 7.2) lowered __builtin_bit_cast of an ext-vector ELEMENT --
-  // x.y, x[j] -- to a read of element 0)
-  static DEV s16x4 part(const f32x4 x, f32x4& rem) {  // x rounded to bf16; rem = x - that (exact)
-    typedef __attribute__((ext_vector_type(4))) unsigned u4;
-    typedef __attribute__((ext_vector_type(4))) unsigned short us4;
-    bf16x4 h;
-    h.x = (bf16)x.x;
-    h.y = (bf16)x.y;
-    h.z = (bf16)x.z;
-    h.w = (bf16)x.w;
-    const u4 hw = __builtin_convertvector(__builtin_bit_cast(us4, h), u4) << 16;  // h as fp32 bits
-    rem = x - __builtin_bit_cast(f32x4, hw);
-    return __builtin_bit_cast(s16x4, h);
+  // Opt-in build (-DMNIST_AMD_F32_SPLIT): each fp32 operand EXACTLY as hi + mid + lo, three bf16 parts cut by
+  // truncation (hi = the top 8 significant bits, mid = the top 8 of the exact remainder, lo = the rest, which has
+  // at most 8 significant bits and so is a bf16 value), and the six products of weight >= 2^-16 of
+  // (hi + mid + lo)^2 -- ~2^-24 relative error, fp32-like -- on THREE v_mfma_f32_16x16x32_bf16 per K-chunk:
+  // the 32-slot MFMA sums all 8 k-slots of a lane, so a lane's slots carry two parts of its 4 k-elements
+  // ([ah | am] . [bh | bh], [ah | am] . [bm | bm], [ah | al] . [bl | bh]).  3 x 16 = 48 cycles per chunk against
+  // 4 x 32 = 128 for the exact v_mfma_f32_16x16x4_f32 (MI355X_MICROARCH.md cycle table); the split is VALU work
+  // (and / sub / perm, ~18 instructions per 4-element fragment) paid per fragment use, hoisted by the compiler
+  // for loop-invariant operands.  (Round 4's rounded 3-part split on six 16x16x16 MFMAs: 40 % slower than exact;
+  // profiles/r4_session2/NOTES.md.)
+  static DEV void split3(const f32x4 x, u32x2& h, u32x2& m, u32x2& l) {
+    const u32x4 xb = __builtin_bit_cast(u32x4, x);
+    const u32x4 hb = xb & 0xFFFF0000u;
+    const f32x4 r1 = x - __builtin_bit_cast(f32x4, hb);  // exact
+    const u32x4 r1b = __builtin_bit_cast(u32x4, r1);
+    const u32x4 mb = r1b & 0xFFFF0000u;
+    const f32x4 r2 = r1 - __builtin_bit_cast(f32x4, mb);  // exact, low 16 bits zero
+    const u32x4 lb = __builtin_bit_cast(u32x4, r2);
+    // pack the high halves of two dwords: element 2j in bits [15:0], 2j+1 in [31:16]
+    h = u32x2{__builtin_amdgcn_perm(xb[1], xb[0], 0x07060302u), __builtin_amdgcn_perm(xb[3], xb[2], 0x07060302u)};
+    m = u32x2{__builtin_amdgcn_perm(r1b[1], r1b[0], 0x07060302u), __builtin_amdgcn_perm(r1b[3], r1b[2], 0x07060302u)};
+    l = u32x2{__builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u), __builtin_amdgcn_perm(lb[3], lb[2], 0x07060302u)};
   }
-  static DEV f32x4 mf(const s16x4 a, const s16x4 b, f32x4 acc) {
-    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, acc, 0, 0, 0);
-  }
+  static DEV bf16x8 cat(const u32x2 p, const u32x2 q) { return __builtin_bit_cast(bf16x8, u32x4{p[0], p[1], q[0], q[1]}); }
   static DEV void mma(f32x4& acc, const Frag& a, const Frag& b) {
-    f32x4 ra, rb, ra2, rb2;
-    const s16x4 ah = part(a.v, ra), bh = part(b.v, rb);
-    const s16x4 am = part(ra, ra2), bm = part(rb, rb2);
-    const s16x4 al = part(ra2, ra), bl = part(rb2, rb);
-    acc = mf(al, bh, acc);
-    acc = mf(ah, bl, acc);
-    acc = mf(am, bm, acc);
-    acc = mf(am, bh, acc);
-    acc = mf(ah, bm, acc);
-    acc = mf(ah, bh, acc);
+    u32x2 ah, am, al, bh, bm, bl;
+    split3(a.v, ah, am, al);
+    split3(b.v, bh, bm, bl);
+    const bf16x8 ahm = cat(ah, am);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat(ah, al), cat(bl, bh), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahm, cat(bm, bm), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahm, cat(bh, bh), acc, 0, 0, 0);
   }
 #endif
   static DEV Frag load(const float* p) { Frag f; f.v = *reinterpret_cast<const f32x4*>(p); return f; }
