@@ -945,13 +945,21 @@ struct BwdRoles {
   // phase B: dgrad row pairs [q0, q0 + np) of 7 (np = 0: no dgrad on this wave); wgrad tiles [n0w, n0w + nw)
   static DEV int dg_np(int w) { return W8 ? (w < 3 ? 2 : (w == 3 ? 1 : 0)) : (w < 3 ? 2 : 1); }
   static DEV int dg_q0(int w) { return W8 ? (w < 4 ? 2 * w : 0) : 2 * w; }
+  // The wgrad tiles go {2, 2, 2, 4} against the dgrad row pairs {2, 2, 2, 1} (waves w and w + 4 of the 8-wave
+  // layout share SIMD w % 4): a dgrad tile is 3x a wgrad tile's MFMAs (fp32: 120 vs 40 v_mfma_f32_16x16x4_f32;
+  // bf16: 15 vs 5 16x16x32), so per SIMD 320 / 320 / 320 / 280 fp32 MFMAs (was {3, 3, 2, 2}: 360 / 360 / 320 / 200)
+  // and the longest per-wave bf16 chain (4 waves) is 40 MFMAs instead of 45.
+  static constexpr bool BAL = !W8 || sizeof(T) == 4;
+  static constexpr int NWT = BAL ? 4 : 3;  // wgrad accumulators per wave
   static DEV int wg_nw(int w) {
+    if (W8 && BAL) return w < 4 ? 0 : (w < 7 ? 2 : 4);
     if (W8) return w < 4 ? 0 : (w < 6 ? 3 : 2);
-    return w < 2 ? 2 : 3;
+    return w < 3 ? 2 : 4;
   }
   static DEV int wg_n0(int w) {
+    if (W8 && BAL) return w < 4 ? 0 : 2 * (w - 4);
     if (W8) return w < 4 ? 0 : (w < 6 ? 3 * (w - 4) : 6 + 2 * (w - 6));
-    return w < 2 ? 2 * w : 4 + 3 * (w - 2);
+    return 2 * w;
   }
 };
 
@@ -1111,7 +1119,7 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
   // ---- static work split of phase B (dgrad row-pair tile = 15 K-chunks, wgrad tile = 5): BwdRoles
   const int np = R::dg_np(w), q0 = R::dg_q0(w);  // dgrad row pairs [q0, q0 + np)
   const int nw = R::wg_nw(w), n0w = R::wg_n0(w);  // wgrad tiles [n0w, n0w + nw)
-  constexpr int NWT = 3;  // wgrad accumulators per wave
+  constexpr int NWT = R::NWT;  // wgrad accumulators per wave
   // ---- per-lane operand offsets (loop invariant)
   // conv2 wgrad B: DENSE columns kcol = tap*6 + c (150 weights) + 1 bias column = 10 tiles of 16
   // (was tap*8 + c: 13 tiles, a quarter of them zero channels 6, 7)
