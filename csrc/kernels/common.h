@@ -52,7 +52,9 @@ template <> struct Mma<float> {
   // 4 x 32 = 128 for the exact v_mfma_f32_16x16x4_f32 (MI355X_MICROARCH.md cycle table); the split is VALU work
   // (and / sub / perm, ~18 instructions per 4-element fragment) paid per fragment use, hoisted by the compiler
   // for loop-invariant operands.  (Round 4's rounded 3-part split on six 16x16x16 MFMAs: 40 % slower than exact;
-  // profiles/r4_session2/NOTES.md.)
+  // profiles/r4_session2/NOTES.md.)  Measured (profiles/r5_session1/f32split): passes every fp32 tolerance test;
+  // conv_fwd -7 %, but conv_bwd +13 % (its streamed operands are re-split every chunk: the VALU cost equals the
+  // MFMA saving) -> LeNet fp32 4-14 % slower, MLP fp32 B=8192 9 % faster.  Not the default.
   static DEV void split3(const f32x4 x, u32x2& h, u32x2& m, u32x2& l) {
     const u32x4 xb = __builtin_bit_cast(u32x4, x);
     const u32x4 hb = xb & 0xFFFF0000u;
