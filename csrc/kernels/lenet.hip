@@ -943,6 +943,10 @@ struct BwdRoles {
   static DEV bool loads_p1(int w) { return !W8 || (w >= 4 && w < 6); }
   static DEV bool loads_p2(int w) { return !W8 || (sizeof(T) == 2 ? w >= 4 : w >= 1); }
   // phase B: dgrad row pairs [q0, q0 + np) of 7 (np = 0: no dgrad on this wave); wgrad tiles [n0w, n0w + nw)
+  // (Measured: putting the dgrad on waves 0-1 {4, 3} and the wgrad on waves 2-3 {5, 5}, or the wgrad on one wave --
+  // fewer waves reading each shared fragment -- made phase B 14 / 32 % slower: the per-wave chains, not the LDS
+  // bandwidth, bound it; profiles/r5_session1/roles/)
+  static constexpr int NPMAX = 2;  // most dgrad row pairs on a wave
   static DEV int dg_np(int w) { return W8 ? (w < 3 ? 2 : (w == 3 ? 1 : 0)) : (w < 3 ? 2 : 1); }
   static DEV int dg_q0(int w) { return W8 ? (w < 4 ? 2 * w : 0) : 2 * w; }
   // The wgrad tiles go {2, 2, 2, 4} against the dgrad row pairs {2, 2, 2, 1} (waves w and w + 4 of the 8-wave
@@ -1381,51 +1385,51 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
       };
       const int x = min(row, 13);
       const T* bq = w2 + row * S::W2P + grp * KV;
-      if (!ABLATED(cb.ablate, 128)) {
-        if (np == 2) {
-          const int y0 = 2 * q0, y1 = y0 + 2;
-          const T* a0 = dys + ((y0 + 4) * 18 + x + 4) * 16;
-          const T* a1 = dys + ((y1 + 4) * 18 + x + 4) * 16;
-          f32x4 acc0 = zero4(), acc1 = zero4();
-          // Row y1 = y0 + 2 sees the SAME dY2 window two kernel rows (kh' + 2 = SH chunks) later:
-          // A(y1, kc) = A(y0, kc - SH).  Tile y0's fragments stay in registers for SH chunks, so tile
-          // y1 loads only its first SH chunks (20 instead of 30 A reads per pair for bf16).
-          constexpr int SH = 160 / KC;  // chunks per two kernel rows (10 taps x 16 channels)
-          static_assert(SH < D2CH, "row-pair A reuse needs more than two kernel rows of K");
-          Frag A0[D2CH], A1[D2CH], FB[D2CH];
-          auto issue = [&](int kc) {
-            FB[kc] = M::load(bq + kc * KC);
-            A0[kc] = M::load(a0 + doff(kc));
-            A1[kc] = kc < SH ? M::load(a1 + doff(kc)) : A0[kc - SH];
-          };
+      // The wave's NP row-pair tiles q0 .. q0 + NP - 1 (rows y0 + 2j) share every B fragment, and tile j sees tile
+      // j - 1's dY2 window two kernel rows (SH chunks) later: A_j(kc) = A_{j-1}(kc - SH).  So only tile 0 reads
+      // all D2CH = 3 SH chunks of A; tiles j >= 1 read their first SH.  The chunks are visited diagonally --
+      // c, c + SH, c + 2 SH for c = 0 .. SH - 1 -- so the fragments one c needs (3 of tile 0, 1 per other tile, 3
+      // B) are all the registers held: A_j(c + m SH) = L_{j-m}(c) for j >= m, else L_0(c + (m - j) SH).
+      auto dgrad_tiles = [&](auto npc) {
+        constexpr int NP = decltype(npc)::value;
+        constexpr int SH = 160 / KC;  // chunks per two kernel rows (10 taps x 16 channels)
+        static_assert(D2CH == 3 * SH, "conv2 dgrad K = 3 x two kernel rows");
+        const int y0 = 2 * q0;
+        const T* a0 = dys + ((y0 + 4) * 18 + x + 4) * 16;
+        f32x4 acc[NP];
 #pragma unroll
-          for (int kc = 0; kc < BWD_PD; ++kc) issue(kc);
+        for (int j = 0; j < NP; ++j) acc[j] = zero4();
+        struct Set { Frag l0[3], lt[NP > 1 ? NP - 1 : 1], fb[3]; };
+        auto ld = [&](int c) {
+          Set r;
 #pragma unroll
-          for (int kc = 0; kc < D2CH; ++kc) {  // chunk kc + PD's fragments in flight during this one's MFMAs
-            if (kc + BWD_PD < D2CH) issue(kc + BWD_PD);
-            M::mma(acc0, A0[kc], FB[kc]);
-            M::mma(acc1, A1[kc], FB[kc]);
+          for (int m = 0; m < 3; ++m) {
+            r.fb[m] = M::load(bq + (c + m * SH) * KC);
+            r.l0[m] = M::load(a0 + doff(c + m * SH));
           }
-          dgrad_tile_epi(y0, acc0);
-          dgrad_tile_epi(y1, acc1);
-        } else {
-          const int y0 = 2 * q0;
-          const T* a0 = dys + ((y0 + 4) * 18 + x + 4) * 16;
-          f32x4 acc0 = zero4();
-          Frag A0[D2CH], FB[D2CH];
-          auto issue = [&](int kc) {
-            FB[kc] = M::load(bq + kc * KC);
-            A0[kc] = M::load(a0 + doff(kc));
-          };
 #pragma unroll
-          for (int kc = 0; kc < BWD_PD; ++kc) issue(kc);
+          for (int j = 1; j < NP; ++j) r.lt[j - 1] = M::load(a0 + 2 * j * 18 * 16 + doff(c));
+          return r;
+        };
+        Set cur = ld(0);
 #pragma unroll
-          for (int kc = 0; kc < D2CH; ++kc) {
-            if (kc + BWD_PD < D2CH) issue(kc + BWD_PD);
-            M::mma(acc0, A0[kc], FB[kc]);
-          }
-          dgrad_tile_epi(y0, acc0);
+        for (int c = 0; c < SH; ++c) {
+          Set nxt = cur;
+          if (c + 1 < SH) nxt = ld(c + 1);
+#pragma unroll
+          for (int m = 0; m < 3; ++m)
+#pragma unroll
+            for (int j = 0; j < NP; ++j)
+              M::mma(acc[j], j >= m ? (j == m ? cur.l0[0] : cur.lt[j - m - 1]) : cur.l0[m - j], cur.fb[m]);
+          cur = nxt;
         }
+#pragma unroll
+        for (int j = 0; j < NP; ++j) dgrad_tile_epi(y0 + 2 * j, acc[j]);
+      };
+      if (!ABLATED(cb.ablate, 128)) {
+        static_assert(R::NPMAX == 2, "dgrad row pairs per wave: 1 or 2");
+        if (np == 1) dgrad_tiles(std::integral_constant<int, 1>{});
+        else if (np == 2) dgrad_tiles(std::integral_constant<int, 2>{});
       }
     }
     __syncthreads();
