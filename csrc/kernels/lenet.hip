@@ -875,7 +875,7 @@ __global__ __launch_bounds__(512) void head16_kernel(BatchRef br, HeadBuffers hb
 // backward
 // LDS images chosen so that every MFMA operand fragment is ONE aligned 16-byte read:
 //   XS  [5][32][32]     xs[kw][y][x]  = xpad[y][x+kw]          conv1 wgrad B (im2col^T rows), + a ones plane
-//   P1T [5][6][14][16]  p1t[kw][c][y][x] = pool1[y][x+kw][c]   conv2 wgrad B
+//   P1T [5][6][14][PW]  p1t[kw][c][y][x] = pool1[y][x+kw][c]   conv2 wgrad B (rows PW = 16 (bf16) / 12 (fp32) wide)
 //   DY2T[16][10*16]     (fp32 only) conv2 pre-act grad, channel-major, rows padded 10->16   conv2 wgrad A
 //   DYS [18][18][16]    same grad, position-major (NHWC), zero border of 4 so the full-correlation
 //                       dgrad reads it without bounds checks                     conv2 dgrad A
@@ -897,6 +897,11 @@ struct BwdSmem {
   // XP / D1P / ONES and the phase-C lane maps below: conflict-free A reads and 1.5-way B reads in the
   // conv1 wgrad (scripts/lds_model.py C2 model; 616 -> 290 LDS cycles per image for that phase)
   static constexpr int W2P = 496, XP = 1048, P1P = 240, D2P = 168, D1P = 944;
+  // conv2 wgrad K: position p = y * PW + x of the 10 x 10 output (x >= 10 padding).  fp32: PW = 12, 120 positions =
+  // 8 chunks instead of 10 (its phase B is MFMA-bound: LeNet fp32 B=8192 0.4139 -> 0.4015 ms), every kernel-row
+  // shift (kh * PW elements) still 16-byte aligned.  bf16 keeps 16 (5 chunks): at 12 -- 4 chunks, 8-byte B reads,
+  // per-lane transposed-read addresses -- B=8192 went 0.1011 -> 0.1086 ms (profiles/r5_session1/pw12/)
+  static constexpr int PW = sizeof(T) == 4 ? 12 : 16;
   static constexpr int D1PRE = 32;  // zero elements before channel 0 of DY1T (row y - 1 of the first row)
   // XS: 5 shifted planes, then an all-ones plane at ONES (bias-gradient column; its position sets the
   // bank of that column); P1T has 32 planes (30 + zero + ones): padding / bias-gradient columns read a
@@ -919,6 +924,7 @@ struct BwdSmem {
   static constexpr int OFF_RED = OFF_XS;  // [NW][256] f32 scratch after the image loop
   static_assert(8 * 256 * 4 <= XS_N * (int)sizeof(T), "reduction scratch must fit in the aliased XS region");
   static_assert(D1P >= 928 && 4 * XP + 4 * 32 + 928 <= ONES, "phase C reads stay inside zeroed rows");
+  static_assert(14 * PW <= P1P && 4 * PW + 128 <= P1P && 128 <= D2P, "conv2 wgrad reads stay inside their (zeroed) planes");
 };
 
 // Per-image thread roles and the phase-B work split of conv_bwd_kernel, by workgroup size (NW waves).
@@ -1083,7 +1089,7 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
   };
   Pre nxt = fetch(0);  // issued before the setup below, so its latency overlaps it
 
-  constexpr int W2CH = 160 / KC;              // conv2 wgrad: 10 rows x 16 positions
+  constexpr int W2CH = (10 * S::PW + KC - 1) / KC;  // conv2 wgrad: 10 rows x PW positions
   constexpr int D2CH = 480 / KC;              // conv2 dgrad K = 30 taps (kh' = -1..4) x 16 ch (15 bf16 / 30 f32)
   // (measured: a register-resident dgrad B operand pushed the kernel to 245 VGPRs and made hipcc
   //  shuttle accumulators VGPR<->AGPR around every MFMA -- the B operand is read from LDS)
@@ -1131,7 +1137,7 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
 #pragma unroll
   for (int i = 0; i < NWT; ++i) {
     const int kcol = (n0w + i) * 16 + row, tap = kcol / 6, c = kcol - 6 * tap;
-    w2off[i] = kcol < 150 ? ((tap % 5) * 6 + c) * S::P1P + (tap / 5) * 16 : (kcol == 150 ? 31 : 30) * S::P1P;
+    w2off[i] = kcol < 150 ? ((tap % 5) * 6 + c) * S::P1P + (tap / 5) * S::PW : (kcol == 150 ? 31 : 30) * S::P1P;
     if (i >= nw) w2off[i] = 30 * S::P1P;  // no such tile on this wave: zero plane
   }
   // conv1 wgrad (phase C) as ONE 16x16 tile per image: M row m = (r, n) reads channel n of DY1T shifted
@@ -1212,13 +1218,13 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
     if (tid >= R::M1_T0 && tid < R::M1_T0 + R::M1_N && !ABLATED(cb.ablate, 8))
       reinterpret_cast<uint4*>(m1s)[tid - R::M1_T0] = valid ? cur.q(O_M1) : make_uint4(0, 0, 0, 0);
     if (tid >= R::P1_T0 && tid < R::P1_T0 + R::P1_N && !ABLATED(cb.ablate, 8)) {
-      // P1T: row y of planes (kw, c), kw = 0..4: p1t[kw*6+c][y][x] = pool1[y][x + kw][c], 0 for x + kw >= 14
+      // P1T: row y of planes (kw, c), kw = 0..4: p1t[kw*6+c][y][x] = pool1[y][x + kw][c] (x < PW), 0 for x + kw >= 14
       const int i = tid - R::P1_T0, c = i / 14, y = i - 14 * c;
       T pv[16];
 #pragma unroll
       for (int k = 0; k < PV; ++k)
         *reinterpret_cast<uint4*>(pv + k * (16 / (int)sizeof(T))) = valid ? cur.q(O_P1 + 4 * k) : make_uint4(0, 0, 0, 0);
-      T* dst = p1t + c * S::P1P + y * 16;
+      T* dst = p1t + c * S::P1P + y * S::PW;
       if constexpr (sizeof(T) == 2) {
         uint32_t D[10];
 #pragma unroll
@@ -1230,6 +1236,7 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
           uint32_t o[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) o[j] = (kw & 1) ? __builtin_amdgcn_alignbyte(D[m + j + 1], D[m + j], 2) : D[m + j];
+          static_assert(S::PW == 16, "bf16 P1T rows: 16 wide");
           T* d = dst + kw * 6 * S::P1P;
           *reinterpret_cast<uint4*>(d) = make_uint4(o[0], o[1], o[2], o[3]);
           *reinterpret_cast<uint4*>(d + 8) = make_uint4(o[4], o[5], o[6], o[7]);
@@ -1239,7 +1246,7 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
         for (int kw = 0; kw < 5; ++kw) {
           float* d = reinterpret_cast<float*>(dst + kw * 6 * S::P1P);
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
+          for (int q = 0; q < S::PW / 4; ++q) {
             f32x4 o;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -1289,7 +1296,7 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
           const int oh = 2 * py + (win >> 1), ow = 2 * px + (win & 1);
           const T v = to_t<T>(((code & 4) && (code & 3) == win) ? g : 0.f);
           dys[((oh + 4) * 18 + ow + 4) * 16 + n] = v;
-          dy2t[n * S::D2P + oh * 16 + ow] = v;
+          dy2t[n * S::D2P + oh * S::PW + ow] = v;
         }
       }
     }
@@ -1308,6 +1315,7 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
           // positions p0 .. p0 + 7 (row y = p0 / 16, columns x0 .. x0 + 7; x >= 10 reads DYS's zero padding) of
           // channel `row`: two 4-position x 16-channel blocks, transposed by the read.  Lane 4q + p of each
           // 16-lane group addresses position x0 + q (+ 4), channels 4p .. 4p + 3; lane i receives channel i.
+          static_assert(S::PW == 16, "bf16 conv2 wgrad positions: 16 per row");
           typedef short v4s __attribute__((ext_vector_type(4)));
           const int p0 = kc * KC + grp * KV, y = p0 >> 4, x0 = p0 & 15;
           const T* a = dys + ((y + 4) * 18 + x0 + ((lane & 15) >> 2) + 4) * 16 + 4 * (lane & 3);
@@ -1323,8 +1331,7 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
         }
       };
       auto ld_b = [&](int kc, int i) {
-        const int p0 = kc * KC + grp * KV;
-        return M::load(p1t + w2off[i] + (p0 >> 4) * 16 + (p0 & 15));
+        return M::load(p1t + w2off[i] + kc * KC + grp * KV);  // positions p = y * PW + x (16-byte aligned)
       };
       // NT real tiles on this wave: no zero-plane filler tile
       // fragments of chunk kc + PD are issued before chunk kc's MFMAs (constant indices: registers)
