@@ -35,6 +35,41 @@ template <> struct Mma<float> {
   static constexpr int KV = 4;    // contiguous k per lane per chunk
   static constexpr int KC = 16;   // k per chunk
   struct Frag { f32x4 v; };
+  // EXACT cut of an fp32 fragment into three bf16 parts by truncation: hi = the top 8 significant bits, mid = the top 8
+  // of the exact remainder, lo = the rest (at most 8 significant bits, so a bf16 value): x == hi + mid + lo.  Packed
+  // as u32x2 (4 bf16, element 2j in bits [15:0]).
+  static DEV void split3(const f32x4 x, u32x2& h, u32x2& m, u32x2& l) {
+    const u32x4 xb = __builtin_bit_cast(u32x4, x);
+    const u32x4 hb = xb & 0xFFFF0000u;
+    const f32x4 r1 = x - __builtin_bit_cast(f32x4, hb);  // exact
+    const u32x4 r1b = __builtin_bit_cast(u32x4, r1);
+    const u32x4 mb = r1b & 0xFFFF0000u;
+    const f32x4 r2 = r1 - __builtin_bit_cast(f32x4, mb);  // exact, low 16 bits zero
+    const u32x4 lb = __builtin_bit_cast(u32x4, r2);
+    h = u32x2{__builtin_amdgcn_perm(xb[1], xb[0], 0x07060302u), __builtin_amdgcn_perm(xb[3], xb[2], 0x07060302u)};
+    m = u32x2{__builtin_amdgcn_perm(r1b[1], r1b[0], 0x07060302u), __builtin_amdgcn_perm(r1b[3], r1b[2], 0x07060302u)};
+    l = u32x2{__builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u), __builtin_amdgcn_perm(lb[3], lb[2], 0x07060302u)};
+  }
+  static DEV bf16x8 cat(const u32x2 p, const u32x2 q) { return __builtin_bit_cast(bf16x8, u32x4{p[0], p[1], q[0], q[1]}); }
+  // a (cut here) times b given as its three bf16 parts: the six products of weight >= 2^-16 of (hi + mid + lo)^2
+  // on THREE v_mfma_f32_16x16x32_bf16 -- the 32-slot MFMA sums all 8 k-slots of a lane, so a lane's slots carry two
+  // parts of its 4 k-elements: [ah | al] . [bl | bh], [ah | am] . [bm | bm], [ah | am] . [bh | bh] (smallest first).
+  // ~2^-24 relative error, 3 x 16 = 48 cycles per 16-k chunk against 4 x 32 = 128 for v_mfma_f32_16x16x4_f32
+  // (MI355X_MICROARCH.md cycle table; scripts/diag/mfma_rate.hip).
+  static DEV void mma_psb(f32x4& acc, const Frag& a, const u32x2 bh, const u32x2 bm, const u32x2 bl) {
+    u32x2 ah, am, al;
+    split3(a.v, ah, am, al);
+    const bf16x8 ahm = cat(ah, am);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat(ah, al), cat(bl, bh), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahm, cat(bm, bm), acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahm, cat(bh, bh), acc, 0, 0, 0);
+  }
+  // both operands cut here (the compiler hoists the cut of a loop-invariant b)
+  static DEV void mma_s(f32x4& acc, const Frag& a, const Frag& b) {
+    u32x2 bh, bm, bl;
+    split3(b.v, bh, bm, bl);
+    mma_psb(acc, a, bh, bm, bl);
+  }
 #ifndef MNIST_AMD_F32_SPLIT
   static DEV void mma(f32x4& acc, const Frag& a, const Frag& b) {
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[0], b.v[0], acc, 0, 0, 0);
@@ -55,29 +90,7 @@ template <> struct Mma<float> {
   // profiles/r4_session2/NOTES.md.)  Measured (profiles/r5_session1/f32split): passes every fp32 tolerance test;
   // conv_fwd -7 %, but conv_bwd +13 % (its streamed operands are re-split every chunk: the VALU cost equals the
   // MFMA saving) -> LeNet fp32 4-14 % slower, MLP fp32 B=8192 9 % faster.  Not the default.
-  static DEV void split3(const f32x4 x, u32x2& h, u32x2& m, u32x2& l) {
-    const u32x4 xb = __builtin_bit_cast(u32x4, x);
-    const u32x4 hb = xb & 0xFFFF0000u;
-    const f32x4 r1 = x - __builtin_bit_cast(f32x4, hb);  // exact
-    const u32x4 r1b = __builtin_bit_cast(u32x4, r1);
-    const u32x4 mb = r1b & 0xFFFF0000u;
-    const f32x4 r2 = r1 - __builtin_bit_cast(f32x4, mb);  // exact, low 16 bits zero
-    const u32x4 lb = __builtin_bit_cast(u32x4, r2);
-    // pack the high halves of two dwords: element 2j in bits [15:0], 2j+1 in [31:16]
-    h = u32x2{__builtin_amdgcn_perm(xb[1], xb[0], 0x07060302u), __builtin_amdgcn_perm(xb[3], xb[2], 0x07060302u)};
-    m = u32x2{__builtin_amdgcn_perm(r1b[1], r1b[0], 0x07060302u), __builtin_amdgcn_perm(r1b[3], r1b[2], 0x07060302u)};
-    l = u32x2{__builtin_amdgcn_perm(lb[1], lb[0], 0x07060302u), __builtin_amdgcn_perm(lb[3], lb[2], 0x07060302u)};
-  }
-  static DEV bf16x8 cat(const u32x2 p, const u32x2 q) { return __builtin_bit_cast(bf16x8, u32x4{p[0], p[1], q[0], q[1]}); }
-  static DEV void mma(f32x4& acc, const Frag& a, const Frag& b) {
-    u32x2 ah, am, al, bh, bm, bl;
-    split3(a.v, ah, am, al);
-    split3(b.v, bh, bm, bl);
-    const bf16x8 ahm = cat(ah, am);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat(ah, al), cat(bl, bh), acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahm, cat(bm, bm), acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahm, cat(bh, bh), acc, 0, 0, 0);
-  }
+  static DEV void mma(f32x4& acc, const Frag& a, const Frag& b) { mma_s(acc, a, b); }
 #endif
   static DEV Frag load(const float* p) { Frag f; f.v = *reinterpret_cast<const f32x4*>(p); return f; }
   static DEV Frag zero() { Frag f; f.v = f32x4{0.f, 0.f, 0.f, 0.f}; return f; }
