@@ -177,8 +177,13 @@ DEV uint32_t hash4(uint32_t seed, uint32_t s, uint32_t a, uint32_t b) {
   return h;
 }
 
-// MNIST normalisation of ToTensor()+Normalize((0.1307,),(0.3081,)) (ddp_tutorial_cpu.py:13-16).
-DEV float mnist_norm(uint32_t u8) { return (float(u8) * (1.0f / 255.0f) - 0.1307f) * (1.0f / 0.3081f); }
+// MNIST normalisation of ToTensor()+Normalize((0.1307,),(0.3081,)) (ddp_tutorial_cpu.py:13-16), folded into ONE fma
+// (x / 255 - 0.1307) / 0.3081 = x * A + B (A, B rounded once from double): v_cvt_f32_ubyte + v_fma per pixel instead of
+// cvt + mul + sub + mul -- the per-pixel staging is on the VALU-issue-bound image loops of conv_fwd / conv_bwd / the MLP
+// head (within 1 ulp of the three-step form; the reference's own ToTensor + Normalize is not bit-reproduced either way)
+constexpr float MNIST_NORM_A = (float)(1.0 / (255.0 * 0.3081));
+constexpr float MNIST_NORM_B = (float)(-0.1307 / 0.3081);
+DEV float mnist_norm(uint32_t u8) { return __builtin_fmaf(float(u8), MNIST_NORM_A, MNIST_NORM_B); }
 
 DEV int round_up(int x, int m) { return (x + m - 1) / m * m; }
 

@@ -9,7 +9,7 @@ mkdir -p "$OUT"
 cd "$ROOT" || exit 1
 AB=$(ls pytorch_ddp_mnist_amd/_C_ab*.so | head -1)
 echo "tests" &&
-timeout -k 10 900 python -u -m pytest tests/test_native_gpu.py tests/test_schedules_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest.txt" 2>&1 || exit 1
+timeout -k 10 900 python -u -m pytest tests/test_native_gpu.py tests/test_schedules_gpu.py tests/test_loaders.py -m gpu -x -q --timeout 300 --timeout-method thread > "$OUT/pytest.txt" 2>&1 || exit 1
 echo "A/B"
 IFS=';' read -ra CS <<< "$CONFIGS"
 for r in 1 2; do
