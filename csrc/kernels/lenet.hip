@@ -322,6 +322,9 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
     }
   };
 
+  // bf16 staging: the lane's window (image columns 8 sg - 2 + i, i < 12) leaves the image only as whole pixel pairs --
+  // pair 0 when sg = 0 (columns -2, -1), pairs 3..5 when sg = 3 (columns 28..33): two loop-invariant masks
+  const uint32_t keep_sg0 = sg == 0 ? 0u : 0xFFFFFFFFu, keep_sg3 = sg == 3 ? 0u : 0xFFFFFFFFu;
   zero_lds<T>(xs, S::NPL * S::XP + S::XTAIL, tid, NT);
   if (TRAIN) {
     zero_lds<T>(p1c, P1IMG, tid, NT);
@@ -346,25 +349,20 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
     }
     // ---- stage: normalise once, 4 aligned 16-byte plane stores per thread
     if (tid < 224 && !ABLATED(cb.ablate, 1)) {
-      float f[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const uint32_t byte = (u.d[(i + 2) >> 2] >> (8 * ((i + 2) & 3))) & 255u;
-        const bool in = valid && (unsigned)(8 * sg - 2 + i) < 28u;  // zero padding is 0 AFTER normalising
-        f[i] = in ? mnist_norm(byte) : 0.f;
-      }
+      auto pixel = [&](int i) { return mnist_norm((u.d[(i + 2) >> 2] >> (8 * ((i + 2) & 3))) & 255u); };
       T* dst = xs + sy * 32 + 8 * sg;
       if constexpr (sizeof(T) == 2) {
-        // packed pairs D[k] = (v[2k], v[2k+1]); E = window for this thread's plane half (sh);
-        // even planes are dword-aligned slices of E, odd planes one alignbyte per dword
-        uint32_t D[8], E[6];
+        // packed pairs D[k] = (v[2k], v[2k+1]), each ONE v_cvt_pk_bf16_f32, the zero padding (0 AFTER normalising)
+        // applied to the pair by the lane's loop-invariant mask and the image's `valid`; E = window for this
+        // thread's plane half (sh); even planes are dword-aligned slices of E, odd planes one alignbyte per dword
+        typedef __attribute__((ext_vector_type(2))) float f32x2;
+        const uint32_t vm = valid ? 0xFFFFFFFFu : 0u;
+        const uint32_t m0 = keep_sg0 & vm, m3 = keep_sg3 & vm;
+        uint32_t D[6], E[6];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          bf16x2 p2v;
-          p2v[0] = (bf16)f[2 * k];
-          p2v[1] = (bf16)f[2 * k + 1];
-          D[k] = __builtin_bit_cast(uint32_t, p2v);
-        }
+        for (int k = 0; k < 6; ++k)
+          D[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2{pixel(2 * k), pixel(2 * k + 1)}), bf16x2)) &
+                 (k == 0 ? m0 : (k >= 3 ? m3 : vm));
         const uint32_t msk = 0u - (uint32_t)sh;  // bit blend: a ?: select here becomes scratch-indexed D
         // 4 planes: this thread writes planes 2 sh, 2 sh + 1 (window E = D shifted by sh dwords = 2 sh taps)
 #pragma unroll
@@ -378,6 +376,12 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
           *reinterpret_cast<uint4*>(dst + (2 * sh + q) * S::XP) = o;
         }
       } else {
+        float f[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const bool in = valid && (unsigned)(8 * sg - 2 + i) < 28u;  // zero padding is 0 AFTER normalising
+          f[i] = in ? pixel(i) : 0.f;
+        }
         // bit blend instead of `sh ? f[i + 1] : f[i]`: hipcc turned that select into a lane-indexed
         // load of f[] from scratch memory (80 B/lane of scratch traffic per image); plane sh
         const uint32_t msk = 0u - (uint32_t)sh;
