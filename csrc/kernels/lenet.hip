@@ -255,7 +255,9 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
     for (int i = 1; i < 4; ++i)
       if (acc[i] > mx) { mx = acc[i]; am = i; }
     const float pre = mx + bias1;
-    const T v = to_t<T>(n1 < 6 ? fmaxf(pre, 0.f) : 0.f);
+    // (padding channels n1 = 6, 7: zero weights and zero bias give pre = 0 exactly, so ReLU stores the 0 the
+    //  conv2 im2col rows need without a select)
+    const T v = to_t<T>(fmaxf(pre, 0.f));
     e1_p1s[t * 2 * 14 * 8] = v;
     if (TRAIN) {
       e1_p1c[t * 2 * 16] = v;
@@ -1190,23 +1192,20 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
       // XS: planes kw = 0..4 of row y, columns [8g, 8g+8): xs[kw][y][x] = xpad[y][x + kw] = w[kw + 2 + j]
       // with w[i] = normalised pixel at image column 8g - 4 + i (0 outside the image)
       const int xt = tid - R::XS_T0, y = 2 + (xt >> 2), g = xt & 3;
-      float wv[16];
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const uint32_t byte = (cur.r[O_PX + (i >> 2)] >> (8 * (i & 3))) & 255u;
-        const bool in = valid && (unsigned)(8 * g - 4 + i) < 28u;  // also masks the clamped (duplicate) words
-        wv[i] = in ? mnist_norm(byte) : 0.f;
-      }
+      auto pixel = [&](int i) { return mnist_norm((cur.r[O_PX + (i >> 2)] >> (8 * (i & 3))) & 255u); };
       T* dst = xs + y * 32 + 8 * g;
       if constexpr (sizeof(T) == 2) {
+        // pixel pairs by one v_cvt_pk_bf16_f32 each; the window leaves the image only as whole pairs -- pairs 0, 1
+        // when g = 0 (columns -4..-1), pairs 4..7 when g = 3 (columns 28..35, also the clamped duplicate words)
+        typedef __attribute__((ext_vector_type(2))) float f32x2;
+        const uint32_t vm = valid ? 0xFFFFFFFFu : 0u;
+        const uint32_t m0 = g == 0 ? 0u : vm, m3 = g == 3 ? 0u : vm;
         uint32_t D[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          bf16x2 pr;
-          pr[0] = (bf16)wv[2 * k];
-          pr[1] = (bf16)wv[2 * k + 1];
-          D[k] = __builtin_bit_cast(uint32_t, pr);
-        }
+        for (int k = 1; k < 8; ++k)  // (D[0] is not read)
+          D[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2{pixel(2 * k), pixel(2 * k + 1)}), bf16x2)) &
+                 (k < 2 ? m0 : (k >= 4 ? m3 : vm));
+        D[0] = 0u;
 #pragma unroll
         for (int kw = 0; kw < 5; ++kw) {
           const int m = (kw + 2) >> 1;
@@ -1218,6 +1217,12 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
           *reinterpret_cast<uint4*>(dst + kw * S::XP) = o;
         }
       } else {
+        float wv[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const bool in = valid && (unsigned)(8 * g - 4 + i) < 28u;  // also masks the clamped (duplicate) words
+          wv[i] = in ? pixel(i) : 0.f;
+        }
 #pragma unroll
         for (int kw = 0; kw < 5; ++kw) {
           float* d = reinterpret_cast<float*>(dst + kw * S::XP);
@@ -1274,24 +1279,15 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
       if (tid >= R::DS_T0 && tid < R::DS_T0 + R::DS_N && !ABLATED(cb.ablate, 32)) {
         const int j = tid - R::DS_T0;
         const int n0 = 2 * (j & 7), p = j >> 3, py = p / 5, px = p % 5;
-        float v[2][4];  // [channel][window]
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-          const uint32_t code = valid ? cur.code(r) : 0u;  // code 0: ReLU blocked, every window gets 0
-          const float g = to_f(cur.grad(r));
-#pragma unroll
-          for (int win = 0; win < 4; ++win) v[r][win] = ((code & 4) && (code & 3) == win) ? g : 0.f;
-        }
-        auto pack2 = [](float a, float b) {
-          bf16x2 q;
-          q[0] = (bf16)a;
-          q[1] = (bf16)b;
-          return __builtin_bit_cast(uint32_t, q);
-        };
+        // the gradient's raw bf16 bits go to the window its pool2 code names (code & 7 == 4 + window: ReLU passed,
+        // argmax = window), 0 elsewhere -- selects on 16-bit values, no float round trip
+        const uint32_t c0 = valid ? (cur.code(0) & 7u) : 0u, c1 = valid ? (cur.code(1) & 7u) : 0u;  // 0: all windows 0
+        const uint32_t g0 = cur.r[O_DS + 2] & 0xFFFFu, g1 = cur.r[O_DS + 3] << 16;
 #pragma unroll
         for (int win = 0; win < 4; ++win) {
           const int oh = 2 * py + (win >> 1), ow = 2 * px + (win & 1);
-          *reinterpret_cast<uint32_t*>(dys + ((oh + 4) * 18 + ow + 4) * 16 + n0) = pack2(v[0][win], v[1][win]);
+          *reinterpret_cast<uint32_t*>(dys + ((oh + 4) * 18 + ow + 4) * 16 + n0) =
+              (c0 == 4u + win ? g0 : 0u) | (c1 == 4u + win ? g1 : 0u);
         }
       }
     } else {
