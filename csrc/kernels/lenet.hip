@@ -1373,6 +1373,26 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
         const int c = row & 7, Y = y + (row >> 3);
         if (c < 6) {
           const uint32_t codes = *reinterpret_cast<const uint32_t*>(m1s + c * M1CP + Y * 16 + grp * 4);
+          T* d = dy1t + c * S::D1P + (2 * Y) * 32 + grp * 8;
+          if constexpr (sizeof(T) == 2) {
+            // the gradient's bf16 bits routed by the pool1 code (bit 2: ReLU passed, bits 0-1: window) into the 16-bit
+            // halves of the two output rows' dwords -- bit-field extracts and selects, one conversion per value.
+            // Pooled columns x >= 14 have code 0 (conv_fwd never writes their padding bytes), so no range check.
+            typedef __attribute__((ext_vector_type(2))) float f32x2;
+            uint32_t w0[4], w1[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const uint32_t vb = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2{acc[i], 0.f}), bf16x2));
+              const uint32_t keep = (uint32_t)(((int32_t)(codes << (29 - 8 * i))) >> 31);  // bit 8i + 2 -> 0 / ~0
+              const uint32_t val = (vb & keep) << (((codes >> (8 * i)) & 1u) << 4);
+              const bool row1 = (codes >> (8 * i + 1)) & 1u;
+              w0[i] = row1 ? 0u : val;
+              w1[i] = row1 ? val : 0u;
+            }
+            *reinterpret_cast<uint4*>(d) = make_uint4(w0[0], w0[1], w0[2], w0[3]);
+            *reinterpret_cast<uint4*>(d + 32) = make_uint4(w1[0], w1[1], w1[2], w1[3]);
+            return;
+          }
           T r0[8], r1[8];
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -1385,16 +1405,10 @@ DEV void conv_bwd_block(const BatchRef br, const LenetConvBuffers cb, const int 
             r1[2 * i] = to_t<T>(am == 2 ? v : 0.f);
             r1[2 * i + 1] = to_t<T>(am == 3 ? v : 0.f);
           }
-          T* d = dy1t + c * S::D1P + (2 * Y) * 32 + grp * 8;
-          if constexpr (sizeof(T) == 2) {
-            *reinterpret_cast<uint4*>(d) = *reinterpret_cast<const uint4*>(r0);
-            *reinterpret_cast<uint4*>(d + 32) = *reinterpret_cast<const uint4*>(r1);
-          } else {
-            reinterpret_cast<uint4*>(d)[0] = reinterpret_cast<const uint4*>(r0)[0];
-            reinterpret_cast<uint4*>(d)[1] = reinterpret_cast<const uint4*>(r0)[1];
-            reinterpret_cast<uint4*>(d + 32)[0] = reinterpret_cast<const uint4*>(r1)[0];
-            reinterpret_cast<uint4*>(d + 32)[1] = reinterpret_cast<const uint4*>(r1)[1];
-          }
+          reinterpret_cast<uint4*>(d)[0] = reinterpret_cast<const uint4*>(r0)[0];
+          reinterpret_cast<uint4*>(d)[1] = reinterpret_cast<const uint4*>(r0)[1];
+          reinterpret_cast<uint4*>(d + 32)[0] = reinterpret_cast<const uint4*>(r1)[0];
+          reinterpret_cast<uint4*>(d + 32)[1] = reinterpret_cast<const uint4*>(r1)[1];
         }
       };
       const int x = min(row, 13);
