@@ -162,6 +162,11 @@ DEV unsigned long long hw_location() {
 // HBM after the kernel-boundary write-back).  A bijection of [0, grid); identity when grid % 8 != 0.
 DEV int xcd_unit(int g, int grid, int on) { return (on && (grid & 7) == 0) ? (g & 7) * (grid >> 3) + (g >> 3) : g; }
 
+// 16-bit halves of two dwords packed into one (v_perm_b32): lo16 = a[15:0] | b[15:0] << 16, hi16 = a[31:16] | b[31:16] << 16
+DEV uint32_t pack_lo16(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x05040100u); }
+DEV uint32_t pack_hi16(uint32_t a, uint32_t b) { return __builtin_amdgcn_perm(b, a, 0x07060302u); }
+DEV uint32_t pack_half16(uint32_t a, uint32_t b, int hi) { return hi ? pack_hi16(a, b) : pack_lo16(a, b); }
+
 DEV int lane_id() { return threadIdx.x & 63; }
 DEV int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 

@@ -350,24 +350,27 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const bool live = (look ? r0 + r + q < B : sIdx[r + q] >= 0) && c < H::K0 / 16;
+          const uint32_t lm = live ? 0xFFFFFFFFu : 0u;  // the row's pixels or zeros, applied to packed pairs
+          typedef __attribute__((ext_vector_type(2))) float f32x2;
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            bf16x8 f;
+            uint32_t d[4];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {  // computed unconditionally, then selected: no per-pixel branch
-              const float nv = mnist_norm((px[i][q][2 * h + (j >> 2)] >> (8 * (j & 3))) & 255u);
-              f[j] = (bf16)(live ? nv : 0.f);
+            for (int k = 0; k < 4; ++k) {  // pixel pairs: one v_cvt_pk_bf16_f32 each, computed unconditionally
+              const uint32_t wv = px[i][q][2 * h + (k >> 1)];
+              const float a = mnist_norm((wv >> (16 * (k & 1))) & 255u), b = mnist_norm((wv >> (16 * (k & 1) + 8)) & 255u);
+              d[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2{a, b}), bf16x2)) & lm;
             }
-            pk[q][h] = __builtin_bit_cast(u32x4, f);
+            pk[q][h] = u32x4{d[0], d[1], d[2], d[3]};
             if (item) *reinterpret_cast<u32x4*>(sX + (r + q) * S::PX + c * 16 + h * 8) = pk[q][h];
           }
         }
         if (TRAIN && item && !ABLATED(hb.ablate, 1)) {
 #pragma unroll
           for (int j = 0; j < 16; ++j) {
-            const int h = j >> 3, wd = (j & 7) >> 1, sh = 16 * (j & 1);
-            const uint32_t lo = ((pk[0][h][wd] >> sh) & 0xFFFFu) | (((pk[1][h][wd] >> sh) & 0xFFFFu) << 16);
-            const uint32_t hi = ((pk[2][h][wd] >> sh) & 0xFFFFu) | (((pk[3][h][wd] >> sh) & 0xFFFFu) << 16);
+            const int h = j >> 3, wd = (j & 7) >> 1;
+            const uint32_t lo = pack_half16(pk[0][h][wd], pk[1][h][wd], j & 1);  // one v_perm_b32 each
+            const uint32_t hi = pack_half16(pk[2][h][wd], pk[3][h][wd], j & 1);
             *reinterpret_cast<u32x2*>(xT + (size_t)(c * 16 + j) * ldB + r0 + r) = u32x2{lo, hi};
           }
         }
@@ -414,9 +417,9 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
           for (int j = 0; j < XVE; ++j) {
             T* dst = xT + (size_t)(k + j) * ldB + r0 + r;
             if constexpr (sizeof(T) == 2) {
-              const int w = j >> 1, sh = 16 * (j & 1);
-              const uint32_t lo = ((word(rv[0], w) >> sh) & 0xFFFFu) | (((word(rv[1], w) >> sh) & 0xFFFFu) << 16);
-              const uint32_t hi = ((word(rv[2], w) >> sh) & 0xFFFFu) | (((word(rv[3], w) >> sh) & 0xFFFFu) << 16);
+              const int w = j >> 1;
+              const uint32_t lo = pack_half16(word(rv[0], w), word(rv[1], w), j & 1);
+              const uint32_t hi = pack_half16(word(rv[2], w), word(rv[3], w), j & 1);
               *reinterpret_cast<u32x2*>(dst) = u32x2{lo, hi};
             } else {
               *reinterpret_cast<u32x4*>(dst) = u32x4{word(rv[0], j), word(rv[1], j), word(rv[2], j), word(rv[3], j)};

@@ -648,9 +648,9 @@ DEV void head16_tile(const BatchRef& br, const HeadBuffers& hb, char* ht, T* sX,
       for (int q = 0; q < 4; ++q) v[q] = *reinterpret_cast<const u32x4*>(sX + (rq + q) * S::PX + c * 8);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int wd = j >> 1, sh = 16 * (j & 1);
-        const uint32_t lo = ((v[0][wd] >> sh) & 0xFFFFu) | (((v[1][wd] >> sh) & 0xFFFFu) << 16);
-        const uint32_t hi = ((v[2][wd] >> sh) & 0xFFFFu) | (((v[3][wd] >> sh) & 0xFFFFu) << 16);
+        const int wd = j >> 1;
+        const uint32_t lo = pack_half16(v[0][wd], v[1][wd], j & 1);  // one v_perm_b32 each
+        const uint32_t hi = pack_half16(v[2][wd], v[3][wd], j & 1);
         *reinterpret_cast<u32x2*>(xT + (size_t)(c * 8 + j) * ldB + r0 + rq) = u32x2{lo, hi};
       }
     }
