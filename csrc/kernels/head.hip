@@ -952,7 +952,7 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
   const int lane = threadIdx.x & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
   const int lin = blockIdx.y * gridDim.x + blockIdx.x;  // profiling stamps: [0] start, [1] end
   if (a.stamps && threadIdx.x == 0 && lin < 512) a.stamps[(STAMP_WGRAD + lin) * 16] = wall_clock64();
-  int tile, split, nsteps, x = 0, m0 = 0, spc = 1, rs = 0;
+  int tile, split, nsteps, x = 0, m0 = 0, spc = 1, sh = 0, rs = 0;
   if (a.xcd_ch == 0) {
     tile = blockIdx.x;
     split = blockIdx.y;
@@ -967,13 +967,14 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
     const int mx = a.contig ? a.nch / 8 : (x < a.nch ? (a.nch - x + 7) / 8 : 0);  // chunks owned by XCD x
     m0 = sub * mx / a.sx;
     const int m1 = (sub + 1) * mx / a.sx;
-    spc = a.xcd_ch / KC;
+    spc = a.xcd_ch / KC;  // a power of two (wgrad_launch): steps -> chunks by shift and mask, no division
+    sh = __builtin_ctz(spc);
     nsteps = (m1 - m0) * spc;
   }
   auto step_row = [&](int st) -> int {  // first batch row of step st (may be >= Bp: skipped)
     if (a.xcd_ch == 0) return rs + st * KC;
-    const int m = m0 + st / spc;
-    return (a.contig ? x * (a.nch / 8) + m : x + 8 * m) * a.xcd_ch + (st % spc) * KC;
+    const int m = m0 + (st >> sh);
+    return (a.contig ? x * (a.nch / 8) + m : x + 8 * m) * a.xcd_ch + (st & (spc - 1)) * KC;
   };
   int j = 0;
   while (j + 1 < a.njobs && tile >= a.job[j + 1].blk_begin) ++j;
@@ -1062,11 +1063,11 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
 
 // Batch rows of a wgrad workgroup's K-steps (wgrad_kernel's split / XCD-aware mapping, see WgArgs).
 struct WgRows {
-  int xcd_ch, rs, m0, spc, x, contig, nch;
+  int xcd_ch, rs, m0, spc, x, contig, nch, sh;  // spc = 1 << sh steps per chunk (a power of two: wgrad_launch)
   DEV int operator()(int st, int KC) const {  // first batch row of step st (monotonic in st)
     if (xcd_ch == 0) return rs + st * KC;
-    const int m = m0 + st / spc;
-    return (contig ? x * (nch / 8) + m : x + 8 * m) * xcd_ch + (st % spc) * KC;
+    const int m = m0 + (st >> sh);  // (was st / spc: ~30 scalar instructions per call, in every K-step's loads)
+    return (contig ? x * (nch / 8) + m : x + 8 * m) * xcd_ch + (st & (spc - 1)) * KC;
   }
 };
 
@@ -1208,7 +1209,7 @@ __global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
   const int lin = blockIdx.y * gridDim.x + blockIdx.x;
   if (a.stamps && threadIdx.x == 0 && lin < 512) a.stamps[(STAMP_WGRAD + lin) * 16] = wall_clock64();
   int tile, split, nsteps;
-  WgRows rows{a.xcd_ch, 0, 0, 1, 0, a.contig, a.nch};
+  WgRows rows{a.xcd_ch, 0, 0, 1, 0, a.contig, a.nch, 0};
   if (a.xcd_ch == 0) {
     tile = blockIdx.x;
     split = blockIdx.y;
@@ -1224,6 +1225,7 @@ __global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
     rows.m0 = sub * mx / a.sx;
     const int m1 = (sub + 1) * mx / a.sx;
     rows.spc = a.xcd_ch / KC;
+    rows.sh = __builtin_ctz(rows.spc);
     nsteps = (m1 - rows.m0) * rows.spc;
   }
   while (nsteps > 0 && rows(nsteps - 1, KC) >= a.Bp) --nsteps;  // steps past the (padded) batch
@@ -1260,7 +1262,8 @@ int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab
   constexpr int KC = Mma<T>::KC;
   const bool lds_stage = std::is_same<Model, MlpModel>::value;
   // XCD-aware mapping when the head's row tiling is known and the split count divides over 8 XCDs
-  if (!fuse && xcd_ch > 0 && xcd_ch % KC == 0 && splits % 8 == 0) {
+  // (steps per row chunk xcd_ch / KC must be a power of two: the kernels map steps to rows by shift and mask)
+  if (!fuse && xcd_ch > 0 && xcd_ch % KC == 0 && ((xcd_ch / KC) & (xcd_ch / KC - 1)) == 0 && splits % 8 == 0) {
     a.xcd_ch = xcd_ch;
     a.nch = (a.Bp + xcd_ch - 1) / xcd_ch;
     a.sx = splits / 8;
