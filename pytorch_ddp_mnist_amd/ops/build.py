@@ -77,8 +77,10 @@ def build_c(force: bool = False, jobs: int = 8, csrc: Path = CSRC, out: Path = N
     # MNIST_AMD_BUILD_DEFINES: extra -D flags of a diagnostic build (e.g. -DMNIST_AMD_ABLATION_BUILD for
     # scripts/ablate.sh); part of the object-cache key, so switching back rebuilds the normal objects
     defs = os.environ.get("MNIST_AMD_BUILD_DEFINES", "").split()
+    # MNIST_AMD_HIP_FLAGS: extra hipcc-only flags of a diagnostic build (code-generation options)
+    hip_extra = os.environ.get("MNIST_AMD_HIP_FLAGS", "").split()
     hip_cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", f"-I{csrc}",
-               "-Wno-unused-result"] + defs
+               "-Wno-unused-result"] + defs + hip_extra
     cpp_cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-D__HIP_PLATFORM_AMD__", f"-I{ROCM / 'include'}",
                f"-I{csrc}", "-fvisibility=hidden"] + defs + _pybind_includes()
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
