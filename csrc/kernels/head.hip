@@ -30,6 +30,30 @@ using wg::WgArgs;
 using wg::WgJob;
 using wg::wgrad_sgd_tile;
 
+// fp32 products as exact 3-part bf16 splits (common.h Mma<float>::mma_s: three 16x16x32 bf16 MFMAs per 16-k
+// chunk, 48 cycles, instead of 4 x 32 for v_mfma_f32_16x16x4_f32; ~2^-24 relative, every fp32 tolerance test
+// passes): the weight-gradient GEMMs (wg_mma; the MLP's from B = 4096, wgrad_launch) and the head's products at
+// row tiles of >= 32 (head_mma<T, true>; the compiler hoists the cut of the B fragment the row tiles share).
+// Measured against exact fp32 MFMA (profiles/r5_session1/hsplit, hsplit2): weight gradient -2 % LeNet fp32
+// B=8192, -3 % B=1024, -6 % MLP fp32 B=8192 (+6 % at B=1024); the head split another -3 % on the MLP at B=8192
+// but +6 % (MLP) / +1.5 % (LeNet) at B=128 (16-row tiles, l1_split_kernel).
+#ifndef MNIST_AMD_HEAD_SPLIT
+#define MNIST_AMD_HEAD_SPLIT 1
+#endif
+#ifndef MNIST_AMD_WGRAD_SPLIT
+#define MNIST_AMD_WGRAD_SPLIT 1
+#endif
+template <typename T, bool SPLIT = true, typename F>
+DEV void head_mma(f32x4& acc, const F& a, const F& b) {
+  if constexpr (sizeof(T) == 4 && SPLIT && MNIST_AMD_HEAD_SPLIT) Mma<float>::mma_s(acc, a, b);
+  else Mma<T>::mma(acc, a, b);
+}
+template <typename T, bool SPLIT = true, typename F>
+DEV void wg_mma(f32x4& acc, const F& a, const F& b) {
+  if constexpr (sizeof(T) == 4 && SPLIT && MNIST_AMD_WGRAD_SPLIT) Mma<float>::mma_s(acc, a, b);
+  else Mma<T>::mma(acc, a, b);
+}
+
 template <typename T, class H, int MT, bool PRE = false>
 struct HeadSmem {
   static constexpr int R = MT * 16;
@@ -123,6 +147,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   using M = Mma<T>;
   using Frag = typename M::Frag;
   constexpr int R = S::R, KV = M::KV, KC = M::KC, NTH = NWV * 64;
+  constexpr bool HSP = !PRE && MT >= 2;  // fp32: products as 3-part bf16 splits (head_mma)
   static_assert(S::FITS, "head tile does not fit in LDS");
   __shared__ __attribute__((aligned(16))) char smem[S::TOTAL];
   T* sX = reinterpret_cast<T*>(smem + S::OFF_X);
@@ -508,7 +533,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
           if (kc >= l1_k1) break;  // wave-uniform (second half of an odd chunk count)
           const Frag b = (PF1 && j == 0) ? b1pre[PF1 ? kk : 0] : M::load(bp + kc * 64 * KV);
 #pragma unroll
-          for (int m = 0; m < MT; ++m) M::mma(acc[m], M::load(ap + m * 16 * S::PX + kc * KC), b);
+          for (int m = 0; m < MT; ++m) head_mma<T, HSP>(acc[m], M::load(ap + m * 16 * S::PX + kc * KC), b);
         }
       }
       if constexpr (KS1) {
@@ -573,7 +598,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       for (int kc = 0; kc < KCH; ++kc) {
         const Frag b = M::load(bp + kc * KC);
 #pragma unroll
-        for (int m = 0; m < MT; ++m) M::mma(acc[m], M::load(ap + m * 16 * S::P1 + kc * KC), b);
+        for (int m = 0; m < MT; ++m) head_mma<T, HSP>(acc[m], M::load(ap + m * 16 * S::P1 + kc * KC), b);
       }
       const int n = nt * 16 + row;
       const float bias = sB2[n];
@@ -603,7 +628,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       f32x4 acc = zero4();
       const T* bp = bW3 + row * LW3 + grp * KV;
       const T* ap = sH2 + (m * 16 + row) * S::P2 + grp * KV;
-      for (int kc = 0; kc < KCH; ++kc) M::mma(acc, M::load(ap + kc * KC), M::load(bp + kc * KC));
+      for (int kc = 0; kc < KCH; ++kc) head_mma<T, HSP>(acc, M::load(ap + kc * KC), M::load(bp + kc * KC));
       const int c = row;
       const float bias = sB3[c];
 #pragma unroll
@@ -724,7 +749,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       for (int kc = 0; kc < KCH; ++kc) {
         const Frag b = TW3 ? load_kstrided<T>(bp + kc * KC * LW3, LW3) : M::load(bp + kc * KC);
 #pragma unroll
-        for (int m = 0; m < MT; ++m) M::mma(acc[m], M::load(ap + m * 16 * S::PD + kc * KC), b);
+        for (int m = 0; m < MT; ++m) head_mma<T, HSP>(acc[m], M::load(ap + m * 16 * S::PD + kc * KC), b);
       }
       const int n = nt * 16 + row;
 #pragma unroll
@@ -766,7 +791,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       for (int kc = 0; kc < KCH; ++kc) {
         const Frag b = TW2 ? load_kstrided<T>(bp + kc * KC * LW2, LW2) : M::load(bp + kc * KC);
 #pragma unroll
-        for (int m = 0; m < MT; ++m) M::mma(acc[m], M::load(ap + m * 16 * S::P2 + kc * KC), b);
+        for (int m = 0; m < MT; ++m) head_mma<T, HSP>(acc[m], M::load(ap + m * 16 * S::P2 + kc * KC), b);
       }
       const int n = nt * 16 + row;
 #pragma unroll
@@ -803,7 +828,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       for (int kc = 0; kc < KCHX; ++kc) {
         const Frag b = j < PXT ? bx[j < PXT ? j : 0][kc] : M::load(bp + kc * KC);
 #pragma unroll
-        for (int m = 0; m < MT; ++m) M::mma(acc[m], M::load(ap + m * 16 * S::P1 + kc * KC), b);
+        for (int m = 0; m < MT; ++m) head_mma<T, HSP>(acc[m], M::load(ap + m * 16 * S::P1 + kc * KC), b);
       }
       const int k = nt * 16 + row;
 #pragma unroll
@@ -926,8 +951,8 @@ __global__ __launch_bounds__(256) void l1_split_kernel(BatchRef br, HeadBuffers 
 #pragma unroll
   for (int i = 0; i < QCH; ++i) {
     if (c0 + i < c1) {  // uniform: only the last K range is shorter
-      if (i & 1) M::mma(acc1, M::load(ap + i * KC), bpre[i]);
-      else M::mma(acc0, M::load(ap + i * KC), bpre[i]);
+      if (i & 1) head_mma<T, false>(acc1, M::load(ap + i * KC), bpre[i]);
+      else head_mma<T, false>(acc0, M::load(ap + i * KC), bpre[i]);
     }
   }
   f32x4 acc;
@@ -1029,10 +1054,10 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgArgs<T> a) {
       const Frag b1 = sel1 == 0 ? rb1[d] : (sel1 == 1 ? ones : zf);
       const int rn = st + WD < nsteps ? step_row(st + WD) : a.Bp;
       if (rn < a.Bp) fetch(d, rn);
-      M::mma(acc[0][0], a0, b0);
-      M::mma(acc[0][1], a0, b1);
-      M::mma(acc[1][0], a1, b0);
-      M::mma(acc[1][1], a1, b1);
+      wg_mma<T>(acc[0][0], a0, b0);
+      wg_mma<T>(acc[0][1], a0, b1);
+      wg_mma<T>(acc[1][0], a1, b0);
+      wg_mma<T>(acc[1][1], a1, b1);
     }
   }
 
@@ -1084,7 +1109,7 @@ struct WgRows {
 //    profiles/r4_session2/ab_mlp8k_raw_rows.txt.)
 // Rows padded by 32 B (conflict-free ds_read_b128 fragment reads).  LDS use keeps it to the schedules where
 // nothing LDS-heavy runs beside it (the MLP; LeNet's FC wgrad runs beside conv_bwd on the LDS-free kernel).
-template <typename T, int SUB>
+template <typename T, int SUB, bool SPL>
 DEV void wgrad_lds_body(const WgArgs<T>& a, const int j, const WgRows rows, const int nsteps, const int tile,
                         const int split, T* sa, T* sb) {
   const WgJob<T>& J = a.job[j];
@@ -1154,10 +1179,10 @@ DEV void wgrad_lds_body(const WgArgs<T>& a, const int j, const WgRows rows, cons
         Frag b0, b1;
         b0.v = use0 ? f0.v : alt0.v;
         b1.v = use1 ? f1.v : alt1.v;
-        M::mma(acc[0][0], a0, b0);
-        M::mma(acc[0][1], a0, b1);
-        M::mma(acc[1][0], a1, b0);
-        M::mma(acc[1][1], a1, b1);
+        wg_mma<T, SPL>(acc[0][0], a0, b0);
+        wg_mma<T, SPL>(acc[0][1], a0, b1);
+        wg_mma<T, SPL>(acc[1][0], a1, b0);
+        wg_mma<T, SPL>(acc[1][1], a1, b1);
       }
     }
   };
@@ -1201,7 +1226,7 @@ DEV void wgrad_lds_body(const WgArgs<T>& a, const int j, const WgRows rows, cons
     }
 }
 
-template <typename T, int SUB>
+template <typename T, int SUB, bool SPL>
 __global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
   constexpr int KC = Mma<T>::KC;
   constexpr int TILE = 64 * ((SUB * 64 + 32) / (int)sizeof(T));
@@ -1232,7 +1257,7 @@ __global__ __launch_bounds__(256) void wgrad_lds_kernel(WgArgs<T> a) {
   nsteps = __builtin_amdgcn_readfirstlane(nsteps);
   int j = 0;
   while (j + 1 < a.njobs && tile >= a.job[j + 1].blk_begin) ++j;
-  wgrad_lds_body<T, SUB>(a, j, rows, nsteps, tile, split, lds[0], lds[1]);
+  wgrad_lds_body<T, SUB, SPL>(a, j, rows, nsteps, tile, split, lds[0], lds[1]);
   if (a.stamps && threadIdx.x == 0 && lin < 512) a.stamps[(STAMP_WGRAD + lin) * 16 + 1] = wall_clock64();
 }
 
@@ -1261,6 +1286,9 @@ int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab
   WgArgs<T> a = wg::make_args<T, H, Model>(hb, B, splits, slab, slab_ld, fuse, job_mask, &blk);
   constexpr int KC = Mma<T>::KC;
   const bool lds_stage = std::is_same<Model, MlpModel>::value;
+  // fp32 MLP weight gradient as 3-part bf16 splits from B = 4096 on (MLP fp32 B=8192 -6 %, but B=1024 +6 %:
+  // profiles/r5_session1/hsplit2); no effect for bf16 (wg_mma)
+  const bool spl = B >= 4096;
   // XCD-aware mapping when the head's row tiling is known and the split count divides over 8 XCDs
   // (steps per row chunk xcd_ch / KC must be a power of two: the kernels map steps to rows by shift and mask)
   if (!fuse && xcd_ch > 0 && xcd_ch % KC == 0 && ((xcd_ch / KC) & (xcd_ch / KC - 1)) == 0 && splits % 8 == 0) {
@@ -1269,12 +1297,14 @@ int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab
     a.sx = splits / 8;
     const int head_grid = (rup(B, 32) + xcd_ch - 1) / xcd_ch;  // head_launch_mtw's grid
     a.contig = hb.xcd && head_grid % 8 == 0 && a.nch == head_grid;
-    if (lds_stage) hipLaunchKernelGGL((wgrad_lds_kernel<T, WGRAD_SUB>), dim3(blk * splits), dim3(256), 0, s, a);
+    if (lds_stage && spl) hipLaunchKernelGGL((wgrad_lds_kernel<T, WGRAD_SUB, true>), dim3(blk * splits), dim3(256), 0, s, a);
+    else if (lds_stage) hipLaunchKernelGGL((wgrad_lds_kernel<T, WGRAD_SUB, false>), dim3(blk * splits), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((wgrad_kernel<T, WGRAD_DEPTH>), dim3(blk * splits), dim3(256), 0, s, a);
   } else if (a.fuse) {
     hipLaunchKernelGGL((wgrad_sgd_kernel<T, Model>), dim3(blk), dim3(256), 0, s, a);
   } else {
-    if (lds_stage) hipLaunchKernelGGL((wgrad_lds_kernel<T, WGRAD_SUB>), dim3(blk, splits), dim3(256), 0, s, a);
+    if (lds_stage && spl) hipLaunchKernelGGL((wgrad_lds_kernel<T, WGRAD_SUB, true>), dim3(blk, splits), dim3(256), 0, s, a);
+    else if (lds_stage) hipLaunchKernelGGL((wgrad_lds_kernel<T, WGRAD_SUB, false>), dim3(blk, splits), dim3(256), 0, s, a);
     else hipLaunchKernelGGL((wgrad_kernel<T, WGRAD_DEPTH>), dim3(blk, splits), dim3(256), 0, s, a);
   }
   return splits;
