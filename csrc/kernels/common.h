@@ -59,10 +59,25 @@ template <> struct Mma<float> {
   static DEV void mma_psb(f32x4& acc, const Frag& a, const u32x2 bh, const u32x2 bm, const u32x2 bl) {
     u32x2 ah, am, al;
     split3(a.v, ah, am, al);
+    mma_pp(acc, ah, am, al, bh, bm, bl);
+  }
+  // both operands given as their three parts (pre-split operand images: no cut at use)
+  static DEV void mma_pp(f32x4& acc, const u32x2 ah, const u32x2 am, const u32x2 al, const u32x2 bh, const u32x2 bm,
+                         const u32x2 bl) {
     const bf16x8 ahm = cat(ah, am);
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cat(ah, al), cat(bl, bh), acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahm, cat(bm, bm), acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahm, cat(bh, bh), acc, 0, 0, 0);
+  }
+  // the three parts of one fp32 value as bf16 bit patterns (the scalar split3, for pre-split operand images)
+  static DEV void split3_1(const float x, uint16_t& h, uint16_t& m, uint16_t& l) {
+    const uint32_t xb = __float_as_uint(x);
+    const float r1 = x - __uint_as_float(xb & 0xFFFF0000u);  // exact
+    const uint32_t r1b = __float_as_uint(r1);
+    const float r2 = r1 - __uint_as_float(r1b & 0xFFFF0000u);  // exact, low 16 bits zero
+    h = (uint16_t)(xb >> 16);
+    m = (uint16_t)(r1b >> 16);
+    l = (uint16_t)(__float_as_uint(r2) >> 16);
   }
   // both operands cut here (the compiler hoists the cut of a loop-invariant b)
   static DEV void mma_s(f32x4& acc, const Frag& a, const Frag& b) {

@@ -34,6 +34,9 @@ constexpr int K0P = L::Head::K0P;  // 416
 // pool1 activations / codes handed from conv_fwd to conv_bwd through HBM, channel-major with rows
 // padded 14 -> 16 (CHW16), the layout conv_bwd stages into LDS with 16-byte stores; channel pitches
 // padded so conv_fwd's per-lane epilogue stores hit distinct LDS banks (lane = channel fastest)
+#ifndef MNIST_AMD_F32_C2SPLIT
+#define MNIST_AMD_F32_C2SPLIT 1  // fp32 conv2 forward on pre-split operand images (FwdSmem::SPL)
+#endif
 constexpr int P1CP = 232;            // pool1 value channel pitch (elements), >= 14 * 16
 constexpr int P1IMG = 6 * P1CP;      // elements per image in cb.p1
 constexpr int M1CP = 240;            // pool1 code channel pitch (bytes), multiple of 16
@@ -89,8 +92,13 @@ struct FwdSmem {
   static constexpr int NPL = sizeof(T) == 2 ? 4 : 2;
   static constexpr int OFF_XS = 0;                                        // [NPL][XP] T
   static constexpr int XTAIL = 64;  // zeroed tail: conv1's all-zero kernel row kh' = 7 reads 1 row past the last plane
+  // SPL (fp32): conv2's operands as pre-split bf16 images -- pool1 as three [196][8] planes (hi, mid, lo) written
+  // by conv1's epilogue, W2 as three [16][W2P] planes staged once -- read by Mma<float>::mma_pp: three 16x16x32
+  // bf16 MFMAs per 16-k chunk (48 cycles) instead of four v_mfma_f32_16x16x4_f32 (128), with no cut at use
+  static constexpr bool SPL = sizeof(T) == 4 && MNIST_AMD_F32_C2SPLIT;
   static constexpr int OFF_P1 = rup((NPL * XP + XTAIL) * (int)sizeof(T), 16);  // [196][8] T   pool1 output (conv2 im2col)
-  static constexpr int OFF_P1C = rup(OFF_P1 + 196 * 8 * (int)sizeof(T), 16);  // [6][P1CP] T pool1, CHW16 (-> HBM)
+  static constexpr int P1_BYTES = SPL ? 3 * 196 * 8 * 2 : 196 * 8 * (int)sizeof(T);
+  static constexpr int OFF_P1C = rup(OFF_P1 + P1_BYTES, 16);                  // [6][P1CP] T pool1, CHW16 (-> HBM)
   static constexpr int OFF_M1 = rup(OFF_P1C + P1IMG * (int)sizeof(T), 16);    // [6][M1CP] u8 pool1 codes, CHW16
   static constexpr int OFF_P2 = rup(OFF_M1 + M1IMG, 16);                  // [400] T      pool2 output (NCHW)
   static constexpr int OFF_M2 = rup(OFF_P2 + 400 * (int)sizeof(T), 16);   // [400] u8     pool2 codes
@@ -106,7 +114,8 @@ struct FwdSmem {
   static constexpr int JUNK_BYTES = rup((6 * 2 * 14 * 8 + 64) * (int)sizeof(T), 16);
   static constexpr int OFF_JUNK = rup(OFF_M2 + 400, 16);                   // junk stores
   static constexpr int OFF_W2 = OFF_JUNK + JUNK_BYTES;                     // [16][W2P] T  conv2 B operand
-  static constexpr int TOTAL = W2LDS ? rup(OFF_W2 + 16 * W2P * (int)sizeof(T), 16) : OFF_W2;
+  static constexpr int W2_BYTES = SPL ? 3 * 16 * W2P * 2 : 16 * W2P * (int)sizeof(T);
+  static constexpr int TOTAL = W2LDS ? rup(OFF_W2 + W2_BYTES, 16) : OFF_W2;
 };
 
 // Coalesced 16-byte copy of a staged LDS image to global memory (both 16-byte aligned).  STREAM: the
@@ -187,6 +196,13 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
   // conv1's B operand lives in registers, and so does conv2's for bf16 (7 chunks; the kernel stays
   // well under 128 VGPRs, 4 waves per SIMD: the whole 1024-block grid co-resident)
   T* w2s = reinterpret_cast<T*>(smem + S::OFF_W2);  // (f32 only)
+  // (SPL) the hi / mid / lo planes of pool1 and W2
+  uint16_t* const p1h = reinterpret_cast<uint16_t*>(smem + S::OFF_P1);
+  uint16_t* const p1m = p1h + 196 * 8;
+  uint16_t* const p1l = p1m + 196 * 8;
+  uint16_t* const w2h = reinterpret_cast<uint16_t*>(smem + S::OFF_W2);
+  uint16_t* const w2m = w2h + 16 * S::W2P;
+  uint16_t* const w2l = w2m + 16 * S::W2P;
   // conv1 B operand for TWO pooled rows per tile: column (r, c) = (row >> 3, row & 7), k = kh'*8 + kw
   // with kh' = kh + 2r in 0..7, so B[(kh', kw)][(r, c)] = W1[c][kh' - 2r][kw] (zero outside 0..4)
   // (a lane's KV k-values never straddle a kernel row, so each fragment is one 16-byte load or zero)
@@ -200,7 +216,17 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
     }
   }
   Frag b2r[S::W2LDS ? 1 : C2CH];
-  if constexpr (S::W2LDS) {
+  if constexpr (S::SPL) {
+    for (int e = tid; e < 16 * 224 / 4; e += NT) {
+      const int r = e / 56, c = (e % 56) * 4;
+      const f32x4 v = *reinterpret_cast<const f32x4*>(pack + L::C2F + r * 224 + c);
+      u32x2 h, m, l;
+      Mma<float>::split3(v, h, m, l);
+      *reinterpret_cast<u32x2*>(w2h + r * S::W2P + c) = h;
+      *reinterpret_cast<u32x2*>(w2m + r * S::W2P + c) = m;
+      *reinterpret_cast<u32x2*>(w2l + r * S::W2P + c) = l;
+    }
+  } else if constexpr (S::W2LDS) {
     constexpr int VE = 16 / (int)sizeof(T);
     for (int e = tid; e < 16 * 224 / VE; e += NT) {
       const int r = e / (224 / VE), c = (e % (224 / VE)) * VE;
@@ -246,6 +272,11 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
   const int n1 = row & 7;
   const bool st1 = c1valid && n1 < 6;
   T* const e1_p1s = c1valid ? p1s + ((row >> 3) * 14 + 4 * wc + grp) * 8 + n1 : reinterpret_cast<T*>(junk);
+  // (SPL: the three planes; a junk lane's three stores all go to its junk base)
+  const int e1_i = ((row >> 3) * 14 + 4 * wc + grp) * 8 + n1;
+  uint16_t* const e1_h = c1valid ? p1h + e1_i : reinterpret_cast<uint16_t*>(junk);
+  uint16_t* const e1_m = c1valid ? p1m + e1_i : reinterpret_cast<uint16_t*>(junk);
+  uint16_t* const e1_l = c1valid ? p1l + e1_i : reinterpret_cast<uint16_t*>(junk);
   T* const e1_p1c = st1 ? p1c + n1 * P1CP + (row >> 3) * 16 + 4 * wc + grp : reinterpret_cast<T*>(junk);
   uint8_t* const e1_m1s = st1 ? m1s + n1 * M1CP + (row >> 3) * 16 + 4 * wc + grp : reinterpret_cast<uint8_t*>(junk);
   auto c1_epi = [&](int t, const f32x4& acc) {  // pool + bias + ReLU, staged in LDS (pooled row 2t + r)
@@ -258,7 +289,15 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
     // (padding channels n1 = 6, 7: zero weights and zero bias give pre = 0 exactly, so ReLU stores the 0 the
     //  conv2 im2col rows need without a select)
     const T v = to_t<T>(fmaxf(pre, 0.f));
-    e1_p1s[t * 2 * 14 * 8] = v;
+    if constexpr (S::SPL) {
+      uint16_t h, m, l;
+      Mma<float>::split3_1(v, h, m, l);
+      e1_h[t * 2 * 14 * 8] = h;
+      e1_m[t * 2 * 14 * 8] = m;
+      e1_l[t * 2 * 14 * 8] = l;
+    } else {
+      e1_p1s[t * 2 * 14 * 8] = v;
+    }
     if (TRAIN) {
       e1_p1c[t * 2 * 16] = v;
       e1_m1s[t * 2 * 16] = (uint8_t)(am | (pre > 0.f ? 4 : 0));
@@ -281,8 +320,39 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
   // MFMAs (the rolled-up form waited for every A read before its MFMA).  (Measured: reading every A fragment
   // of the tiles first -- 14 reads in flight, 56 VGPRs -- pushed the fused kernel past 128 VGPRs into
   // scratch spills inside the image loop.)
+  struct SplitA { u32x2 h, m, l; };
+  auto c2_as = [&](int base, int kc) {  // (SPL) the A fragment's three parts: 4 channels of one tap per lane
+    const int pos = min(kc * 2 + (grp >> 1), 24), c0 = (grp & 1) * 4;
+    const int i = base + ((pos / 5) * 14 + pos % 5) * 8 + c0;
+    return SplitA{*reinterpret_cast<const u32x2*>(p1h + i), *reinterpret_cast<const u32x2*>(p1m + i),
+                  *reinterpret_cast<const u32x2*>(p1l + i)};
+  };
   auto c2_acc = [&](auto ntc, const int* mts, f32x4* acc) {
     constexpr int NT = decltype(ntc)::value;
+    if constexpr (S::SPL) {
+      int base[NT];
+      SplitA a[NT];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        base[j] = c2_base(mts[j]);
+        a[j] = c2_as(base[j], 0);
+      }
+      const int bo = row * S::W2P + grp * KV;
+#pragma unroll 1  // (fully unrolled, the training kernel spilled 26 VGPRs at its 128-register bound)
+      for (int kc = 0; kc < C2CH; ++kc) {
+        SplitA an[NT];
+#pragma unroll
+        for (int j = 0; j < NT; ++j) an[j] = kc + 1 < C2CH ? c2_as(base[j], kc + 1) : a[j];
+        const int bi = bo + kc * KC;
+        const u32x2 bh = *reinterpret_cast<const u32x2*>(w2h + bi), bm = *reinterpret_cast<const u32x2*>(w2m + bi),
+                    bl = *reinterpret_cast<const u32x2*>(w2l + bi);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) Mma<float>::mma_pp(acc[j], a[j].h, a[j].m, a[j].l, bh, bm, bl);
+#pragma unroll
+        for (int j = 0; j < NT; ++j) a[j] = an[j];
+      }
+      return;
+    }
     int base[NT];
     Frag a[NT];
 #pragma unroll
