@@ -500,7 +500,8 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
             // fp32: conv1's products as exact 3-part bf16 splits on 16x16x32 MFMAs (Mma<float>::mma_s; the cut of the
             // loop-invariant weights hoisted): 3 x 16 instead of 4 x 32 MFMA cycles per chunk on the convolution
             // whose K is 61 % padding (LeNet fp32 B=8192 0.4028 -> 0.3830 ms, profiles/r5_session1/f32conv1/).
-            // conv2 the same way -- B pre-split in LDS -- measured neutral; conv_bwd's streamed operands slower.
+            // conv2: both operands pre-split in LDS (FwdSmem::SPL; B alone pre-split was neutral); conv_bwd's streamed
+            // operands slower.
             if constexpr (sizeof(T) == 4) Mma<float>::mma_s(acc, fa[kc], b1[kc]);
             else M::mma(acc, fa[kc], b1[kc]);
           }
