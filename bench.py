@@ -368,6 +368,7 @@ def main(argv=None) -> int:
     ms = elapsed / a.steps * 1e3
     value = n_gpus * a.batch * a.steps / elapsed
     from pytorch_ddp_mnist_amd.ops.native import load_c as _load_c
+    from pytorch_ddp_mnist_amd.ops.precision import dtype_label, fp32_products
     split = getattr(_load_c(), "F32_SPLIT", 0) if a.dtype == "fp32" else 0
     out = {
         "metric": METRIC,
@@ -380,8 +381,9 @@ def main(argv=None) -> int:
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        # an opt-in split build (MNIST_AMD_F32_SPLIT) computes fp32 products as bf16-part MFMAs: say so
-        "dtype": a.dtype + (f" (products as {split}-part bf16 MFMAs)" if split else ""),
+        # fp32: which products run as exact 3-part bf16 splits (ops/precision.py; every one with the opt-in
+        # MNIST_AMD_F32_SPLIT build) -- config.fp32_products lists both kinds
+        "dtype": dtype_label(a.dtype, a.model, a.batch, split),
         "data": f"synthetic (MNIST-shaped 28x28 uint8, class-template + noise, mode={a.synthetic_mode}; "
                 "random-init weights)" + ("; loaded from a CDF-5 netCDF file" if load else ""),
         "config": {
@@ -397,6 +399,7 @@ def main(argv=None) -> int:
             "plan": info,
             "plan_autotune": tune,
             "hipgraph": use_graph,
+            **({"fp32_products": fp32_products(a.model, a.batch, split)} if a.dtype == "fp32" else {}),
         },
         "rccl_world": comm.world if comm is not None else None,
         "allreduce": "oneshot" if oneshot is not None else ("rccl" if comm is not None else None),
@@ -411,6 +414,8 @@ def main(argv=None) -> int:
             "epochs_trained": round((a.warmup + a.steps + acc_steps) * a.batch * n_gpus / 60000, 2)},
         "train_loss_mean": round(train.mean_loss, 4),
     }
+    if n_gpus > 1:
+        tr.agree_oneshot(ctx.all_reduce_max)  # one-shot data plane: every rank raises if any rank latched a failure
     if a.digest or a.dump_params:
         tr.synchronize()
         p = tr.params.detach().cpu()

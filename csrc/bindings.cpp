@@ -234,6 +234,14 @@ PYBIND11_MODULE(_C, m) {
       .def_property("comm_enabled", &Trainer::comm_enabled, &Trainer::set_comm_enabled)
       .def_property_readonly("phase_split", &Trainer::phase_split)
       .def("buckets", &Trainer::buckets)
+      .def("groups", [](const Trainer& t) {
+        py::list out;
+        for (const auto& g : t.groups()) out.append(py::make_tuple(g.p0, g.p1, g.mask));
+        return out;
+      })
+      .def("time_units", &Trainer::time_units, py::arg("iters"), py::arg("warmup"), py::arg("stream"),
+           py::call_guard<py::gil_scoped_release>())
+      .def_static("job_begin", [](int model, int job) { return model_job_begin(static_cast<ModelKind>(model), job); })
       .def("set_plan", &Trainer::set_plan)
       .def_property_readonly("plan", &Trainer::plan)
       .def("set_concurrent", &Trainer::set_concurrent)

@@ -1266,6 +1266,182 @@ __global__ __launch_bounds__(256) void wgrad_sgd_kernel(WgArgs<T> a) {
   wgrad_sgd_tile<T, Model>(a, blockIdx.x);
 }
 
+// ====================================================================================
+// Large-batch weight gradient with split-K INSIDE the workgroup (round 6; replaces wgrad_kernel /
+// wgrad_lds_kernel from B >= SK_MIN_B).  Same 64x64 output blocks, batch splits and slab layout as wgrad_kernel,
+// but each of the 4 waves computes the WHOLE 64x64 block (4x4 MFMA tiles, 64 accumulators) over every 4th
+// K-step of the workgroup's batch range, and the four partial blocks are summed through LDS in a fixed order
+// ((w0 + w1) + (w2 + w3)) before the one slab row is written.  Against wgrad_kernel (four 32x32 quadrants per
+// block, every fragment fetched by two waves): half the L2 -> CU fragment traffic, 16 instead of 4 MFMAs per
+// 8 fragment loads, and a quarter of the dependent K-steps per wave -- SK_PF steps (8 x SK_PF fragments) are
+// issued before the first MFMA, so a whole 512-row split is ONE memory round trip per wave (LeNet-5 / MLP at
+// B = 8192, 16 splits).  Round-5 counters of wgrad_kernel: 15.9 us at 1.9 % MFMA busy, latency-bound
+// (profiles/r5_session1/pmc_table_final.md).
+// fp32 (SPL): the 4 A and 4 B fragments of a K-step are cut into bf16 hi / mid / lo parts ONCE and reused by the
+// 16 products (Mma<float>::mma_pp), instead of a cut per product.
+constexpr int SK_MIN_B = 2048;  // smallest batch on the split-K-in-workgroup kernel
+// PF: K-steps per wave whose fragments are in flight together (8 x PF 16-byte loads per lane)
+template <typename T, bool SPL, int PF>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF > 2 || (sizeof(T) == 4 && SPL) ? 2 : 3))) void wgrad_sk_kernel(WgArgs<T> a) {
+  using M = Mma<T>;
+  using Frag = typename M::Frag;
+  constexpr int KV = M::KV, KC = M::KC;
+  constexpr bool CUT = sizeof(T) == 4 && SPL;
+  __shared__ __attribute__((aligned(16))) f32x4 red[2][16][64];  // 32 KB: two waves' partial blocks at a time
+  const int lane = threadIdx.x & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
+  const int L = blockIdx.x;
+  if (a.stamps && threadIdx.x == 0 && L < 512) a.stamps[(STAMP_WGRAD + L) * 16] = wall_clock64();
+  int tile, split;
+  if (a.xcd_ch > 0) {  // XCD-aware: workgroup L runs on XCD L % 8 and takes a split of that XCD's batch rows
+    const int x = L & 7, q = L >> 3;
+    tile = q / a.sx;
+    split = x * a.sx + q % a.sx;
+  } else {
+    const int ns = (a.Bp + a.rlen - 1) / a.rlen;
+    tile = L / ns;
+    split = L % ns;
+  }
+  const int rs = split * a.rlen, re = min(rs + a.rlen, a.Bp);
+  const int nsteps = (re - rs) / KC;                      // K-steps of this workgroup (block-uniform)
+  const int nw = nsteps > w ? (nsteps - w + 3) / 4 : 0;  // this wave's: steps w, w + 4, ...
+  int j = 0;
+  while (j + 1 < a.njobs && tile >= a.job[j + 1].blk_begin) ++j;
+  const WgJob<T>& J = a.job[j];
+  const int lb = tile - J.blk_begin;
+  const int bn = lb / J.nblk_k, bk = lb % J.nblk_k;
+  const int n0 = bn * 64, k0 = bk * 64;
+  // Branch-free body: every fragment load is issued (rows clamped into the operand images: A rows past NP read
+  // the zero-padded row NP - 1 or feed only discarded outputs, B rows past K the last row) and all 16 MFMAs of a
+  // K-step run; B columns past K read ones (bias column) or zeros by a per-lane select.  (Branching around the
+  // padding tiles' loads and MFMAs put 261 conditional branches into the loop.)
+  const T* ap[4];
+  const T* bp[4];
+  bool use[4];
+  Frag alt[4];
+  Frag ones;
+#pragma unroll
+  for (int q = 0; q < KV; ++q) M::set(ones, q, 1.f);
+  const Frag zf = M::zero();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    ap[i] = J.dyT + (size_t)min(n0 + 16 * i + row, J.NP - 1) * a.ldB + rs + grp * KV;
+    const int kk = k0 + 16 * i + row;
+    bp[i] = J.xT + (size_t)min(kk, J.K > 0 ? J.K - 1 : 0) * a.ldB + rs + grp * KV;
+    use[i] = kk < J.K;
+    alt[i] = (kk == J.K && J.bias) ? ones : zf;  // bias column: ones; padding: zeros
+  }
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = zero4();
+
+  // K-step groups: every fragment of PF steps is issued before the first MFMA (the sched_barrier keeps hipcc
+  // from sinking each load next to its use -- it had turned the group into one load + vmcnt(0) per 4 MFMAs); a
+  // group's steps past this wave's count re-read its last step and multiply zero A fragments
+  for (int g = 0; g < nw; g += PF) {
+    Frag fa[PF][4], fb[PF][4];
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      const int off = (w + 4 * min(g + p, nw - 1)) * KC;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        fa[p][i] = M::load(ap[i] + off);
+        fb[p][i] = M::load(bp[i] + off);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const bool full = g + PF <= nw;  // wave-uniform
+#pragma unroll
+    for (int p = 0; p < PF; ++p) {
+      Frag av[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        av[i].v = (full || g + p < nw) ? fa[p][i].v : zf.v;
+        b[i].v = use[i] ? fb[p][i].v : alt[i].v;
+      }
+      if constexpr (CUT) {
+        u32x2 ah[4], am[4], al[4], bh[4], bm[4], bl[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          Mma<float>::split3(av[i].v, ah[i], am[i], al[i]);
+          Mma<float>::split3(b[i].v, bh[i], bm[i], bl[i]);
+        }
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) Mma<float>::mma_pp(acc[mi][ni], ah[mi], am[mi], al[mi], bh[ni], bm[ni], bl[ni]);
+      } else {
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < 4; ++ni) M::mma(acc[mi][ni], av[mi], b[ni]);
+      }
+    }
+  }
+  if (a.stamps && threadIdx.x == 0 && L < 512) a.stamps[(STAMP_WGRAD + L) * 16 + 1] = wall_clock64();
+  // fixed-order sum of the four waves' partial blocks, (w0 + w2) + (w1 + w3), through 32 KB of LDS; then wave 0
+  // writes the block's slab row with buffer stores whose out-of-range offsets (padding outputs) the hardware drops
+  if (w >= 2) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) red[w - 2][t][lane] = acc[t >> 2][t & 3];
+  }
+  __syncthreads();
+  if (w < 2) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) acc[t >> 2][t & 3] += red[w][t][lane];
+  }
+  __syncthreads();
+  if (w == 1) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) red[0][t][lane] = acc[t >> 2][t & 3];
+  }
+  __syncthreads();
+  if (w == 0) {
+    const int nout = J.N * J.K + (J.bias ? J.N : 0);  // this job's parameters
+    const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(
+        a.slab + (size_t)split * a.slab_ld + J.out_off, (short)0, nout * 4, 0x00020000);
+    const int kb = J.K + (J.bias ? 1 : 0);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const f32x4 sv = acc[mi][ni] + red[0][mi * 4 + ni][lane];
+        const int k = k0 + ni * 16 + row;
+        const bool wcol = k < J.K;  // weight column (else: the bias column k == K, or padding)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int n = n0 + mi * 16 + grp * 4 + i;
+          // weight (n, k) at n * K + k, bias n at N * K + n; padding rows / columns: an offset past the buffer end
+          const int q = wcol ? n * J.K + k : J.N * J.K + n;
+          const bool ok = (n < J.N) & (k < kb);
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sv[i]), rs_out, ok ? q * 4 : 0x7FFFFFF0, 0, 0);
+        }
+      }
+    if (a.stamps && threadIdx.x == 0 && L < 512) {
+      a.stamps[(STAMP_WGRAD + L) * 16 + 2] = wall_clock64();
+      a.stamps[(STAMP_WGRAD + L) * 16 + 3] = hw_location() + 1;  // (+1: never 0, marks the 3-phase stamp set)
+    }
+  }
+}
+
+// MNIST_AMD_WGRAD_SK_PF: K-steps in flight per wave (2 or 4)
+int wgrad_sk_pf() {
+  static const int v = [] {
+    const char* e = std::getenv("MNIST_AMD_WGRAD_SK_PF");
+    return e && *e == '4' ? 4 : 2;
+  }();
+  return v;
+}
+// MNIST_AMD_WGRAD_SK=1: the split-K-in-workgroup kernel from SK_MIN_B (A/B switch; off until it measures faster)
+bool wgrad_sk_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("MNIST_AMD_WGRAD_SK");
+    return e && *e == '1';
+  }();
+  return on;
+}
+
 // wgrad_kernel keeps ONE ring slot of K-step fragments per wave (the next step's fragments fetched while this
 // one computes: two / four steps ahead measured within noise / 0.3-1.6 % slower on both models).  The
 // LDS-staged weight gradient (wgrad_lds_kernel) is used for the MLP, whose wgrad runs alone on the chip; the
@@ -1289,6 +1465,24 @@ int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab
   // fp32 MLP weight gradient as 3-part bf16 splits from B = 4096 on (MLP fp32 B=8192 -6 %, but B=1024 +6 %:
   // profiles/r5_session1/hsplit2); no effect for bf16 (wg_mma)
   const bool spl = B >= 4096;
+  if (!fuse && B >= SK_MIN_B && wgrad_sk_enabled()) {
+    // split-K-in-workgroup kernel over contiguous batch splits; with a split count that divides over the 8 XCDs,
+    // XCD x takes splits [x * S / 8, (x + 1) * S / 8) -- the batch rows the XCD-contiguous head (xcd_unit) wrote
+    // there (a bijection either way; only the L2 locality depends on the head's mapping)
+    a.xcd_ch = splits % 8 == 0 ? 1 : 0;
+    a.sx = splits / 8;
+    // LeNet fp32: products as 3-part bf16 splits (as wgrad_kernel's wg_mma); MLP fp32 from B = 4096 (as wgrad_lds)
+    const bool cut = std::is_same<Model, MlpModel>::value ? spl : true;
+    const dim3 grid(blk * splits);
+    if (sizeof(T) == 2 && wgrad_sk_pf() == 4) {  // (fp32: 2; at 4 the cut parts spill)
+      if (cut) hipLaunchKernelGGL((wgrad_sk_kernel<T, true, 4>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((wgrad_sk_kernel<T, false, 4>), grid, dim3(256), 0, s, a);
+    } else {
+      if (cut) hipLaunchKernelGGL((wgrad_sk_kernel<T, true, 2>), grid, dim3(256), 0, s, a);
+      else hipLaunchKernelGGL((wgrad_sk_kernel<T, false, 2>), grid, dim3(256), 0, s, a);
+    }
+    return splits;
+  }
   // XCD-aware mapping when the head's row tiling is known and the split count divides over 8 XCDs
   // (steps per row chunk xcd_ch / KC must be a power of two: the kernels map steps to rows by shift and mask)
   if (!fuse && xcd_ch > 0 && xcd_ch % KC == 0 && ((xcd_ch / KC) & (xcd_ch / KC - 1)) == 0 && splits % 8 == 0) {

@@ -187,3 +187,6 @@ int model_conv_params(ModelKind m);
 // LeNet: conv_params (phase 0 = FC head); MLP: the layer-2 weight (phase 0 = layers 2+3)
 int model_phase_split(ModelKind m);
 int model_pack_size(ModelKind m);
+// First parameter of FC weight-gradient job j (0: first FC layer, 1: second, 2: third; 3: nparam): the
+// launch_head_wgrad job-mask bit j computes exactly the gradients [model_job_begin(j), model_job_begin(j + 1))
+int model_job_begin(ModelKind m, int job);

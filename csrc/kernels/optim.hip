@@ -306,6 +306,16 @@ int model_nparam(ModelKind m) { return m == ModelKind::MLP ? MlpModel::NPARAM : 
 int model_conv_params(ModelKind m) { return m == ModelKind::MLP ? 0 : LenetModel::CONV_PARAMS; }
 int model_phase_split(ModelKind m) { return m == ModelKind::MLP ? MlpModel::Head::W2 : LenetModel::CONV_PARAMS; }
 int model_pack_size(ModelKind m) { return m == ModelKind::MLP ? MlpModel::PACK_SIZE : LenetModel::PACK_SIZE; }
+int model_job_begin(ModelKind m, int job) {
+  if (m == ModelKind::MLP) {
+    using H = MlpModel::Head;
+    const int b[4] = {H::W1, H::W2, H::W3, MlpModel::NPARAM};
+    return b[std::min(std::max(job, 0), 3)];
+  }
+  using H = LenetModel::Head;
+  const int b[4] = {H::W1, H::W2, H::W3, LenetModel::NPARAM};
+  return b[std::min(std::max(job, 0), 3)];
+}
 
 void launch_reduce_sgd(ModelKind m, DType t, const float* slab_a, int lda, int na, const float* slab_b, int ldb,
                        int nb, int split, int p0, int n, float scale, float* params, float* grad, float* mom,

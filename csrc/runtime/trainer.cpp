@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <functional>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
@@ -97,11 +98,10 @@ Trainer::Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const
   max_conv_slabs_ = model_ == ModelKind::LENET ? lenet_conv_bwd_max_blocks(batch_, 0) : 0;
   concurrent_ = concurrent_mode() != 0;
   const int ps = model_phase_split(model_);  // default buckets: one per backward phase (see Plan)
-  buckets_.push_back({ps, nparam_, 0});
-  buckets_.push_back({0, ps, 1});
+  set_buckets({{ps, nparam_, 0}, {0, ps, 1}});
   HIP_CHECK(hipStreamCreateWithFlags(&comm_stream_, hipStreamNonBlocking));
   HIP_CHECK(hipStreamCreateWithFlags(&aux_stream_, hipStreamNonBlocking));
-  events_.resize(6);
+  events_.resize(6 + MAX_GROUPS);  // [6 + g]: group g reduced (SPLIT)
   for (auto& e : events_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIP_CHECK(hipMalloc(&zero_counter_, 2 * sizeof(int32_t)));
   HIP_CHECK(hipMemset(zero_counter_, 0, 2 * sizeof(int32_t)));
@@ -114,7 +114,7 @@ void Trainer::destroy() {
   invalidate();
   // after an abort a replay may still sit in a collective that never completes: its graph execs (leaked by
   // invalidate), streams and events stay alive rather than being destroyed under it (the process is failing)
-  if (comm_ && comm_->aborted()) return;
+  if (comm_aborted()) return;
   sync_own_streams();
   for (auto& e : events_) if (e) hipEventDestroy(e);
   events_.clear();
@@ -134,10 +134,13 @@ void Trainer::release() {
   // teardown order (DistContext.finalize): every graph that captured a collective is dropped -- after its
   // replays drained -- before the communicator is destroyed, then the communicator reference is released
   invalidate();
-  if (comm_ && !comm_->aborted()) {
+  if (!comm_aborted()) {
     (void)hipStreamSynchronize(comm_stream_);
     (void)hipStreamSynchronize(aux_stream_);
   }
+  // remembered past the reset below: destroy() / sync_own_streams() must still see that a replay may be stuck in an
+  // aborted collective (advisor, round 5: after close() -> release() they found comm_ null and synchronised anyway)
+  if (comm_ && comm_->aborted()) comm_was_aborted_ = true;
   comm_.reset();
   oneshot_.reset();
   ov_fc_.reset();
@@ -152,6 +155,117 @@ int Trainer::fc_splits_for(int B) const {
   int splits = std::max(1, std::min(fc_splits_, Bp / KC));
   const int rlen = ((Bp + splits - 1) / splits + KC - 1) / KC * KC;
   return (Bp + rlen - 1) / rlen;
+}
+
+void Trainer::set_buckets(const std::vector<Bucket>& b) {
+  // groups: contiguous ranges in backward-ready order (group 0 ends at nparam, each next one ends where the previous
+  // starts, the last starts at 0), every boundary a unit boundary (model_job_begin; LeNet: the conv range is the
+  // last group on its own)
+  if (b.empty()) throw std::invalid_argument("set_buckets: no buckets");
+  int ng = 0;
+  for (const Bucket& x : b) {
+    if (x.p0 < 0 || x.p1 > nparam_ || x.p0 >= x.p1) throw std::invalid_argument("set_buckets: bad bucket range");
+    if (x.phase < 0 || x.phase >= MAX_GROUPS) throw std::invalid_argument("set_buckets: group index out of range");
+    ng = std::max(ng, x.phase + 1);
+  }
+  std::vector<int> bounds = {0, nparam_};
+  for (int j = 0; j < 4; ++j) bounds.push_back(model_job_begin(model_, j));
+  const int cp = model_conv_params(model_);
+  auto on_bound = [&](int p) { return std::find(bounds.begin(), bounds.end(), p) != bounds.end(); };
+  int end = nparam_;
+  for (int g = 0; g < ng; ++g) {
+    std::vector<Bucket> mine;
+    for (const Bucket& x : b) if (x.phase == g) mine.push_back(x);
+    if (mine.empty()) throw std::invalid_argument("set_buckets: empty bucket group " + std::to_string(g));
+    std::sort(mine.begin(), mine.end(), [](const Bucket& u, const Bucket& v) { return u.p0 < v.p0; });
+    for (size_t i = 1; i < mine.size(); ++i)
+      if (mine[i].p0 != mine[i - 1].p1) throw std::invalid_argument("set_buckets: group " + std::to_string(g) + " is not contiguous");
+    const int p0 = mine.front().p0, p1 = mine.back().p1;
+    if (p1 != end) throw std::invalid_argument("set_buckets: groups must tile [0, nparam) in backward-ready order");
+    if (!on_bound(p0)) throw std::invalid_argument("set_buckets: group boundary " + std::to_string(p0) + " splits a layer");
+    if (cp > 0 && p0 < cp && p1 > cp) throw std::invalid_argument("set_buckets: a group mixes conv and FC gradients");
+    end = p0;
+  }
+  if (end != 0) throw std::invalid_argument("set_buckets: groups must cover [0, nparam)");
+  buckets_ = b;
+  // graphs are cached per bucket plan (schedule_key), so a calibration can interleave several plans
+  auto it = std::find_if(bucket_plans_.begin(), bucket_plans_.end(), [&](const std::vector<Bucket>& v) {
+    return v.size() == b.size() && std::equal(v.begin(), v.end(), b.begin(), [](const Bucket& x, const Bucket& y) {
+             return x.p0 == y.p0 && x.p1 == y.p1 && x.phase == y.phase;
+           });
+  });
+  if (it == bucket_plans_.end()) {
+    if (bucket_plans_.size() >= 255) throw std::invalid_argument("set_buckets: too many distinct bucket plans");
+    bucket_plans_.push_back(b);
+    it = bucket_plans_.end() - 1;
+  }
+  bucket_id_ = static_cast<int>(it - bucket_plans_.begin());
+}
+
+std::vector<Trainer::Group> Trainer::groups() const {
+  int ng = 0;
+  for (const Bucket& x : buckets_) ng = std::max(ng, x.phase + 1);
+  std::vector<Group> out(ng, Group{nparam_, 0, 0});
+  for (const Bucket& x : buckets_) {
+    out[x.phase].p0 = std::min(out[x.phase].p0, x.p0);
+    out[x.phase].p1 = std::max(out[x.phase].p1, x.p1);
+  }
+  for (Group& g : out)
+    for (int j = 0; j < 3; ++j)
+      if (model_job_begin(model_, j) >= g.p0 && model_job_begin(model_, j + 1) <= g.p1) g.mask |= 1 << j;
+  return out;
+}
+
+std::vector<double> Trainer::time_units(int iters, int warmup, uintptr_t stream) {
+  hipStream_t s = S(stream);
+  const int B = batch_;
+  const HeadBuffers hb = head_buffers(ptr<float>(p_.metrics));
+  const float scale = 1.0f / float(B);
+  const int hrows = head_rows_per_block(model_, dtype_, batch_);
+  float* g = ptr<float>(p_.grad);
+  // (the operand buffers hold the last step's activations / gradients: the values do not matter for timing,
+  //  grad is overwritten -- callers save and restore training state around this)
+  std::vector<std::function<void()>> units;
+  for (int j = 2; j >= 0; --j)  // ready order: the last FC layer first
+    units.push_back([=] {
+      const int sp = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s, hrows,
+                                       nullptr, 1 << j);
+      launch_reduce(ptr<const float>(p_.slab_fc), nparam_, sp, model_job_begin(model_, j), model_job_begin(model_, j + 1),
+                    scale, g, s);
+    });
+  units.push_back([=] {
+    const int sp = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s, hrows, nullptr, 7);
+    launch_reduce(ptr<const float>(p_.slab_fc), nparam_, sp, model_job_begin(model_, 0), nparam_, scale, g, s);
+  });
+  if (model_ == ModelKind::LENET)
+    units.push_back([=] {
+      int nslab = 0;
+      launch_lenet_conv_bwd(dtype_, batch_ref(B), conv_buffers(B), &nslab, s, bwd_blocks_);
+      launch_reduce(ptr<const float>(p_.slab_conv), model_conv_params(model_), nslab, 0, model_conv_params(model_), scale, g, s);
+    });
+  hipEvent_t e0, e1;
+  HIP_CHECK(hipEventCreate(&e0));
+  HIP_CHECK(hipEventCreate(&e1));
+  std::vector<double> out;
+  for (auto& u : units) {
+    for (int i = 0; i < warmup; ++i) u();
+    std::vector<float> ts;
+    for (int i = 0; i < iters; ++i) {
+      HIP_CHECK(hipEventRecord(e0, s));
+      u();
+      HIP_CHECK(hipEventRecord(e1, s));
+      HIP_CHECK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+      ts.push_back(ms);
+    }
+    HIP_CHECK(hipGetLastError());
+    std::sort(ts.begin(), ts.end());
+    out.push_back(ts.empty() ? 0.0 : 1000.0 * ts[ts.size() / 2]);
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  return out;
 }
 
 std::vector<std::string> Trainer::graph_nodes() const {
@@ -194,7 +308,7 @@ void Trainer::sync_own_streams() {
   // a replay of a cached graph may still be running on the stream it was launched on and on its forked
   // aux / comm branches: drain those (not the whole device, which would also wait on other trainers'
   // and other libraries' work).  After an abort a collective may never complete: nothing is waited for.
-  if (comm_ && comm_->aborted()) return;
+  if (comm_aborted()) return;
   if (last_stream_) (void)hipStreamSynchronize(last_stream_);
   (void)hipStreamSynchronize(aux_stream_);
   (void)hipStreamSynchronize(comm_stream_);
@@ -202,7 +316,7 @@ void Trainer::sync_own_streams() {
 
 void Trainer::invalidate() {
   if (graphs_.empty()) return;
-  if (comm_ && comm_->aborted()) {
+  if (comm_aborted()) {
     // a replay may be stuck in an aborted collective: leak the graph execs (as RcclComm::time_all_reduce
     // does) instead of destroying them under it
     graphs_.clear();
@@ -357,9 +471,10 @@ std::vector<Bucket> Trainer::issued_collectives() const {
     const int cp = model_conv_params(model_);
     return {{cp, nparam_, 0}, {0, cp, 1}};
   }
-  if (plan_ == Plan::SPLIT) {
-    for (const Bucket& b : buckets_) if (b.phase == 0) out.push_back(b);
-    for (const Bucket& b : buckets_) if (b.phase != 0) out.push_back(b);
+  if (plan_ == Plan::SPLIT) {  // group by group in ready order (LeNet: the conv group after the FC ones)
+    const int ng = static_cast<int>(groups().size());
+    for (int g = 0; g < ng; ++g)
+      for (const Bucket& b : buckets_) if (b.phase == g) out.push_back(b);
     return out;
   }
   return coalesced_buckets();
@@ -415,6 +530,10 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
       // like the local schedule: the FC branch is joined by the next step's head inside a multi-step graph
       if (defer_join) aux_pending_ = true;
       else HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));
+      return;
+    }
+    if (comm && plan_ == Plan::SPLIT) {
+      launch_lenet_split_tail(B, nslab, s, hb, hrows);
       return;
     }
     if (comm) {
@@ -500,13 +619,12 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
 // Comm stream: wait for phase `phase`'s reduced gradients, all-reduce its buckets, then update that
 // phase's parameter range (and operand images) with the 1/W average folded in.  Everything stays on the
 // comm stream, so no other stream waits on an event recorded behind a captured RCCL call mid-step.
-void Trainer::comm_phase(int phase, hipEvent_t ready, bool bump) {
+void Trainer::comm_phase(int g, hipEvent_t ready, bool bump) {
   HIP_CHECK(hipStreamWaitEvent(comm_stream_, ready, 0));
-  all_reduce(buckets_, phase, comm_stream_);
-  const int ps = model_phase_split(model_);
-  const int p0 = phase == 0 ? ps : 0, p1 = phase == 0 ? nparam_ : ps;
+  all_reduce(buckets_, g, comm_stream_);
+  const Group gr = groups().at(g);
   launch_sgd_pack_range(model_, dtype_, ptr<float>(p_.params), ptr<const float>(p_.grad), ptr<float>(p_.mom),
-                        ptr<void>(p_.pack), p0, p1, lr_, momentum_, 1.0f / float(world_),
+                        ptr<void>(p_.pack), gr.p0, gr.p1, lr_, momentum_, 1.0f / float(world_),
                         bump ? ptr<int32_t>(p_.step) : nullptr, comm_stream_, dp_skip());
   post_launch(comm_stream_);
 }
@@ -530,18 +648,18 @@ void Trainer::launch_mlp_comm_tail(int B, hipStream_t s, const HeadBuffers& hb, 
     post_launch(s);
     return;
   }
-  int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, slab, nparam_, s, hrows, nullptr, 6);
-  post_launch(s);
-  launch_reduce(slab, nparam_, splits, ps, nparam_, scale, g, s);
-  post_launch(s);
-  HIP_CHECK(hipEventRecord(events_[1], s));
-  comm_phase(0, events_[1], false);
-  splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, slab, nparam_, s, hrows, nullptr, 1);
-  post_launch(s);
-  launch_reduce(slab, nparam_, splits, 0, ps, scale, g, s);
-  post_launch(s);
-  HIP_CHECK(hipEventRecord(events_[2], s));
-  comm_phase(1, events_[2], true);
+  // SPLIT: the bucket groups in ready order (default: layers 2+3, then layer 1), each one's weight gradient and
+  // reduce on the main stream, its buckets + update on the comm stream beside the next group's weight gradient
+  (void)ps;
+  const std::vector<Group> gs = groups();
+  for (size_t k = 0; k < gs.size(); ++k) {
+    const int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, slab, nparam_, s, hrows, nullptr, gs[k].mask);
+    post_launch(s);
+    launch_reduce(slab, nparam_, splits, gs[k].p0, gs[k].p1, scale, g, s);
+    post_launch(s);
+    HIP_CHECK(hipEventRecord(events_[6 + k], s));
+    comm_phase(static_cast<int>(k), events_[6 + k], k + 1 == gs.size());
+  }
   HIP_CHECK(hipEventRecord(events_[0], comm_stream_));
   HIP_CHECK(hipStreamWaitEvent(s, events_[0], 0));
 }
@@ -566,21 +684,47 @@ void Trainer::launch_lenet_comm_tail(int B, int nslab, int splits, hipStream_t s
     post_launch(s);
     return;
   }
-  // SPLIT: the comm stream sends the FC buckets as soon as reduce(FC) is done (beside conv_bwd) and
-  // updates the FC range right behind them; the conv buckets follow reduce(conv), then the conv update
-  // (+ step bump).  (A graph where another stream waits on an event recorded behind a captured RCCL call
-  // made hipStreamEndCapture segfault on ROCm 7.0's runtime, so only the main stream consumes the comm
-  // stream's completion, once, at the end of the step.)
-  trace("split: comm AR(FC) + update(FC)");
-  comm_phase(0, events_[5], false);
+  throw std::logic_error("launch_lenet_comm_tail: JOIN only (SPLIT: launch_lenet_split_tail)");
+}
+
+// SPLIT: the FC bucket groups in ready order (default: ONE group, the whole FC head; a link-aware plan: e.g.
+// fc3 + fc2, then fc1), each one's weight gradient (its job mask) and reduce on the aux stream beside conv_bwd;
+// the comm stream sends a group's buckets as soon as it is reduced and updates its range right behind them; the
+// conv buckets follow reduce(conv), then the conv update (+ step bump).  Per-parameter arithmetic is that of the
+// one-group form (same tiles, splits, reduce tree), so every bucket plan gives bitwise-identical parameters.
+// (A graph where another stream waits on an event recorded behind a captured RCCL call made hipStreamEndCapture
+// segfault on ROCm 7.0's runtime, so only the main stream consumes the comm stream's completion, once, at the
+// end of the step.)
+void Trainer::launch_lenet_split_tail(int B, int nslab, hipStream_t s, const HeadBuffers& hb, int hrows) {
+  const float scale = 1.0f / float(B);
+  const int cp = model_conv_params(model_);
+  float* g = ptr<float>(p_.grad);
+  const std::vector<Group> gs = groups();
+  int conv_g = -1;
+  for (size_t k = 0; k < gs.size(); ++k) {
+    if (gs[k].mask == 0) {  // the conv group (set_buckets: the last one)
+      conv_g = static_cast<int>(k);
+      continue;
+    }
+    trace("split: FC group wgrad + reduce (aux), AR + update (comm)");
+    const int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, aux_stream_,
+                                         hrows, nullptr, gs[k].mask);
+    post_launch(aux_stream_);
+    launch_reduce(ptr<const float>(p_.slab_fc), nparam_, splits, gs[k].p0, gs[k].p1, scale, g, aux_stream_);
+    post_launch(aux_stream_);
+    HIP_CHECK(hipEventRecord(events_[6 + k], aux_stream_));
+    comm_phase(static_cast<int>(k), events_[6 + k], false);
+  }
+  if (conv_g < 0) throw std::logic_error("launch_lenet_split_tail: no conv bucket group");
   trace("split: reduce(conv)");
   launch_reduce(ptr<const float>(p_.slab_conv), cp, nslab, 0, cp, scale, g, s);
   post_launch(s);
   HIP_CHECK(hipEventRecord(events_[1], s));
   trace("split: comm AR(conv) + update(conv)");
-  comm_phase(1, events_[1], true);
+  comm_phase(conv_g, events_[1], true);
   HIP_CHECK(hipEventRecord(events_[0], comm_stream_));
   HIP_CHECK(hipStreamWaitEvent(s, events_[0], 0));
+  // the FC branch ended with an event the comm stream waited for, and the comm stream is joined above
   trace("split: done");
 }
 
@@ -682,7 +826,8 @@ void Trainer::drop(GraphSlot& g) {
 // different cached graph instead of re-capturing, so a calibration can interleave the candidates'
 // replays back to back; anything that changes the kernels' arguments clears the cache (invalidate).
 uint64_t Trainer::schedule_key(int nsteps) const {
-  return (static_cast<uint64_t>(nsteps) << 40) | (static_cast<uint64_t>(bwd_blocks_) << 8) |
+  return (static_cast<uint64_t>(nsteps) << 40) | (static_cast<uint64_t>(bucket_id_ & 255) << 32) |
+         (static_cast<uint64_t>(bwd_blocks_) << 8) |
          (static_cast<uint64_t>(fwd_head_) << 4) | (static_cast<uint64_t>(comm_enabled_) << 3) | (static_cast<uint64_t>(concurrent_) << 2) |
          static_cast<uint64_t>(plan_);
 }

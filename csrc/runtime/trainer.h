@@ -29,7 +29,10 @@ struct TrainerPtrs {
 };
 
 // A gradient bucket = contiguous range of the flat grad slab, all-reduced as one RCCL call as
-// soon as the backward phase that produces it has been reduced (phase 0 = FC head, 1 = conv).
+// soon as the bucket GROUP (`phase`) that holds it has been reduced.  Groups are numbered in backward-ready
+// order and each covers whole gradient-producing units (model_job_begin: the FC layers, last to first; LeNet's
+// conv range [0, conv_params) is always the last group): the default plan is two groups (LeNet FC | conv, MLP
+// layers 2+3 | layer 1); a link-aware plan (parallel/ddp.py choose_bucket_groups) cuts the FC head into more.
 struct Bucket {
   int p0, p1, phase;
 };
@@ -52,6 +55,7 @@ enum class Plan : int { JOIN = 0, SPLIT = 1, OVERLAP = 2 };
 
 class Trainer {
  public:
+  static constexpr int MAX_GROUPS = 8;  // bucket groups of a plan (Bucket::phase < MAX_GROUPS)
   // LeNet training steps of B <= XB_MAX_B rows hand conv_bwd batch-ordered pixel rows (TrainerPtrs::xb)
   static constexpr int XB_MAX_B = 2048;
   Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const TrainerPtrs& p);
@@ -76,8 +80,18 @@ class Trainer {
   void set_world(int w) { world_ = w; invalidate(); }
   void set_optimizer(float lr, float momentum) { lr_ = lr; momentum_ = momentum; invalidate(); }
   void set_dropout(float p, uint32_t seed) { drop_p_ = p; seed_ = seed; invalidate(); }
-  void set_buckets(const std::vector<Bucket>& b) { buckets_ = b; invalidate(); }
+  // validated (contiguous groups in ready order on unit boundaries); graphs are cached per bucket plan
+  void set_buckets(const std::vector<Bucket>& b);
   std::vector<Bucket> buckets() const { return buckets_; }
+  // bucket groups in ready order: parameter range + the FC weight-gradient jobs that produce it (0: conv)
+  struct Group {
+    int p0, p1, mask;
+  };
+  std::vector<Group> groups() const;
+  // Per-unit backward cost (us, median of `iters` eager launches on `stream` after `warmup`): the FC units in
+  // ready order (each its own weight-gradient launch + reduce; LeNet fc3, fc2, fc1 / MLP layer 3, 2, 1), then all
+  // FC units as ONE launch + reduce, then (LeNet) conv_bwd + its reduce.  Input of the bucket-plan model.
+  std::vector<double> time_units(int iters, int warmup, uintptr_t stream);
   void set_plan(int p) {
     if (p < 0 || p > 2) throw std::invalid_argument("plan must be 0 (join), 1 (split) or 2 (overlap)");
     if (p == 2 && (model_ != ModelKind::LENET || !has_overlap()))
@@ -170,12 +184,17 @@ class Trainer {
   // wgrad + FC update) un-joined at the end of the step; the NEXT step's head waits for it instead.
   void launch_step(int B, hipStream_t s, bool defer_join = false);
   void launch_lenet_comm_tail(int B, int nslab, int splits, hipStream_t s);
+  // Plan::SPLIT (LeNet) after the fork: the FC groups' weight gradients + reduces on the aux stream, each group's
+  // buckets and update on the comm stream as soon as it is reduced; then the conv group behind conv_bwd
+  void launch_lenet_split_tail(int B, int nslab, hipStream_t s, const HeadBuffers& hb, int hrows);
   // Plan::OVERLAP after the fork (conv_bwd launched on s, nothing yet on aux); returns with the aux branch open
   void launch_lenet_overlap(int B, int nslab, hipStream_t s, const HeadBuffers& hb, int hrows);
   void launch_mlp_comm_tail(int B, hipStream_t s, const HeadBuffers& hb, int hrows);
-  // comm stream: wait for `ready`, all-reduce phase `phase`'s buckets, update its parameter range
-  void comm_phase(int phase, hipEvent_t ready, bool bump);
+  // comm stream: wait for `ready`, all-reduce group `g`'s buckets, update its parameter range
+  void comm_phase(int g, hipEvent_t ready, bool bump);
   bool use_comm() const { return (comm_ || oneshot_ || has_overlap()) && comm_enabled_; }
+  // the attached communicator was aborted (also after release() dropped it)
+  bool comm_aborted() const { return comm_was_aborted_ || (comm_ && comm_->aborted()); }
   // the update kernels' skip word: the one-shot data plane's latched error (oneshot.hip), none with RCCL
   const uint32_t* dp_skip() const { return oneshot_ ? oneshot_->err_word() : nullptr; }
   void sync_own_streams();
@@ -203,6 +222,7 @@ class Trainer {
   bool fwd_head_ = true;
   bool comm_enabled_ = true;
   bool destroyed_ = false;  // destroy() ran
+  bool comm_was_aborted_ = false;  // release() dropped an aborted communicator
   hipStream_t last_stream_ = nullptr;  // stream of the last graph launch / capture (drained by invalidate)
   int bwd_blocks_ = 0;
   int max_conv_slabs_ = 0;  // rows of the conv slab (lenet_conv_bwd_max_blocks(batch) at the default target)
@@ -210,6 +230,8 @@ class Trainer {
   std::shared_ptr<OneShotAllReduce> oneshot_;
   std::shared_ptr<OneShotAllReduce> ov_fc_, ov_conv_;
   std::vector<Bucket> buckets_;
+  int bucket_id_ = 0;                              // index of buckets_ in bucket_plans_ (graph-cache key)
+  std::vector<std::vector<Bucket>> bucket_plans_;  // every bucket plan installed so far
   hipStream_t comm_stream_ = nullptr;
   hipStream_t aux_stream_ = nullptr;  // concurrent FC wgrad branch (fork/join inside the step graph)
   std::vector<hipEvent_t> events_;

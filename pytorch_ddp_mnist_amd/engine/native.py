@@ -19,10 +19,12 @@ allocator, never re-allocated per step) and exposes epoch-level operations:
 """
 from __future__ import annotations
 
+import atexit
 import math
 import os
 import sys
 import time
+import weakref
 from dataclasses import dataclass
 from typing import Dict, Optional, Tuple
 
@@ -38,6 +40,27 @@ PLANS = {"join": 0, "split": 1, "overlap": 2}
 # in-kernel span is ~4.5 us at world 1 (profiles/r5_session1/prof1/oneshot_lat.txt)
 STANDALONE_CALLS_PER_GRAPH = 8
 
+# Every live trainer is closed (graphs -> streams / events / device counters, NativeTrainer.close) by an atexit hook
+# when a script ends without DistContext.finalize: Python runs atexit handlers in reverse registration order, and this
+# one is registered after `import torch`, so it runs before torch's own exit handlers and long before the C++ static
+# destructors that tear the HIP runtime down -- the native teardown never runs against a dead runtime (the failure
+# mode suspected behind the round-4 rank exit 139; PARITY.md §5.3).
+_LIVE_TRAINERS: "weakref.WeakSet" = weakref.WeakSet()
+
+
+def _close_live_trainers() -> None:
+    for tr in list(_LIVE_TRAINERS):
+        if getattr(tr, "comm", None) is not None or getattr(tr, "oneshot", None) is not None:
+            continue  # collectives attached: DistContext.finalize's bounded teardown owns it (a dead peer must not
+            #           turn the exit of a failing rank into a wait on a collective that never completes)
+        try:
+            tr.close()
+        except Exception as e:  # teardown must not raise at exit; report and go on
+            print(f"[mnist_amd] trainer teardown at exit: {e}", file=sys.stderr, flush=True)
+
+
+atexit.register(_close_live_trainers)
+
 
 def resolve_plan(name: Optional[str]) -> Optional[str]:
     """CLI ``--plan`` value -> the plan to pin, or None for the start-up calibration.
@@ -51,6 +74,17 @@ def resolve_plan(name: Optional[str]) -> Optional[str]:
     if name not in PLANS:
         raise ValueError(f"unknown step plan {name!r} (choices: auto, fixed, {', '.join(sorted(PLANS))})")
     return name
+
+
+def split_allowed(world: int) -> bool:
+    """SPLIT-family plans (per-group collectives on a comm stream beside the backward) are calibration candidates at
+    world 1 (tests, --comm-world1) and, at world >= 2, only with ``MNIST_AMD_SPLIT=1``: they have not run across real
+    GPUs yet, and a replay that hangs at world >= 2 can only end in the calibration watchdog's abort, while JOIN is
+    the schedule every multi-rank run can fall back on (advisor, round 5).  ``MNIST_AMD_NO_SPLIT=1`` removes them
+    everywhere."""
+    if os.environ.get("MNIST_AMD_NO_SPLIT", "0") == "1":
+        return False
+    return world <= 1 or os.environ.get("MNIST_AMD_SPLIT", "0") == "1"
 
 
 def forced_plan() -> Optional[str]:
@@ -230,6 +264,8 @@ class NativeTrainer:
         self.rt = C.Trainer(mid, did, self.batch, self.ld_b, fc_splits, P)
         self.rt.set_optimizer(float(lr), float(momentum))
         self.rt.set_dropout(float(dropout), int(seed) & 0xFFFFFFFF)
+        self._base_buckets = [(b.p0, b.p1, b.phase) for b in self.rt.buckets()]  # the native default (2 groups)
+        _LIVE_TRAINERS.add(self)
         self.stream = torch.cuda.Stream(device=dev)
         self.world = 1
         self.comm = None
@@ -320,13 +356,61 @@ class NativeTrainer:
         coll = [(b.p0, b.p1) for b in self.rt.issued_collectives()]
         dp = self.comm is not None or self.oneshot is not None or self.overlap is not None
         ov = self.plan == "overlap"
+        groups = {(b.p0, b.p1): b.phase for b in self.rt.buckets()}
         return {"plan": self.plan if dp else ("local" if self.rt.concurrent else "local-serial"),
                 "allreduce": "oneshot" if (self.oneshot is not None or ov) else ("rccl" if self.comm is not None else None),
                 "conv_bwd_grid": self.rt.bwd_grid if self.model_name == "lenet5" else None,
-                "collectives": [{"params": [a, b], "bytes": 4 * (b - a)} for a, b in coll]}
+                "collectives": [{"params": [a, b], "bytes": 4 * (b - a),
+                                 **({"group": groups[(a, b)]} if self.plan == "split" and (a, b) in groups else {})}
+                                for a, b in coll]}
 
     def set_buckets(self, ranges) -> None:
+        """Install a bucket plan (ranges (p0, p1, group), groups in backward-ready order: csrc Trainer::set_buckets)
+        as the trainer's base plan; calibration candidates that carry their own ``buckets`` switch to theirs."""
+        self._base_buckets = [tuple(int(v) for v in r) for r in ranges]
+        self._install_buckets(self._base_buckets)
+
+    def _install_buckets(self, ranges) -> None:
         self.rt.set_buckets([self.C.Bucket(int(a), int(b), int(ph)) for a, b, ph in ranges])
+
+    def current_buckets(self):
+        return [(b.p0, b.p1, b.phase) for b in self.rt.buckets()]
+
+    def bucket_model(self, reduce_max=None, iters: int = 24, warmup: int = 4) -> dict:
+        """Inputs of the link-aware bucket plan (parallel/ddp.py choose_bucket_groups), measured on this job:
+        the RCCL all-reduce latency at LATENCY_SWEEP_BYTES on the real communicator (standalone collectives, 8 per
+        graph, rank-max median) and each gradient-producing unit's backward cost (Trainer::time_units, rank-max).
+        Collective: every rank calls it at the same point.  Gradients and slabs are scratch here (restored)."""
+        from ..parallel.ddp import LATENCY_SWEEP_BYTES, LatencyCurve, choose_bucket_groups, fc_unit_count
+        if self.comm is None:
+            raise RuntimeError("bucket_model: needs an RCCL communicator")
+        rmax = reduce_max if reduce_max is not None else (lambda v: v)
+        pts = []
+        nmax = max(LATENCY_SWEEP_BYTES) // 4
+        buf = torch.zeros(nmax, dtype=torch.float32, device=self.device)
+        self._sync_in()
+        for nb in LATENCY_SWEEP_BYTES:
+            try:
+                ts = self.comm.time_all_reduce(buf.data_ptr(), nb // 4, warmup, iters, self.stream.cuda_stream,
+                                               comm_timeout(), per_graph=STANDALONE_CALLS_PER_GRAPH)
+            except RuntimeError as e:
+                self.comm.abort()
+                raise CollectiveError(f"rank {self.comm.rank}: {e} (communicator aborted)") from e
+            ts = sorted(ts)
+            pts.append((nb, rmax(ts[len(ts) // 2] * 1000.0)))
+        lat = LatencyCurve(pts)
+        saved = self.grad.clone()
+        with torch.cuda.stream(self.stream):
+            us = [rmax(float(v)) for v in self.rt.time_units(iters, warmup, self.stream.cuda_stream)]
+            self.grad.copy_(saved)
+        self.synchronize()
+        nfc = fc_unit_count(self.model_name)
+        unit_us, fc_all = us[:nfc], us[nfc]
+        main = us[nfc + 1] if len(us) > nfc + 1 else 0.0
+        ranked = choose_bucket_groups(self.model_name, lat, unit_us, fc_all, main)
+        return {"latency_us": lat.as_dict(), "unit_us": [round(v, 2) for v in unit_us], "fc_all_us": round(fc_all, 2),
+                "main_us": round(main, 2),
+                "ranked": [{"groups": g, "modelled_us": round(t, 2)} for g, t in ranked], "_ranked": ranked}
 
     def broadcast_params(self, root: int = 0) -> None:
         """DDP construction semantics: every rank starts from rank 0's parameters (over RCCL, or over the
@@ -387,7 +471,8 @@ class NativeTrainer:
     def current_schedule(self) -> dict:
         """The installed schedule as a complete :meth:`apply_plan` candidate."""
         return {"plan": self.plan, "bwd_blocks": int(self.rt.bwd_blocks) if self.model_name == "lenet5" else 0,
-                "concurrent": bool(self.rt.concurrent), "fwd_head": bool(self.rt.fwd_head)}
+                "concurrent": bool(self.rt.concurrent), "fwd_head": bool(self.rt.fwd_head),
+                "buckets": self.current_buckets()}
 
     def apply_plan(self, cfg: dict) -> None:
         """Install one candidate of :meth:`autotune_plan` ({plan, bwd_blocks, concurrent, fwd_head, comm}).
@@ -397,6 +482,7 @@ class NativeTrainer:
         self.rt.comm_enabled = bool(cfg.get("comm", True))
         self.rt.set_concurrent(bool(cfg.get("concurrent", True)))
         self.rt.set_fwd_head(bool(cfg.get("fwd_head", True)))
+        self._install_buckets(cfg.get("buckets") or self._base_buckets)
         self.set_plan(cfg.get("plan", "join"), int(cfg.get("bwd_blocks", 0)))
 
     def time_schedules(self, candidates: Dict[str, dict], iters: int = 48, warmup: int = 8,
@@ -536,9 +622,10 @@ class NativeTrainer:
         ``exposed_comm_ms`` is measured against the local schedule with the chosen plan's fwd_head /
         conv_bwd-grid settings and the faster of the concurrent / serial single-GPU branch.
         """
-        from ..parallel.ddp import (choose_plan, default_plan_candidates, local_plan_candidates,
-                                    mlp_plan_candidates)
+        from ..parallel.ddp import (bucket_plan_candidates, choose_plan, default_plan_candidates,
+                                    local_plan_candidates, mlp_plan_candidates)
         forced = forced_plan()
+        bmodel = None
         dp = self.comm is not None or self.oneshot is not None  # a gradient data plane is attached
         ovl = dp and self.overlap is not None and self.model_name == "lenet5"  # + the one-shot OVERLAP plan
         if dp and forced:
@@ -551,8 +638,14 @@ class NativeTrainer:
                     candidates = default_plan_candidates(self.C.conv_bwd_blocks(self.batch), ncu)
                 else:
                     candidates = mlp_plan_candidates()
-                if self.world > 1 and os.environ.get("MNIST_AMD_NO_SPLIT", "0") == "1":
+                if not split_allowed(self.world):
                     candidates = {k: v for k, v in candidates.items() if v.get("plan", "join") == "join"}
+                elif self.comm is not None and self.oneshot is None and os.environ.get("MNIST_AMD_BUCKET_MODEL", "1") != "0":
+                    # link-aware bucket groups: the modelled best plan and the best multi-bucket plan join the
+                    # candidates (parallel/ddp.py choose_bucket_groups; inputs measured on this communicator)
+                    bmodel = self.bucket_model(reduce_max=reduce_max)
+                    candidates.update(bucket_plan_candidates(self.model_name, bmodel.pop("_ranked"),
+                                                             base=candidates.get("split")))
                 if ovl:
                     candidates["overlap"] = dict(plan="overlap")
             elif self.model_name == "lenet5":
@@ -581,6 +674,8 @@ class NativeTrainer:
                "steps_per_replay": self.last_timing["graph_steps"], "interleaved": True}
         if self.capture_failures:
             out["capture_failures"] = self.capture_failures
+        if bmodel is not None:
+            out["bucket_model"] = bmodel
         if extra and any(k in timings for k in extra):
             local = min(timings[k] for k in extra if k in timings)
             out["nocomm_ms"] = round(local, 4)
@@ -850,6 +945,21 @@ class NativeTrainer:
 
     def _oneshot_instances(self):
         return ([self.oneshot] if self.oneshot is not None else []) + list(self.overlap or ())
+
+    def agree_oneshot(self, reduce_max) -> None:
+        """Collective end-of-run check of the one-shot data plane: a latched failure is one-sided (a late peer that
+        arrives after another rank timed out still finds every flag raised, sums and updates), so before a
+        successful return every rank reports its latch over the control plane (``reduce_max``, e.g. a gloo MAX
+        all-reduce) and ALL ranks raise :class:`CollectiveError` if any rank failed (advisor, round 5).  No-op
+        without one-shot instances.  Collective: every rank calls it at the same point."""
+        insts = self._oneshot_instances()
+        if not insts:
+            return
+        self.stream.synchronize()
+        local = next((e for e in (o.check() for o in insts) if e), "")
+        if reduce_max(1.0 if local else 0.0) > 0.0:
+            raise CollectiveError(local or "one-shot all-reduce failed on a peer rank (its latched error; this rank's "
+                                  "parameters may differ from that rank's)")
 
     def _check_oneshot(self, t0: Optional[float] = None) -> None:
         """One-shot data plane: a flag wait that timed out is latched on the device (no sum written, later calls

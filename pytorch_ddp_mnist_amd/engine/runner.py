@@ -253,6 +253,12 @@ class NativeEngine:
         self.tr.synchronize()
 
 
+def _uses_oneshot(engine) -> bool:
+    """A one-shot xGMI all-reduce plane (data plane or the OVERLAP plan's instances) is attached."""
+    tr = getattr(engine, "tr", None)
+    return getattr(tr, "oneshot", None) is not None or getattr(tr, "overlap", None) is not None
+
+
 def make_engine(cfg: TrainConfig, ctx: DistContext, xtr, ytr, xte, yte):
     if cfg.init_seed is not None:
         torch.manual_seed(cfg.init_seed)
@@ -352,6 +358,11 @@ def run(cfg: TrainConfig, entry: str = "ddp_tutorial_cpu", show_banner: bool = F
             loader = InterleavedLoader(readers[0], idx, engine.write_train_rows)
             order = torch.arange(len(idx))
         bar = ProgressBar.make(cfg, ctx.rank, len(order), "training")
+        if ctx.world > 1 and _uses_oneshot(engine):
+            # the one-shot data plane's flag waits are bounded (MNIST_AMD_ONESHOT_TIMEOUT, 5 s) and a timeout is
+            # latched as fatal: per-rank host work before the epoch (per-sample reads, rank 0's resume save) must not
+            # put one rank's first collective that far ahead of another's (advisor, round 5)
+            ctx.barrier()
         with range_(f"epoch{i}.train"), timer("train"):
             tr = engine.train_epoch(order, progress=bar, prefetch=nxt, batch_loader=loader)
         if loader is not None:
@@ -400,6 +411,8 @@ def run(cfg: TrainConfig, entry: str = "ddp_tutorial_cpu", show_banner: bool = F
             if ctx.rank == 0:
                 save_resume(cfg.resume, params, mom, i, cfg.model, cfg.dtype, global_step=gstep)
     engine.finish()
+    if ctx.world > 1 and _uses_oneshot(engine):
+        engine.tr.agree_oneshot(ctx.all_reduce_max)  # every rank raises if any rank latched a one-shot failure
     sd = engine.state_dict()
     if ctx.rank == 0 and cfg.save_path:
         save_model(sd, cfg.save_path)

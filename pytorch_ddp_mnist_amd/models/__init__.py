@@ -24,6 +24,13 @@ CONV_PARAMS = {"mlp": 0, "lenet5": 2572}
 # first parameter of backward phase 0 = the late layers, whose gradients backward produces first
 # (LeNet: the FC head after the convs; MLP: layers 3.* and 5.* after 0.*) -- csrc model_phase_split
 PHASE_SPLIT = {"mlp": 100480, "lenet5": 2572}
+# Gradient-producing units in backward-READY order, (name, p0, p1) in the flat slab: the FC layers last to first
+# (each one weight-gradient job of the native kernels, csrc model_job_begin), then LeNet's convolutions (conv_bwd).
+# Reference gradient-ready order: survey §2.7.  Bucket plans (parallel/ddp.py) group contiguous runs of them.
+UNITS = {
+    "mlp": [("5.*", 116992, 118272), ("3.*", 100480, 116992), ("0.*", 0, 100480)],
+    "lenet5": [("11.*", 60856, 61706), ("9.*", 50692, 60856), ("7.*", 2572, 50692), ("conv", 0, 2572)],
+}
 
 
 def build_model(name: str) -> nn.Module:
@@ -63,4 +70,4 @@ def flatten_grads(module: nn.Module) -> torch.Tensor:
 
 __all__ = ["create_model", "create_lenet5", "build_model", "param_layout", "flatten_state",
            "unflatten_state", "flatten_grads", "MODEL_IDS", "NPARAM", "CONV_PARAMS",
-           "PHASE_SPLIT"]
+           "PHASE_SPLIT", "UNITS"]

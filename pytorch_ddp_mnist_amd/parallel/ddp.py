@@ -112,6 +112,152 @@ def model_phases(model: str) -> List[Tuple[int, int]]:
     return [(c, n), (0, c)]
 
 
+# ------------------------------------------------------------------------------------------------------------
+# Link-aware bucket groups: WHICH gradients leave together, chosen from the measured RCCL latency
+# curve of the real communicator and the measured backward cost of each gradient-producing unit.
+#
+# A plan is a partition of the model's units (models.UNITS, backward-ready order) into contiguous GROUPS; group g's
+# gradients are produced by one weight-gradient launch (+ reduce) and all-reduced as soon as they are ready, on the
+# comm stream, in group order (csrc/runtime/trainer.cpp launch_lenet_split_tail / launch_mlp_comm_tail).  The
+# default SPLIT plan is two groups (LeNet: FC head | conv; MLP: layers 3+2 | layer 1).  On xGMI every collective
+# of these sizes (1 KB - 400 KB) is latency-bound -- a ring's per-hop synchronisation, not the ~153 GB/s of a link,
+# sets its time -- so a group is worth cutting off only when its all-reduce can start early enough to hide under
+# the remaining backward work AND the extra launches and collective latencies it adds stay hidden as well.  The
+# model below prices exactly that; the start-up calibration then times the best modelled plans for real.
+# ------------------------------------------------------------------------------------------------------------
+class LatencyCurve:
+    """All-reduce latency (us) vs message bytes, piecewise linear through measured points (rank-max medians of
+    standalone collectives on the job's communicator); flat below the smallest point, extended with the last
+    segment's slope above the largest."""
+
+    def __init__(self, points: Sequence[Tuple[int, float]]):
+        pts = sorted((int(b), float(t)) for b, t in points)
+        if not pts:
+            raise ValueError("LatencyCurve: no points")
+        self.pts = pts
+
+    def __call__(self, nbytes: float) -> float:
+        p = self.pts
+        if nbytes <= p[0][0] or len(p) == 1:
+            return p[0][1]
+        for (b0, t0), (b1, t1) in zip(p, p[1:]):
+            if nbytes <= b1:
+                return t0 + (t1 - t0) * (nbytes - b0) / max(1, b1 - b0)
+        (b0, t0), (b1, t1) = p[-2], p[-1]
+        return t1 + max(0.0, (t1 - t0) / max(1, b1 - b0)) * (nbytes - b1)
+
+    def as_dict(self) -> Dict[str, float]:
+        return {str(b): round(t, 2) for b, t in self.pts}
+
+
+# message sizes the start-up sweep times (4 KB .. 1 MB: every bucket either model can form lies inside)
+LATENCY_SWEEP_BYTES = (4096, 16384, 32768, 65536, 131072, 262144, 524288, 1048576)
+
+
+def partitions(n: int) -> List[List[List[int]]]:
+    """Every split of units 0..n-1 (in order) into non-empty contiguous groups (2**(n-1) of them)."""
+    out = []
+    for mask in range(1 << max(0, n - 1)):
+        groups, cur = [], [0]
+        for i in range(1, n):
+            if mask >> (i - 1) & 1:
+                groups.append(cur)
+                cur = [i]
+            else:
+                cur.append(i)
+        groups.append(cur)
+        out.append(groups)
+    return out
+
+
+def fc_unit_count(model: str) -> int:
+    """Units produced by FC weight-gradient launches (all of the MLP's; LeNet's without the conv unit)."""
+    from ..models import UNITS
+    return sum(1 for name, _, _ in UNITS[model] if name != "conv")
+
+
+def groups_to_buckets(model: str, groups: Sequence[Sequence[int]], cap_bytes: Optional[int] = None,
+                      elem_bytes: int = 4) -> List[Range]:
+    """Bucket ranges (p0, p1, group) of a partition of the FC units (indices into models.UNITS); LeNet's conv unit
+    is appended as the last group.  ``cap_bytes`` splits a group into several collectives (cut from the end, as
+    :func:`plan_buckets`), all issued when the group is ready."""
+    from ..models import UNITS
+    units = UNITS[model]
+    nfc = fc_unit_count(model)
+    flat = [i for g in groups for i in g]
+    if flat != list(range(nfc)):
+        raise ValueError(f"groups_to_buckets: {groups} is not an ordered partition of the {nfc} FC units")
+    spans = [(min(units[i][1] for i in g), max(units[i][2] for i in g)) for g in groups]
+    if nfc < len(units):
+        spans.append((units[-1][1], units[-1][2]))
+    out: List[Range] = []
+    for gi, (p0, p1) in enumerate(spans):
+        for a, b, _ in plan_buckets([(p0, p1)], cap_bytes, elem_bytes):
+            out.append((a, b, gi))
+    return out
+
+
+def default_groups(model: str) -> List[List[int]]:
+    """The two-group default (LeNet: the whole FC head, then conv; MLP: layers 3+2, then layer 1)."""
+    n = fc_unit_count(model)
+    return [list(range(n))] if model == "lenet5" else [list(range(n - 1)), [n - 1]]
+
+
+def model_split_tail_us(model: str, groups: Sequence[Sequence[int]], lat: LatencyCurve, unit_us: Sequence[float],
+                        fc_all_us: float, main_us: float = 0.0, update_us: float = 2.0, elem_bytes: int = 4) -> float:
+    """Modelled time from the start of the weight gradients to the end of the step's last update under SPLIT with
+    these groups.  ``unit_us``: each FC unit's weight gradient + reduce as its own launches (ready order);
+    ``fc_all_us``: all FC units as ONE launch + reduce (merging k units into a group saves (k-1) x the measured
+    per-launch saving); ``main_us`` (LeNet): conv_bwd + its reduce, on the main stream beside the FC groups.
+    Groups run back to back (LeNet: aux stream; MLP: main stream); the comm stream sends group g when it is ready
+    and its previous collective is done (one all-reduce + one update each); LeNet's conv group goes last."""
+    from ..models import UNITS
+    units = UNITS[model]
+    nfc = fc_unit_count(model)
+    save = max(0.0, (sum(unit_us[:nfc]) - fc_all_us) / (nfc - 1)) if nfc > 1 else 0.0
+    t = comm = 0.0
+    for g in groups:
+        t += sum(unit_us[i] for i in g) - save * (len(g) - 1)
+        nbytes = elem_bytes * sum(units[i][2] - units[i][1] for i in g)
+        comm = max(comm, t) + lat(nbytes) + update_us
+    if nfc < len(units):  # LeNet: the conv group after conv_bwd + reduce on the main stream
+        nbytes = elem_bytes * (units[-1][2] - units[-1][1])
+        comm = max(comm, main_us) + lat(nbytes) + update_us
+    return comm
+
+
+def model_join_tail_us(model: str, lat: LatencyCurve, fc_all_us: float, main_us: float = 0.0,
+                       update_us: float = 2.0, elem_bytes: int = 4) -> float:
+    """The JOIN plan on the same clock: both branches reduced, then ONE all-reduce of every gradient and one update."""
+    from ..models import NPARAM
+    return max(fc_all_us, main_us) + lat(elem_bytes * NPARAM[model]) + update_us
+
+
+def choose_bucket_groups(model: str, lat: LatencyCurve, unit_us: Sequence[float], fc_all_us: float,
+                         main_us: float = 0.0, update_us: float = 2.0) -> List[Tuple[List[List[int]], float]]:
+    """Every partition of the FC units ranked by :func:`model_split_tail_us` (fastest first; ties: fewer groups)."""
+    ranked = [(g, model_split_tail_us(model, g, lat, unit_us, fc_all_us, main_us, update_us))
+              for g in partitions(fc_unit_count(model))]
+    ranked.sort(key=lambda x: (round(x[1], 3), len(x[0])))
+    return ranked
+
+
+def bucket_plan_candidates(model: str, ranked: Sequence[Tuple[List[List[int]], float]], base: Optional[dict] = None
+                           ) -> Dict[str, dict]:
+    """SPLIT candidates from a ranking: the modelled best plan (``split_bm``) unless it is the default grouping, and
+    the best plan with at least two FC groups (``split_mb``: LeNet >= 3 buckets, MLP >= 3), so the calibration
+    always measures one multi-bucket plan against the default.  Each candidate carries its bucket ranges."""
+    base = dict(base or {"plan": "split", "bwd_blocks": 0})
+    out: Dict[str, dict] = {}
+    dflt = default_groups(model)
+    if ranked and ranked[0][0] != dflt:
+        out["split_bm"] = dict(base, buckets=groups_to_buckets(model, ranked[0][0]), groups=ranked[0][0])
+    multi = [g for g, _ in ranked if len(g) >= (2 if model == "lenet5" else 3)]
+    if multi and multi[0] != dflt and ("split_bm" not in out or out["split_bm"]["groups"] != multi[0]):
+        out["split_mb"] = dict(base, buckets=groups_to_buckets(model, multi[0]), groups=multi[0])
+    return out
+
+
 def coalesce_buckets(buckets: Sequence[Range]) -> List[Range]:
     """Merge a bucket into the previous one when they are contiguous and belong to different backward
     phases (the JOIN plan's one all-reduce of the coalesced slab; csrc/runtime/trainer.cpp

@@ -2,7 +2,7 @@
 # Build the native _C extension of another git revision as pytorch_ddp_mnist_amd/_C_ab.so (CPU host, before a
 # GPU call), for same-box A/B runs against the working tree's build:
 #   scripts/build_ab.sh REV [NAME]      (NAME: module name, default _C_ab)
-#   gpurun -- 'bash scripts/ab_env.sh TAG "--steps 2000 --warmup 50" "MNIST_AMD_C_PATH=pytorch_ddp_mnist_amd/_C_ab.so" "-"'
+#   gpurun -- 'bash scripts/ab.sh TAG "--steps 2000 --warmup 50" "MNIST_AMD_C_PATH=pytorch_ddp_mnist_amd/_C_ab.so" "-"'
 set -e
 REV=${1:?revision}
 NAME=${2:-_C_ab}

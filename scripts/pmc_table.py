@@ -1,6 +1,8 @@
-"""Per-kernel hardware-counter table from the four passes of scripts/pmc_final.sh.
+"""Per-kernel hardware-counter table from the passes of scripts/prof.sh pmc (a-d; e adds the
+instruction-issue table).
 
-    python scripts/pmc_table.py gpurun_out/pmcf [--batch 8192] > profiles/<tag>/pmc_table.md
+    python scripts/pmc_table.py gpurun_out/TAG_CONFIG [--batch 8192] > profiles/<tag>/pmc_table.md
+    (passes written by: scripts/prof.sh pmc TAG CONFIG)
 
 Columns: mean duration (counter runs, kernel-trace timestamps), VGPR/AGPR/LDS per workgroup,
 waves per SIMD the resources allow, MFMA-busy share of the kernel's SIMD-cycles, LDS bank-conflict
@@ -78,6 +80,9 @@ def main():
     ap.add_argument("--model", default="lenet5", choices=["lenet5", "mlp"])
     a = ap.parse_args()
     P = {s: load(os.path.join(f"{a.prefix}_{s}", "run_counter_collection.csv")) for s in "abcd"}
+    pe = os.path.join(f"{a.prefix}_e", "run_counter_collection.csv")
+    if os.path.exists(pe):
+        P["e"] = load(pe)
     print("| kernel | calls | us | VGPR/AGPR | LDS B/WG | waves/SIMD (res.) | MFMA busy % | LDS bank-conflict % "
           "| LDS active % | WAIT_ANY % | TFLOP/s | HBM read GB/s | HBM write GB/s |")
     print("|---|---|---|---|---|---|---|---|---|---|---|---|---|")
@@ -98,6 +103,37 @@ def main():
         occ = waves_per_simd(vg, ag, lds, wg)
         print(f"| {k} | {n} | {t * 1e6:.1f} | {vg}/{ag} | {lds} | {occ:g} | {mfma:.1f} | {lds_c:.1f} | {lds_act:.0f} | {wait:.0f} | "
               f"{tf:.1f} | {rd:.0f} | {wr:.0f} |")
+    if "e" in P:
+        issue_table(P)
+
+
+def issue_table(P):
+    """Instruction issue mix (pass e + a + b): instructions per wave by class and how full the issue
+    slots were.  SQ_INSTS_VALU includes the MFMAs; a wave64 VALU instruction occupies its SIMD's vector
+    issue for 2 cycles and a v_mfma_f32_16x16x32_bf16 for 8 of its 16 (MI355X_MICROARCH.md, 'vector-
+    instruction ISSUE cost'); SQ_ACTIVE_INST_* and SQ_WAVE_CYCLES count quad-cycles."""
+    print()
+    print("| kernel | waves | VALU/wave | MFMA/wave | LDS/wave | SALU/wave | SMEM/wave | VMEM/wave | branch/wave "
+          "| vector-issue busy % of SIMD cycles | MFMA pipe busy % | VALU-active % of wave time | LDS-active % of wave time "
+          "| any-inst % of wave time |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|---|---|---|")
+    for k in sorted(P["e"], key=lambda x: -P["e"][x][2]):
+        ce, _, t, n = P["e"][k]
+        ca = P["a"].get(k, ({},))[0]
+        cb = P["b"].get(k, ({},))[0]
+        waves = ce.get("SQ_WAVES", 0.0) or 1.0
+        cyc = ce.get("GRBM_GUI_ACTIVE", 0.0) / N_XCD
+        valu, mfma = ca.get("SQ_INSTS_VALU", 0.0), ce.get("SQ_INSTS_MFMA", 0.0)
+        simd_cyc = max(1.0, cyc * N_CU * SIMD)
+        vec_issue = 100.0 * ((valu - mfma) * 2 + mfma * 8) / simd_cyc
+        mfma_busy = 100.0 * cb.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / simd_cyc
+        wc = max(1.0, ce.get("SQ_WAVE_CYCLES", 0.0))
+        pw = lambda v: v / waves
+        print(f"| {k} | {waves:.0f} | {pw(valu - mfma):.0f} | {pw(mfma):.0f} | {pw(ca.get('SQ_INSTS_LDS', 0.0)):.0f} | "
+              f"{pw(cb.get('SQ_INSTS_SALU', 0.0)):.0f} | {pw(ce.get('SQ_INSTS_SMEM', 0.0)):.0f} | "
+              f"{pw(cb.get('SQ_INSTS_VMEM', 0.0)):.0f} | {pw(ce.get('SQ_INSTS_BRANCH', 0.0)):.0f} | {vec_issue:.1f} | "
+              f"{mfma_busy:.1f} | {100.0 * ce.get('SQ_ACTIVE_INST_VALU', 0.0) / wc:.0f} | "
+              f"{100.0 * ce.get('SQ_ACTIVE_INST_LDS', 0.0) / wc:.0f} | {100.0 * ca.get('SQ_ACTIVE_INST_ANY', 0.0) / max(1.0, ca.get('SQ_WAVE_CYCLES', 0.0)):.0f} |")
 
 
 if __name__ == "__main__":

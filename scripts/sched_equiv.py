@@ -10,10 +10,12 @@ rank's "all-reduced" gradient is its own): they must equal a local run at half t
 ``_k<k>`` variants run the steps as ONE k-step graph (run_steps), whose steps may leave the aux
 branch join to the next step's head; they must equal the same number of single-step graphs.
 Usage: python scripts/sched_equiv.py [--model mlp|lenet5] [--dtype bf16|fp32] [--batch B] VARIANT [VARIANT ...]
-  VARIANT = {local,local_halflr,join,split,overlap}[_b<blocks>][_w2][_k<k>][_t<rows>]   (overlap: LeNet, world-1
-  one-shot; _t<rows>: one more step of a partial batch of <rows> rows after the full ones, eager launch)
+  VARIANT = {local,local_halflr,join,split,overlap}[_g<groups>][_b<blocks>][_w2][_k<k>][_t<rows>]   (overlap: LeNet,
+  world-1 one-shot; _t<rows>: one more step of a partial batch of <rows> rows after the full ones, eager launch;
+  _g<groups>: the bucket groups of the FC units in ready order, "." between groups, e.g. split_g0.1.2)
 """
 import argparse
+import gc
 import hashlib
 import os
 import re
@@ -27,6 +29,7 @@ from pytorch_ddp_mnist_amd.data.synthetic import make_split  # noqa: E402
 from pytorch_ddp_mnist_amd.engine.native import NativeTrainer  # noqa: E402
 from pytorch_ddp_mnist_amd.models import build_model  # noqa: E402
 from pytorch_ddp_mnist_amd.ops.native import load_c  # noqa: E402
+from pytorch_ddp_mnist_amd.parallel.ddp import groups_to_buckets  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("variants", nargs="+")
@@ -42,11 +45,12 @@ C = load_c()
 order = torch.randperm(N, generator=torch.Generator().manual_seed(1)).to(torch.int32)
 
 for v in a.variants:
-    m = re.fullmatch(r"(local_halflr|local|join|split|overlap)(?:_b(\d+))?(_w2)?(?:_k(\d+))?(?:_t(\d+))?", v)
+    m = re.fullmatch(r"(local_halflr|local|join|split|overlap)(?:_g([0-9.]+))?(?:_b(\d+))?(_w2)?(?:_k(\d+))?(?:_t(\d+))?", v)
     if not m:
         raise SystemExit(f"unknown variant {v}")
-    kind, blocks, w2, k = m.group(1), int(m.group(2) or 0), bool(m.group(3)), int(m.group(4) or 0)
-    tail_rows = int(m.group(5) or 0)
+    kind, gspec = m.group(1), m.group(2)
+    blocks, w2, k = int(m.group(3) or 0), bool(m.group(4)), int(m.group(5) or 0)
+    tail_rows = int(m.group(6) or 0)
     lr = 0.025 if kind == "local_halflr" else 0.05
     torch.manual_seed(0)
     tr = NativeTrainer(a.model, a.dtype, a.batch, torch.from_numpy(x.reshape(-1, 784)), torch.from_numpy(y),
@@ -54,6 +58,8 @@ for v in a.variants:
     if kind in ("join", "split"):
         tr.attach_comm(C.RcclComm(C.RcclComm.make_unique_id(), 0, 1, 0), 2 if w2 else 1, plan=kind,
                        bwd_blocks=blocks)
+        if gspec:  # bucket groups of the FC units in ready order, e.g. "0.1.2" = three groups, "01.2" = two
+            tr.set_buckets(groups_to_buckets(a.model, [[int(c) for c in part] for part in gspec.split(".")]))
         tr.broadcast_params(0)
     elif kind == "overlap":  # world-1 one-shot instances (identity sums), the 1/W of a 2-rank job with _w2
         fc, conv = C.OneShotAllReduce(0, 1, 0, tr.nparam), C.OneShotAllReduce(0, 1, 0, int(tr.rt.conv_params))
@@ -73,3 +79,12 @@ for v in a.variants:
     print("digest", v, hashlib.sha256(tr.params.cpu().numpy().tobytes()).hexdigest(), flush=True)
     if a.dump:
         torch.save(tr.params.cpu(), f"{a.dump}.{v}.pt")
+    # deterministic teardown before the next variant, in DistContext.finalize's order (graphs -> trainer streams ->
+    # communicator): left to the garbage collector, a previous variant's communicator could be destroyed in the
+    # middle of the next variant's graph replays (a HIP-runtime segfault in hipGraphLaunch was seen that way)
+    comm = tr.comm
+    tr.close()
+    if comm is not None:
+        comm.destroy(60.0)
+    del tr, comm
+    gc.collect()

@@ -94,6 +94,13 @@ if fused:  # fwd_head_kernel: 16-row workgroups; head rows hold the head phases 
         bnames += [f"img{t} A (stage)", f"img{t} B (w2+dgrad)", f"img{t} C (w1)"]
     report("conv_bwd", bw, bnames + [None, "slab write"], 15)
     per_cu("conv_bwd", bw, allst[4608:4608 + nb, 0], 15)
+    wg = allst[3072:3584]
+    wg = wg[wg[:, 0] > 0]
+    if len(wg) and (wg[:, 3] > 0).all():  # wgrad_sk: [1] K loop done, [2] reduced + stored, [3] location + 1
+        report("wgrad", wg, ["loads + MFMA", "reduce + store"], 2)
+        per_cu("wgrad", wg, wg[:, 3] - 1, 2)
+        print(f"  fwd_head last end -> wgrad first start {(wg[:, 0].min() - allst[:nblk, 8].max()) * 10 / 1000:.2f} us; "
+              f"wgrad last end -> conv_bwd first start {(bw[:, 0].min() - wg[:, 2].max()) * 10 / 1000:.2f} us")
 elif model == "lenet5":
     report("head", allst[:nblk], ["idx+stage X", "L1", "L2", "L3", "softmax", "dH2", "dH1", "dX"], 8)
     # inside the staging phase: [0] entry -> [9] loads issued -> [10] weights stored -> [11] X stored -> [1] barrier
@@ -148,8 +155,11 @@ if model == "mlp":
     def live(st):
         return st[st[:, 0] > 0]
     l1s, hs, wgs = live(allst[3584:4096]), allst[:nblk], live(allst[3072:3584])
-    wlast = 2 if (wgs[:, 2] > 0).all() else 1   # wgrad_sgd stamps 0..2, the split wgrad 0..1
-    report("wgrad", wgs, ["GEMM", "epilogue"][:wlast], wlast)
+    wlast = 2 if (wgs[:, 2] > 0).all() else 1   # wgrad_sgd / wgrad_sk stamps 0..2, the split wgrad 0..1
+    sk = (wgs[:, 3] > 0).all()                  # wgrad_sk: [1] K loop done, [2] block reduced + stored, [3] location
+    report("wgrad", wgs, (["loads + MFMA", "reduce + store"] if sk else ["GEMM", "epilogue"])[:wlast], wlast)
+    if sk:
+        per_cu("wgrad per CU", wgs, wgs[:, 3] - 1, 2)
     if len(l1s):
         report("l1_split", l1s, ["stage X", "GEMM"], 2)
     T0 = (l1s if len(l1s) else hs)[:, 0].min()

@@ -11,8 +11,11 @@ def bench(path):
         if not l.startswith("{"):
             continue
         d = json.loads(l)
+        tune = d["config"].get("plan_autotune") or {}
+        tm = " ".join(f"{k}={v}" for k, v in (tune.get("timings_ms") or {}).items())
         print(f"  {d['config']['model']:20s} {d['dtype']:5s} B={d['config']['per_gpu_batch']:6d} "
-              f"{d['ms_per_step']:8.4f} ms/step {d['value']/1e6:8.3f} M img/s top1={d['top1']}")
+              f"{d['ms_per_step']:8.4f} ms/step {d['value']/1e6:8.3f} M img/s top1={d.get('top1')}"
+              + (f" chosen={tune.get('chosen')} [{tm}]" if tune else ""))
 
 
 def stats(path, n=10):

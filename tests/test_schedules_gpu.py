@@ -48,6 +48,36 @@ def test_schedules_bitwise_equal(native):
 
 
 @pytest.mark.timeout(600)
+def test_bucket_groups_bitwise_equal(native):
+    """Link-aware bucket plans (parallel/ddp.py choose_bucket_groups): SPLIT with the FC head cut into 2 or 3 bucket
+    groups -- each its own weight-gradient launch (job mask), reduce, all-reduce and update -- gives the parameters of
+    the local step, bitwise (world-1 communicator; _w2: the 1/W arithmetic of two ranks)."""
+    serial = _digests({"MNIST_AMD_CONCURRENT": "0"}, ["local", "local_halflr"])
+    d = _digests({"MNIST_AMD_CONCURRENT": "1"}, ["split_g0.1.2", "split_g01.2", "split_g0.12", "split_g0.1.2_w2",
+                                                  "split_g0.1.2_k4", "join_g0.1.2"])
+    for k in ("split_g0.1.2", "split_g01.2", "split_g0.12", "split_g0.1.2_k4", "join_g0.1.2"):
+        assert d[k] == serial["local"], k
+    assert d["split_g0.1.2_w2"] == serial["local_halflr"]
+    m = _digests({}, ["local", "split_g0.1.2", "split_g012", "split_g0.12_k4"], model="mlp")
+    for k in ("split_g0.1.2", "split_g012", "split_g0.12_k4"):
+        assert m[k] == m["local"], k
+
+
+@pytest.mark.timeout(900)
+def test_large_batch_schedules_bitwise_equal(native):
+    """The headline batch (8192: fused forward + head, split-K-in-workgroup weight gradient, 16 FC splits): serial,
+    concurrent, JOIN / SPLIT and multi-group SPLIT steps give bitwise-identical parameters."""
+    extra = ("--batch", "8192", "--steps", "2")
+    serial = _digests({"MNIST_AMD_CONCURRENT": "0"}, ["local"], extra=extra)
+    d = _digests({"MNIST_AMD_CONCURRENT": "1"}, ["local", "join", "split", "split_g0.1.2", "split_g01.2"], extra=extra)
+    for k in ("local", "join", "split", "split_g0.1.2", "split_g01.2"):
+        assert d[k] == serial["local"], k
+    m = _digests({}, ["local", "join", "split", "split_g0.1.2"], model="mlp", extra=extra)
+    for k in ("join", "split", "split_g0.1.2"):
+        assert m[k] == m["local"], k
+
+
+@pytest.mark.timeout(600)
 @pytest.mark.parametrize("dtype,batch", [("fp32", 128), ("bf16", 128)])
 def test_small_batch_serial_equals_concurrent(native, dtype, batch):
     """Small batches (one FC batch split): the serial schedule runs conv_bwd and the SGD-fused FC weight

@@ -109,4 +109,12 @@ def test_comm_profile_world1(native, model):
     assert prof["step_plan_ms"] > 0 and prof["step_local_ms"] > 0
     assert abs(prof["exposed_comm_us"] - 1000 * (prof["step_plan_ms"] - prof["step_local_ms"])) < 0.1
     tune = out["config"]["plan_autotune"]
-    assert "nocomm" in tune["timings_ms"] and tune["chosen"] in ("join", "split", "split_r16")
+    assert "nocomm" in tune["timings_ms"] and tune["chosen"] in ("join", "split", "split_r16", "split_bm", "split_mb")
+    # link-aware bucket plan: the latency sweep and unit costs measured on this communicator, every partition of
+    # the FC units ranked, and a multi-bucket SPLIT candidate timed beside the default plans
+    bm = tune["bucket_model"]
+    assert len(bm["latency_us"]) == 8 and all(v > 0 for v in bm["latency_us"].values())
+    assert len(bm["unit_us"]) == 3 and bm["fc_all_us"] > 0 and len(bm["ranked"]) == 4
+    assert any(k in tune["timings_ms"] for k in ("split_bm", "split_mb"))
+    multi = [k for k in ("split_bm", "split_mb") if k in tune["candidates"]]
+    assert any(len({b[2] for b in tune["candidates"][k]["buckets"]}) >= 3 for k in multi)
