@@ -280,5 +280,6 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("pack_size", &Trainer::pack_size)
       .def_property_readonly("conv_slabs", &Trainer::conv_slabs)
       .def_property_readonly("conv_params", &Trainer::conv_params)
-      .def_property_readonly("fc_splits", &Trainer::fc_splits);
+      .def_property_readonly("fc_splits", &Trainer::fc_splits)
+      .def_property_readonly("fc_ld", &Trainer::fc_ld);
 }

@@ -1287,6 +1287,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF > 2 || (
   using Frag = typename M::Frag;
   constexpr int KV = M::KV, KC = M::KC;
   constexpr bool CUT = sizeof(T) == 4 && SPL;
+  constexpr int TP = 68;  // row pitch (floats) of the reduced 64x64 block in LDS: 16-byte rows, spread banks
   __shared__ __attribute__((aligned(16))) f32x4 red[2][16][64];  // 32 KB: two waves' partial blocks at a time
   const int lane = threadIdx.x & 63, w = wave_id(), row = lane & 15, grp = lane >> 4;
   const int L = blockIdx.x;
@@ -1310,26 +1311,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF > 2 || (
   const int lb = tile - J.blk_begin;
   const int bn = lb / J.nblk_k, bk = lb % J.nblk_k;
   const int n0 = bn * 64, k0 = bk * 64;
-  // Branch-free body: every fragment load is issued (rows clamped into the operand images: A rows past NP read
-  // the zero-padded row NP - 1 or feed only discarded outputs, B rows past K the last row) and all 16 MFMAs of a
-  // K-step run; B columns past K read ones (bias column) or zeros by a per-lane select.  (Branching around the
-  // padding tiles' loads and MFMAs put 261 conditional branches into the loop.)
-  const T* ap[4];
-  const T* bp[4];
-  bool use[4];
-  Frag alt[4];
+  // Operand fragments by raw buffer loads whose resource ends at the operand's last real row (dY^T: N rows, X^T:
+  // K rows): padding rows read as zeros WITHOUT memory traffic (LeNet's 10-row fc3 gradient in a 64-row block no
+  // longer pulls 54 dead rows).  Branch-free body: every load is issued and all 16 MFMAs of a K-step run; the bias
+  // column (k == K) reads ones by a per-lane select.  (Branching around the padding tiles' loads and MFMAs had put
+  // 261 conditional branches into the loop.)
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(J.dyT), (short)0,
+                                                                      J.N * a.ldB * (int)sizeof(T), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(J.xT), (short)0,
+                                                                      J.K * a.ldB * (int)sizeof(T), 0x00020000);
+  int ao[4], bo[4];
+  bool ones_col[4];
   Frag ones;
 #pragma unroll
   for (int q = 0; q < KV; ++q) M::set(ones, q, 1.f);
-  const Frag zf = M::zero();
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    ap[i] = J.dyT + (size_t)min(n0 + 16 * i + row, J.NP - 1) * a.ldB + rs + grp * KV;
+    ao[i] = ((n0 + 16 * i + row) * a.ldB + rs + grp * KV) * (int)sizeof(T);
     const int kk = k0 + 16 * i + row;
-    bp[i] = J.xT + (size_t)min(kk, J.K > 0 ? J.K - 1 : 0) * a.ldB + rs + grp * KV;
-    use[i] = kk < J.K;
-    alt[i] = (kk == J.K && J.bias) ? ones : zf;  // bias column: ones; padding: zeros
+    bo[i] = (kk * a.ldB + rs + grp * KV) * (int)sizeof(T);
+    ones_col[i] = kk == J.K && J.bias;
   }
+  auto ld = [&](const __amdgpu_buffer_rsrc_t& r, int voff, int soff) {
+    Frag f;
+    f.v = __builtin_bit_cast(decltype(f.v), __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
+    return f;
+  };
   f32x4 acc[4][4];
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi)
@@ -1339,15 +1346,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF > 2 || (
   // K-step groups: every fragment of PF steps is issued before the first MFMA (the sched_barrier keeps hipcc
   // from sinking each load next to its use -- it had turned the group into one load + vmcnt(0) per 4 MFMAs); a
   // group's steps past this wave's count re-read its last step and multiply zero A fragments
+  const Frag zf = M::zero();
   for (int g = 0; g < nw; g += PF) {
     Frag fa[PF][4], fb[PF][4];
 #pragma unroll
     for (int p = 0; p < PF; ++p) {
-      const int off = (w + 4 * min(g + p, nw - 1)) * KC;
+      const int soff = (w + 4 * min(g + p, nw - 1)) * KC * (int)sizeof(T);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        fa[p][i] = M::load(ap[i] + off);
-        fb[p][i] = M::load(bp[i] + off);
+        fa[p][i] = ld(ra, ao[i], soff);
+        fb[p][i] = ld(rb, bo[i], soff);
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -1358,7 +1366,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF > 2 || (
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         av[i].v = (full || g + p < nw) ? fa[p][i].v : zf.v;
-        b[i].v = use[i] ? fb[p][i].v : alt[i].v;
+        b[i].v = ones_col[i] ? ones.v : fb[p][i].v;
       }
       if constexpr (CUT) {
         u32x2 ah[4], am[4], al[4], bh[4], bm[4], bl[4];
@@ -1380,8 +1388,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF > 2 || (
     }
   }
   if (a.stamps && threadIdx.x == 0 && L < 512) a.stamps[(STAMP_WGRAD + L) * 16 + 1] = wall_clock64();
-  // fixed-order sum of the four waves' partial blocks, (w0 + w2) + (w1 + w3), through 32 KB of LDS; then wave 0
-  // writes the block's slab row with buffer stores whose out-of-range offsets (padding outputs) the hardware drops
+  // fixed-order sum of the four waves' partial blocks, (w0 + w2) + (w1 + w3), through 32 KB of LDS
   if (w >= 2) {
 #pragma unroll
     for (int t = 0; t < 16; ++t) red[w - 2][t][lane] = acc[t >> 2][t & 3];
@@ -1397,31 +1404,43 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(PF > 2 || (
     for (int t = 0; t < 16; ++t) red[0][t][lane] = acc[t >> 2][t & 3];
   }
   __syncthreads();
+  // wave 0 completes the sum, then lays the block out row-major ([n][k], pitch TP: 17 KB, over both buffers --
+  // it has read buffer 0 into registers first, and nothing reads buffer 1 any more) ...
+  static_assert(64 * TP * 4 <= (int)sizeof(red), "the row-major block must fit the reduction buffers");
+  float* tileb = reinterpret_cast<float*>(&red[0][0][0]);
   if (w == 0) {
-    const int nout = J.N * J.K + (J.bias ? J.N : 0);  // this job's parameters
-    const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(
-        a.slab + (size_t)split * a.slab_ld + J.out_off, (short)0, nout * 4, 0x00020000);
-    const int kb = J.K + (J.bias ? 1 : 0);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) acc[t >> 2][t & 3] += red[0][t][lane];
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        const f32x4 sv = acc[mi][ni] + red[0][mi * 4 + ni][lane];
-        const int k = k0 + ni * 16 + row;
-        const bool wcol = k < J.K;  // weight column (else: the bias column k == K, or padding)
+      for (int ni = 0; ni < 4; ++ni)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int n = n0 + mi * 16 + grp * 4 + i;
-          // weight (n, k) at n * K + k, bias n at N * K + n; padding rows / columns: an offset past the buffer end
-          const int q = wcol ? n * J.K + k : J.N * J.K + n;
-          const bool ok = (n < J.N) & (k < kb);
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(sv[i]), rs_out, ok ? q * 4 : 0x7FFFFFF0, 0, 0);
-        }
-      }
-    if (a.stamps && threadIdx.x == 0 && L < 512) {
-      a.stamps[(STAMP_WGRAD + L) * 16 + 2] = wall_clock64();
-      a.stamps[(STAMP_WGRAD + L) * 16 + 3] = hw_location() + 1;  // (+1: never 0, marks the 3-phase stamp set)
-    }
+        for (int i = 0; i < 4; ++i) tileb[(mi * 16 + grp * 4 + i) * TP + ni * 16 + row] = acc[mi][ni][i];
+  }
+  __syncthreads();
+  // ... and all 256 threads write the slab row as 16-byte stores: weight (n, k..k+3) at n * K + k (K % 4 == 0 for
+  // every layer, and slab rows / job offsets are 16-byte aligned: Trainer::fc_ld), the bias column k == K at
+  // N * K + n; padding rows / columns get an offset past the resource end, which the hardware drops
+  const int nout = J.N * J.K + (J.bias ? J.N : 0);  // this job's parameters
+  const __amdgpu_buffer_rsrc_t rs_out = __builtin_amdgcn_make_buffer_rsrc(
+      a.slab + (size_t)split * a.slab_ld + J.out_off, (short)0, nout * 4, 0x00020000);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int c = threadIdx.x + 256 * e, n = c >> 4, kc = (c & 15) * 4;
+    const f32x4 v = *reinterpret_cast<const f32x4*>(&tileb[n * TP + kc]);
+    const bool ok = (n0 + n < J.N) & (k0 + kc < J.K);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), rs_out,
+                                           ok ? ((n0 + n) * J.K + k0 + kc) * 4 : 0x7FFFFFF0, 0, 0);
+  }
+  if (J.bias && J.K >= k0 && J.K < k0 + 64 && threadIdx.x < 64) {
+    const int n = threadIdx.x;
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(tileb[n * TP + (J.K - k0)]), rs_out,
+                                          n0 + n < J.N ? (J.N * J.K + n0 + n) * 4 : 0x7FFFFFF0, 0, 0);
+  }
+  if (a.stamps && threadIdx.x == 0 && L < 512) {
+    a.stamps[(STAMP_WGRAD + L) * 16 + 2] = wall_clock64();
+    a.stamps[(STAMP_WGRAD + L) * 16 + 3] = hw_location() + 1;  // (+1: never 0, marks the 3-phase stamp set)
   }
 }
 
@@ -1433,13 +1452,16 @@ int wgrad_sk_pf() {
   }();
   return v;
 }
-// MNIST_AMD_WGRAD_SK=1: the split-K-in-workgroup kernel from SK_MIN_B (A/B switch; off until it measures faster)
-bool wgrad_sk_enabled() {
-  static const bool on = [] {
+// MNIST_AMD_WGRAD_SK=1: the split-K-in-workgroup kernel from SK_MIN_B in every schedule (opt-in A/B).  Measured (profiles/r6_session1/NOTES.md): LeNet bf16
+// B=8192 ~9.7 us span vs 15.9 us for wgrad_kernel alone, but beside conv_bwd its 32 KB of LDS per workgroup cannot
+// co-reside with conv_bwd's two 71 KB workgroups (the concurrent step 0.1068 vs 0.0975 ms); the MLP's LDS-staged
+// wgrad_lds_kernel stays faster (32.2 vs 35.6 us per step)
+int wgrad_sk_mode() {
+  static const int m = [] {
     const char* e = std::getenv("MNIST_AMD_WGRAD_SK");
-    return e && *e == '1';
+    return e && *e ? (*e == '1' ? 1 : 0) : -1;
   }();
-  return on;
+  return m;
 }
 
 // wgrad_kernel keeps ONE ring slot of K-step fragments per wave (the next step's fragments fetched while this
@@ -1465,7 +1487,11 @@ int wgrad_launch(const HeadBuffers& hb, int B, int splits, float* slab, int slab
   // fp32 MLP weight gradient as 3-part bf16 splits from B = 4096 on (MLP fp32 B=8192 -6 %, but B=1024 +6 %:
   // profiles/r5_session1/hsplit2); no effect for bf16 (wg_mma)
   const bool spl = B >= 4096;
-  if (!fuse && B >= SK_MIN_B && wgrad_sk_enabled()) {
+  const int skm = wgrad_sk_mode();
+  // (off by default: on the chosen schedules the LDS-free wgrad_kernel runs beside conv_bwd, and giving the serial
+  //  candidate a different kernel would end the bitwise equality of the single-GPU schedules)
+  const bool sk = skm == 1;
+  if (!fuse && B >= SK_MIN_B && sk) {
     // split-K-in-workgroup kernel over contiguous batch splits; with a split count that divides over the 8 XCDs,
     // XCD x takes splits [x * S / 8, (x + 1) * S / 8) -- the batch rows the XCD-contiguous head (xcd_unit) wrote
     // there (a bijection either way; only the L2 locality depends on the head's mapping)

@@ -122,8 +122,8 @@ struct SgdFuse {
 // job_mask: which layers' weight gradients to compute (bit l = layer l+1; 7 = all three).  A subset
 // writes only those layers' slab columns (the MLP's SPLIT plan sends layers 2+3 while layer 1 computes).
 int launch_head_wgrad(ModelKind m, DType t, const HeadBuffers& hb, int B, int splits, float* slab,
-                       int slab_ld, hipStream_t s, int head_rows = 0, const SgdFuse* fuse = nullptr,
-                       int job_mask = 7);
+                      int slab_ld, hipStream_t s, int head_rows = 0, const SgdFuse* fuse = nullptr,
+                      int job_mask = 7);
 
 void launch_lenet_conv_fwd(DType t, bool train, const BatchRef& br, const LenetConvBuffers& cb,
                            hipStream_t s);

@@ -1636,14 +1636,6 @@ void conv_bwd_fc_kernel(BatchRef br, LenetConvBuffers cb, int ipb, int nconv, wg
 
 }  // namespace
 
-// MNIST_AMD_BWD_NW=8: bf16 conv_bwd on 8-wave workgroups (experiment switch)
-static int bwd_nw_bf16() {
-  static const int v = [] {
-    const char* e = std::getenv("MNIST_AMD_BWD_NW");
-    return e && *e ? std::atoi(e) : 4;
-  }();
-  return v;
-}
 static int fwd_ipb(int B) { return std::min(MAX_IPB, std::max(1, (B + 1023) / 1024)); }
 // default conv_bwd workgroup target: 512 = one full round of 2 blocks/CU (1024 / 768 measured slower)
 static int default_bwd_target() { return 512; }
@@ -1707,9 +1699,10 @@ void launch_lenet_conv_bwd(DType t, const BatchRef& br, const LenetConvBuffers& 
   if (br.B <= 0) return;
   // Waves per workgroup (BwdRoles): fp32 -- 150 KB of LDS, one workgroup per CU -- runs 8 waves (0.440 vs
   // 0.478 ms per LeNet fp32 B=8192 step, same box); bf16 keeps 4 (two workgroups per CU: 8 waves would take
-  // every VGPR of the SIMDs and starve the FC weight gradient that runs beside conv_bwd, 0.119-0.127 vs 0.103 ms)
+  // every VGPR of the SIMDs and starve the FC weight gradient that runs beside conv_bwd, 0.119-0.127 vs 0.103 ms;
+  // round 6 timed 8 waves in every single-GPU schedule, serial included, same box: concurrent 0.1135 / serial 0.1147
+  // / separate 0.1067 vs 4 waves 0.1068 / 0.1091 / 0.1009 ms, profiles/r6_session1/NOTES.md)
   if (t == DType::F32) hipLaunchKernelGGL((conv_bwd_kernel<float, 8>), dim3(grid), dim3(512), 0, s, br, cb, ipb);
-  else if (bwd_nw_bf16() == 8) hipLaunchKernelGGL((conv_bwd_kernel<bf16, 8>), dim3(grid), dim3(512), 0, s, br, cb, ipb);
   else hipLaunchKernelGGL((conv_bwd_kernel<bf16, 4>), dim3(grid), dim3(256), 0, s, br, cb, ipb);
 }
 

@@ -95,6 +95,7 @@ Trainer::Trainer(int model, int dtype, int batch, int ld_b, int fc_splits, const
   if (batch <= 0) throw std::invalid_argument("batch must be positive");
   if (ld_b < ((batch + 63) / 64) * 64) throw std::invalid_argument("ld_b must be >= batch rounded up to 64");
   nparam_ = model_nparam(model_);
+  fc_ld_ = (nparam_ + 3) / 4 * 4;
   max_conv_slabs_ = model_ == ModelKind::LENET ? lenet_conv_bwd_max_blocks(batch_, 0) : 0;
   concurrent_ = concurrent_mode() != 0;
   const int ps = model_phase_split(model_);  // default buckets: one per backward phase (see Plan)
@@ -228,14 +229,14 @@ std::vector<double> Trainer::time_units(int iters, int warmup, uintptr_t stream)
   std::vector<std::function<void()>> units;
   for (int j = 2; j >= 0; --j)  // ready order: the last FC layer first
     units.push_back([=] {
-      const int sp = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s, hrows,
+      const int sp = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), fc_ld_, s, hrows,
                                        nullptr, 1 << j);
-      launch_reduce(ptr<const float>(p_.slab_fc), nparam_, sp, model_job_begin(model_, j), model_job_begin(model_, j + 1),
+      launch_reduce(ptr<const float>(p_.slab_fc), fc_ld_, sp, model_job_begin(model_, j), model_job_begin(model_, j + 1),
                     scale, g, s);
     });
   units.push_back([=] {
-    const int sp = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s, hrows, nullptr, 7);
-    launch_reduce(ptr<const float>(p_.slab_fc), nparam_, sp, model_job_begin(model_, 0), nparam_, scale, g, s);
+    const int sp = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), fc_ld_, s, hrows, nullptr, 7);
+    launch_reduce(ptr<const float>(p_.slab_fc), fc_ld_, sp, model_job_begin(model_, 0), nparam_, scale, g, s);
   });
   if (model_ == ModelKind::LENET)
     units.push_back([=] {
@@ -416,7 +417,7 @@ void Trainer::forward_backward(int B, uintptr_t stream) {
     if (!hrows) hrows = launch_head(model_, dtype_, true, br, hb, head_rows_per_block(model_, dtype_, batch_), s);
     post_launch(s);
   }
-  launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s, hrows);
+  launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), fc_ld_, s, hrows);
   post_launch(s);
   if (model_ == ModelKind::LENET) {
     launch_lenet_conv_bwd(dtype_, br, conv_buffers(B), nullptr, s, bwd_blocks_);
@@ -431,7 +432,7 @@ void Trainer::reduce_grads(int B, uintptr_t stream) {
   const HeadBuffers hb = head_buffers(ptr<float>(p_.metrics));
   (void)hb;
   const int splits = fc_splits_for(B);
-  launch_reduce(ptr<const float>(p_.slab_fc), nparam_, splits, cp, nparam_, scale, ptr<float>(p_.grad), s);
+  launch_reduce(ptr<const float>(p_.slab_fc), fc_ld_, splits, cp, nparam_, scale, ptr<float>(p_.grad), s);
   post_launch(s);
   if (cp > 0) {
     launch_reduce(ptr<const float>(p_.slab_conv), cp, lenet_conv_bwd_blocks(B, bwd_blocks_), 0, cp, scale, ptr<float>(p_.grad), s);
@@ -538,7 +539,7 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     }
     if (comm) {
       const int splits =
-          launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, aux_stream_, hrows);
+          launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), fc_ld_, aux_stream_, hrows);
       post_launch(aux_stream_);
       launch_lenet_comm_tail(B, nslab, splits, s);
       return;
@@ -551,13 +552,13 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     if (fc_splits_ == 1 && fuse_wgrad_sgd_) {
       const SgdFuse f{scale, lr_, momentum_, ptr<float>(p_.params), ptr<float>(p_.grad),
                       momentum_ != 0.f ? ptr<float>(p_.mom) : nullptr, ptr<void>(p_.pack), nullptr};
-      launch_head_wgrad(model_, dtype_, hb, B, 1, ptr<float>(p_.slab_fc), nparam_, aux_stream_, hrows, &f);
+      launch_head_wgrad(model_, dtype_, hb, B, 1, ptr<float>(p_.slab_fc), fc_ld_, aux_stream_, hrows, &f);
       post_launch(aux_stream_);
     } else {
-      splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, aux_stream_, hrows);
+      splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), fc_ld_, aux_stream_, hrows);
       post_launch(aux_stream_);
       launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
-                        nparam_, splits, cp, cp, nparam_, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
+                        fc_ld_, splits, cp, cp, nparam_, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
                         ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, nullptr, aux_stream_);
       post_launch(aux_stream_);
     }
@@ -567,7 +568,7 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     if (defer_join) aux_pending_ = true;
     else HIP_CHECK(hipStreamWaitEvent(s, events_[5], 0));
     launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
-                      nparam_, splits, cp, 0, cp, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
+                      fc_ld_, splits, cp, 0, cp, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
                       ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, ptr<int32_t>(p_.step), s);
     post_launch(s);
     return;
@@ -582,7 +583,7 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     const SgdFuse f{scale, lr_, momentum_, ptr<float>(p_.params), ptr<float>(p_.grad),
                     momentum_ != 0.f ? ptr<float>(p_.mom) : nullptr,  // as launch_reduce_sgd
                     ptr<void>(p_.pack), ptr<int32_t>(p_.step)};
-    launch_head_wgrad(model_, dtype_, hb, B, 1, ptr<float>(p_.slab_fc), nparam_, s, hrows, &f);
+    launch_head_wgrad(model_, dtype_, hb, B, 1, ptr<float>(p_.slab_fc), fc_ld_, s, hrows, &f);
     post_launch(s);
     return;
   }
@@ -597,12 +598,12 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
     const int nslab = launch_lenet_conv_bwd_fc(dtype_, br, conv_buffers(B), hb, f, s, bwd_blocks_);
     post_launch(s);
     launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
-                      nparam_, 1, cp, 0, cp, scale, ptr<float>(p_.params), ptr<float>(p_.grad), ptr<float>(p_.mom),
+                      fc_ld_, 1, cp, 0, cp, scale, ptr<float>(p_.params), ptr<float>(p_.grad), ptr<float>(p_.mom),
                       ptr<void>(p_.pack), lr_, momentum_, ptr<int32_t>(p_.step), s);
     post_launch(s);
     return;
   }
-  const int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, s, hrows);
+  const int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), fc_ld_, s, hrows);
   post_launch(s);
   int nslab = 0;
   if (model_ == ModelKind::LENET) {  // serial single-GPU schedule (MNIST_AMD_CONCURRENT=0)
@@ -611,7 +612,7 @@ void Trainer::launch_step(int B, hipStream_t s, bool defer_join) {
   }
   // no communicator: ONE fused reduce + SGD + pack kernel (2 boundaries fewer than reduce -> sgd)
   launch_reduce_sgd(model_, dtype_, ptr<const float>(p_.slab_conv), cp, nslab, ptr<const float>(p_.slab_fc),
-                    nparam_, splits, cp, 0, nparam_, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
+                    fc_ld_, splits, cp, 0, nparam_, scale, ptr<float>(p_.params), ptr<float>(p_.grad),
                     ptr<float>(p_.mom), ptr<void>(p_.pack), lr_, momentum_, ptr<int32_t>(p_.step), s);
   post_launch(s);
 }
@@ -638,9 +639,9 @@ void Trainer::launch_mlp_comm_tail(int B, hipStream_t s, const HeadBuffers& hb, 
   float* g = ptr<float>(p_.grad);
   float* slab = ptr<float>(p_.slab_fc);
   if (plan_ == Plan::JOIN) {
-    const int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, slab, nparam_, s, hrows);
+    const int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, slab, fc_ld_, s, hrows);
     post_launch(s);
-    launch_reduce(slab, nparam_, splits, 0, nparam_, scale, g, s);
+    launch_reduce(slab, fc_ld_, splits, 0, nparam_, scale, g, s);
     post_launch(s);
     all_reduce(coalesced_buckets(), -1, s);
     launch_sgd_pack(model_, dtype_, ptr<float>(p_.params), g, ptr<float>(p_.mom), ptr<void>(p_.pack), nparam_, lr_,
@@ -653,9 +654,9 @@ void Trainer::launch_mlp_comm_tail(int B, hipStream_t s, const HeadBuffers& hb, 
   (void)ps;
   const std::vector<Group> gs = groups();
   for (size_t k = 0; k < gs.size(); ++k) {
-    const int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, slab, nparam_, s, hrows, nullptr, gs[k].mask);
+    const int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, slab, fc_ld_, s, hrows, nullptr, gs[k].mask);
     post_launch(s);
-    launch_reduce(slab, nparam_, splits, gs[k].p0, gs[k].p1, scale, g, s);
+    launch_reduce(slab, fc_ld_, splits, gs[k].p0, gs[k].p1, scale, g, s);
     post_launch(s);
     HIP_CHECK(hipEventRecord(events_[6 + k], s));
     comm_phase(static_cast<int>(k), events_[6 + k], k + 1 == gs.size());
@@ -671,7 +672,7 @@ void Trainer::launch_lenet_comm_tail(int B, int nslab, int splits, hipStream_t s
   const float scale = 1.0f / float(B), gs = 1.0f / float(world_);
   const int cp = model_conv_params(model_);
   float* g = ptr<float>(p_.grad);
-  launch_reduce(ptr<const float>(p_.slab_fc), nparam_, splits, cp, nparam_, scale, g, aux_stream_);
+  launch_reduce(ptr<const float>(p_.slab_fc), fc_ld_, splits, cp, nparam_, scale, g, aux_stream_);
   post_launch(aux_stream_);
   HIP_CHECK(hipEventRecord(events_[5], aux_stream_));
   if (plan_ == Plan::JOIN) {
@@ -707,10 +708,10 @@ void Trainer::launch_lenet_split_tail(int B, int nslab, hipStream_t s, const Hea
       continue;
     }
     trace("split: FC group wgrad + reduce (aux), AR + update (comm)");
-    const int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, aux_stream_,
+    const int splits = launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), fc_ld_, aux_stream_,
                                          hrows, nullptr, gs[k].mask);
     post_launch(aux_stream_);
-    launch_reduce(ptr<const float>(p_.slab_fc), nparam_, splits, gs[k].p0, gs[k].p1, scale, g, aux_stream_);
+    launch_reduce(ptr<const float>(p_.slab_fc), fc_ld_, splits, gs[k].p0, gs[k].p1, scale, g, aux_stream_);
     post_launch(aux_stream_);
     HIP_CHECK(hipEventRecord(events_[6 + k], aux_stream_));
     comm_phase(static_cast<int>(k), events_[6 + k], false);
@@ -736,9 +737,9 @@ void Trainer::launch_lenet_overlap(int B, int nslab, hipStream_t s, const HeadBu
   const int cp = model_conv_params(model_);
   float* g = ptr<float>(p_.grad);
   const int splits =
-      launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), nparam_, aux_stream_, hrows);
+      launch_head_wgrad(model_, dtype_, hb, B, fc_splits_, ptr<float>(p_.slab_fc), fc_ld_, aux_stream_, hrows);
   post_launch(aux_stream_);
-  launch_reduce(ptr<const float>(p_.slab_fc), nparam_, splits, cp, nparam_, scale, g, aux_stream_);
+  launch_reduce(ptr<const float>(p_.slab_fc), fc_ld_, splits, cp, nparam_, scale, g, aux_stream_);
   post_launch(aux_stream_);
   ov_fc_->all_reduce_sum_f32(g + cp, size_t(nparam_ - cp), aux_stream_);
   launch_sgd_pack_range(model_, dtype_, ptr<float>(p_.params), g, ptr<float>(p_.mom), ptr<void>(p_.pack), cp, nparam_,

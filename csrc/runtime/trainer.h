@@ -171,6 +171,7 @@ class Trainer {
   int conv_slabs() const;
   int conv_params() const;
   int fc_splits() const { return fc_splits_; }
+  int fc_ld() const { return fc_ld_; }
 
  private:
   BatchRef batch_ref(int B) const;
@@ -212,6 +213,7 @@ class Trainer {
   ModelKind model_;
   DType dtype_;
   int batch_, ldb_, fc_splits_, nparam_;
+  int fc_ld_ = 0;  // FC slab row stride: nparam rounded up to 4 floats (16-byte aligned rows for the wide slab stores)
   TrainerPtrs p_;
   float lr_ = 0.01f, momentum_ = 0.f, drop_p_ = 0.2f;
   uint32_t seed_ = 1234;

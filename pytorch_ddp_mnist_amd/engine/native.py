@@ -215,7 +215,7 @@ class NativeTrainer:
         self.eval_metrics = z(C.metric_rows(self.batch), 4, dt=torch.float32)
         self.xT, self.h1T, self.h2T = z(K0P, self.ld_b), z(N1P, self.ld_b), z(N2P, self.ld_b)
         self.dy1T, self.dy2T, self.dy3T = z(N1P, self.ld_b), z(N2P, self.ld_b), z(16, self.ld_b)
-        self.slab_fc = z(fc_splits, self.nparam, dt=torch.float32)
+        self.slab_fc = z(fc_splits, _rup(self.nparam, 4), dt=torch.float32)  # rows 16-byte aligned (Trainer::fc_ld)
         # rows for any batch <= self.batch (a partial last batch can need more workgroups than a full one).
         # (Round 5 measured the transposed layout -- one slab column per workgroup, one wave per parameter in the
         # conv update -- and reverted it: conv_bwd's scattered column stores cost 50.7 -> 54.4 us at B = 8192

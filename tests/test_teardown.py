@@ -65,3 +65,45 @@ def test_live_trainer_at_exit_is_closed_by_the_hook():
                        text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-3000:]
     assert "hook-close" in r.stdout and "teardown at exit" not in r.stdout
+
+
+def test_oneshot_epoch_barrier_and_end_agreement_selection():
+    """The runner's one-shot guards (advisor r5): a barrier before each epoch's steps and an end-of-run latch
+    agreement run exactly when a one-shot plane (data plane or OVERLAP instances) is attached."""
+    from types import SimpleNamespace
+
+    from pytorch_ddp_mnist_amd.engine.runner import _uses_oneshot
+    assert not _uses_oneshot(SimpleNamespace(tr=SimpleNamespace(oneshot=None, overlap=None)))
+    assert _uses_oneshot(SimpleNamespace(tr=SimpleNamespace(oneshot=object(), overlap=None)))
+    assert _uses_oneshot(SimpleNamespace(tr=SimpleNamespace(oneshot=None, overlap=(object(), object()))))
+    assert not _uses_oneshot(SimpleNamespace())  # the torch-CPU engine has no native trainer
+
+
+def test_agree_oneshot_raises_on_every_rank():
+    """NativeTrainer.agree_oneshot: a latch on ANY rank (reduce_max > 0) raises CollectiveError on this rank too,
+    also when this rank's own instances report no error."""
+    import pytest as _pt
+
+    from pytorch_ddp_mnist_amd.engine.native import CollectiveError, NativeTrainer
+
+    class _Inst:
+        def __init__(self, err):
+            self.err = err
+
+        def check(self):
+            return self.err
+
+    class _Stream:
+        def synchronize(self):
+            pass
+
+    fake = type("FakeTrainer", (), {})()
+    fake.stream = _Stream()
+    fake.oneshot, fake.overlap = _Inst(""), None
+    fake._oneshot_instances = lambda: [fake.oneshot]
+    NativeTrainer.agree_oneshot(fake, lambda v: v)           # nobody failed: no error
+    with _pt.raises(CollectiveError, match="peer rank"):
+        NativeTrainer.agree_oneshot(fake, lambda v: 1.0)     # a peer latched a failure
+    fake.oneshot = _Inst("flag wait timed out")
+    with _pt.raises(CollectiveError, match="timed out"):
+        NativeTrainer.agree_oneshot(fake, lambda v: v)
