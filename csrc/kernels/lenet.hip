@@ -217,14 +217,26 @@ DEV void conv_fwd_images(const BatchRef& br, const LenetConvBuffers& cb, int fir
   }
   Frag b2r[S::W2LDS ? 1 : C2CH];
   if constexpr (S::SPL) {
-    for (int e = tid; e < 16 * 224 / 4; e += NT) {
-      const int r = e / 56, c = (e % 56) * 4;
-      const f32x4 v = *reinterpret_cast<const f32x4*>(pack + L::C2F + r * 224 + c);
-      u32x2 h, m, l;
-      Mma<float>::split3(v, h, m, l);
-      *reinterpret_cast<u32x2*>(w2h + r * S::W2P + c) = h;
-      *reinterpret_cast<u32x2*>(w2m + r * S::W2P + c) = m;
-      *reinterpret_cast<u32x2*>(w2l + r * S::W2P + c) = l;
+    // every thread's W2 loads issued before its first cut / LDS store (clamped, branch-free): ONE memory round
+    // trip for the workgroup's W2 staging instead of one per loop trip -- at B = 128 each workgroup stages W2 for
+    // a single image, so this prologue is on the step's critical path (round 5: 7.6 -> 8.4 us conv_fwd fp32)
+    constexpr int NV = 16 * 224 / 4, IT = (NV + NT - 1) / NT;
+    f32x4 wv[IT];
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = min(tid + i * NT, NV - 1), r = e / 56, c = (e % 56) * 4;
+      wv[i] = *reinterpret_cast<const f32x4*>(pack + L::C2F + r * 224 + c);
+    }
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      const int e = tid + i * NT, r = e / 56, c = (e % 56) * 4;
+      if (e < NV) {
+        u32x2 h, m, l;
+        Mma<float>::split3(wv[i], h, m, l);
+        *reinterpret_cast<u32x2*>(w2h + r * S::W2P + c) = h;
+        *reinterpret_cast<u32x2*>(w2m + r * S::W2P + c) = m;
+        *reinterpret_cast<u32x2*>(w2l + r * S::W2P + c) = l;
+      }
     }
   } else if constexpr (S::W2LDS) {
     constexpr int VE = 16 / (int)sizeof(T);
