@@ -339,8 +339,65 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
   // ---------------------------------------------------------------- stage the input tile
   // (PRE: layer 1 already ran in l1_split_kernel, which also wrote xT; X itself is not needed)
   if constexpr (PRE) {
+  } else if constexpr (H::GATHER && sizeof(T) == 2) {
+    // bf16: one work item = one 8-pixel chunk of 4 consecutive rows: four 8-byte image loads (all items' loads
+    // issued before any conversion), four 16-byte LDS stores and eight 4-row-wide xT stores.  (16-pixel items left
+    // 6 of the 16 waves with the whole gather -- 392 items -- and the rest waiting at the staging barrier.)
+    static_assert(H::K0 % 8 == 0 && H::K0P % 8 == 0 && R % 4 == 0, "gather chunking");
+    constexpr int GC = H::K0P / 8, NGI = (R / 4) * GC, ITG = (NGI + NTH - 1) / NTH;
+    T* xT = reinterpret_cast<T*>(hb.xT);
+    u32x2 px[ITG][4];
+#pragma unroll
+    for (int i = 0; i < ITG; ++i) {
+      const int e = min(tid + i * NTH, NGI - 1), r = (e % (R / 4)) * 4, c = e / (R / 4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {  // branch-free: padding chunks / rows past the batch read row 0, zeroed at use
+        // (look-ahead: the tile's own rows of xnext, contiguous; else the dataset rows by sample index)
+        const uint8_t* src = look ? br.xnext + (size_t)(r0 + r + q) * 784 : br.images + (size_t)max(sIdx[r + q], 0) * 784;
+        px[i][q] = *reinterpret_cast<const u32x2*>(src + min(c, H::K0 / 8 - 1) * 8);
+      }
+    }
+    // pinned order: pixel loads, then the W1 prefetch, then the conversion (which then waits for the
+    // pixels only -- the scheduler otherwise hoisted the prefetch above them and sank the pixel loads into
+    // the conversion, one wait per row)
+    __builtin_amdgcn_sched_barrier(0);
+    prefetch_b1();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < ITG; ++i) {
+      // threads past the last item convert the (clamped) last item again and skip the stores: no branch
+      // around the loads' consumers
+      const int eu = tid + i * NTH, e = min(eu, NGI - 1), r = (e % (R / 4)) * 4, c = e / (R / 4);
+      const bool item = eu < NGI;
+      u32x4 pk[4];  // row q's 8 pixels as 8 bf16
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool live = (look ? r0 + r + q < B : sIdx[r + q] >= 0) && c < H::K0 / 8;
+        const uint32_t lm = live ? 0xFFFFFFFFu : 0u;  // the row's pixels or zeros, applied to packed pairs
+        typedef __attribute__((ext_vector_type(2))) float f32x2;
+        uint32_t d[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {  // pixel pairs: one v_cvt_pk_bf16_f32 each, computed unconditionally
+          const uint32_t wv = px[i][q][k >> 1];
+          const float a = mnist_norm((wv >> (16 * (k & 1))) & 255u), b = mnist_norm((wv >> (16 * (k & 1) + 8)) & 255u);
+          d[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2{a, b}), bf16x2)) & lm;
+        }
+        pk[q] = u32x4{d[0], d[1], d[2], d[3]};
+        if (item) *reinterpret_cast<u32x4*>(sX + (r + q) * S::PX + c * 8) = pk[q];
+      }
+      if (TRAIN && item && !ABLATED(hb.ablate, 1)) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {  // pixel j of the 4 rows: halfword j of each row, one v_perm_b32 per pair
+          const int wd = j >> 1;
+          const uint32_t lo = pack_half16(pk[0][wd], pk[1][wd], j & 1);
+          const uint32_t hi = pack_half16(pk[2][wd], pk[3][wd], j & 1);
+          *reinterpret_cast<u32x2*>(xT + (size_t)(c * 8 + j) * ldB + r0 + r) = u32x2{lo, hi};
+        }
+      }
+    }
+    stamp(11);  // gathered tile converted and stored to LDS, xT stores issued
   } else if constexpr (H::GATHER) {
-    // one work item = one 16-pixel chunk of 4 consecutive rows: four 16-byte image loads (all items'
+    // fp32: one work item = one 16-pixel chunk of 4 consecutive rows: four 16-byte image loads (all items'
     // loads issued before any conversion), 16-byte LDS stores, and 4-row-wide xT stores (one per pixel)
     static_assert(H::K0 % 16 == 0 && H::K0P % 16 == 0 && R % 4 == 0, "gather chunking");
     constexpr int GC = H::K0P / 16, NGI = (R / 4) * GC, ITG = (NGI + NTH - 1) / NTH;
@@ -368,38 +425,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       // around the loads' consumers
       const int eu = tid + i * NTH, e = min(eu, NGI - 1), r = (e % (R / 4)) * 4, c = e / (R / 4);
       const bool item = eu < NGI;
-      if constexpr (sizeof(T) == 2) {
-        // each row's 16 pixels -> 16 bf16 packed in 8 registers (two 16-byte LDS stores); the xT store of
-        // pixel j takes halfword j of the four rows (as the pool2-row path below)
-        u32x4 pk[4][2];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const bool live = (look ? r0 + r + q < B : sIdx[r + q] >= 0) && c < H::K0 / 16;
-          const uint32_t lm = live ? 0xFFFFFFFFu : 0u;  // the row's pixels or zeros, applied to packed pairs
-          typedef __attribute__((ext_vector_type(2))) float f32x2;
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            uint32_t d[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {  // pixel pairs: one v_cvt_pk_bf16_f32 each, computed unconditionally
-              const uint32_t wv = px[i][q][2 * h + (k >> 1)];
-              const float a = mnist_norm((wv >> (16 * (k & 1))) & 255u), b = mnist_norm((wv >> (16 * (k & 1) + 8)) & 255u);
-              d[k] = __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2{a, b}), bf16x2)) & lm;
-            }
-            pk[q][h] = u32x4{d[0], d[1], d[2], d[3]};
-            if (item) *reinterpret_cast<u32x4*>(sX + (r + q) * S::PX + c * 16 + h * 8) = pk[q][h];
-          }
-        }
-        if (TRAIN && item && !ABLATED(hb.ablate, 1)) {
-#pragma unroll
-          for (int j = 0; j < 16; ++j) {
-            const int h = j >> 3, wd = (j & 7) >> 1;
-            const uint32_t lo = pack_half16(pk[0][h][wd], pk[1][h][wd], j & 1);  // one v_perm_b32 each
-            const uint32_t hi = pack_half16(pk[2][h][wd], pk[3][h][wd], j & 1);
-            *reinterpret_cast<u32x2*>(xT + (size_t)(c * 16 + j) * ldB + r0 + r) = u32x2{lo, hi};
-          }
-        }
-      } else {
+      {
 #pragma unroll
         for (int j0 = 0; j0 < 16; j0 += 4) {  // fp32: 4 pixels at a time (one 16-byte LDS store per row)
           float v[4][4];
