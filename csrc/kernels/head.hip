@@ -397,12 +397,12 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
     }
     stamp(11);  // gathered tile converted and stored to LDS, xT stores issued
   } else if constexpr (H::GATHER) {
-    // fp32: one work item = one 16-pixel chunk of 4 consecutive rows: four 16-byte image loads (all items'
+    // fp32: one work item = one 8-pixel chunk of 4 consecutive rows (as bf16): four 8-byte image loads (all items'
     // loads issued before any conversion), 16-byte LDS stores, and 4-row-wide xT stores (one per pixel)
-    static_assert(H::K0 % 16 == 0 && H::K0P % 16 == 0 && R % 4 == 0, "gather chunking");
-    constexpr int GC = H::K0P / 16, NGI = (R / 4) * GC, ITG = (NGI + NTH - 1) / NTH;
+    static_assert(H::K0 % 8 == 0 && H::K0P % 8 == 0 && R % 4 == 0, "gather chunking");
+    constexpr int GC = H::K0P / 8, NGI = (R / 4) * GC, ITG = (NGI + NTH - 1) / NTH;
     T* xT = reinterpret_cast<T*>(hb.xT);
-    u32x4 px[ITG][4];
+    u32x2 px[ITG][4];
 #pragma unroll
     for (int i = 0; i < ITG; ++i) {
       const int e = min(tid + i * NTH, NGI - 1), r = (e % (R / 4)) * 4, c = e / (R / 4);
@@ -410,7 +410,7 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       for (int q = 0; q < 4; ++q) {  // branch-free: padding chunks / rows past the batch read row 0, zeroed at use
         // (look-ahead: the tile's own rows of xnext, contiguous; else the dataset rows by sample index)
         const uint8_t* src = look ? br.xnext + (size_t)(r0 + r + q) * 784 : br.images + (size_t)max(sIdx[r + q], 0) * 784;
-        px[i][q] = *reinterpret_cast<const u32x4*>(src + min(c, H::K0 / 16 - 1) * 16);
+        px[i][q] = *reinterpret_cast<const u32x2*>(src + min(c, H::K0 / 8 - 1) * 8);
       }
     }
     // pinned order: pixel loads, then the W1 prefetch, then the conversion (which then waits for the
@@ -427,22 +427,22 @@ __global__ __launch_bounds__(NWV * 64) void head_kernel(BatchRef br, HeadBuffers
       const bool item = eu < NGI;
       {
 #pragma unroll
-        for (int j0 = 0; j0 < 16; j0 += 4) {  // fp32: 4 pixels at a time (one 16-byte LDS store per row)
+        for (int j0 = 0; j0 < 8; j0 += 4) {  // fp32: 4 pixels at a time (one 16-byte LDS store per row)
           float v[4][4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            const bool live = (look ? r0 + r + q < B : sIdx[r + q] >= 0) && c < H::K0 / 16;
+            const bool live = (look ? r0 + r + q < B : sIdx[r + q] >= 0) && c < H::K0 / 8;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               const float nv = mnist_norm((px[i][q][(j0 + j) >> 2] >> (8 * ((j0 + j) & 3))) & 255u);
               v[q][j] = live ? nv : 0.f;
             }
-            if (item) *reinterpret_cast<f32x4*>(sX + (r + q) * S::PX + c * 16 + j0) = f32x4{v[q][0], v[q][1], v[q][2], v[q][3]};
+            if (item) *reinterpret_cast<f32x4*>(sX + (r + q) * S::PX + c * 8 + j0) = f32x4{v[q][0], v[q][1], v[q][2], v[q][3]};
           }
           if (TRAIN && item) {
 #pragma unroll
             for (int j = 0; j < 4; ++j)
-              store_col4<T>(xT + (size_t)(c * 16 + j0 + j) * ldB + r0 + r, v[0][j], v[1][j], v[2][j], v[3][j]);
+              store_col4<T>(xT + (size_t)(c * 8 + j0 + j) * ldB + r0 + r, v[0][j], v[1][j], v[2][j], v[3][j]);
           }
         }
       }
