@@ -65,6 +65,8 @@ case $MODE in
         lenet_serial) E="MNIST_AMD_CONCURRENT=0" ;;
         mlp8k) E="STAMP_MODEL=mlp" ;;
         lenetf) E="STAMP_DTYPE=fp32" ;;
+        mlp128) E="STAMP_MODEL=mlp STAMP_BATCH=128 STAMP_DTYPE=fp32" ;;
+        lenet128) E="STAMP_BATCH=128" ;;
         *) echo "no stamps config $c"; exit 1 ;;
       esac
       env $E timeout -k 10 120 python scripts/stamps.py > "$OUT/${TAG}_stamps_$c.txt" 2>&1 || { echo "stamps $c failed"; exit 1; }
