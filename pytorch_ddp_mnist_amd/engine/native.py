@@ -410,7 +410,10 @@ class NativeTrainer:
         ranked = choose_bucket_groups(self.model_name, lat, unit_us, fc_all, main)
         return {"latency_us": lat.as_dict(), "unit_us": [round(v, 2) for v in unit_us], "fc_all_us": round(fc_all, 2),
                 "main_us": round(main, 2),
-                "ranked": [{"groups": g, "modelled_us": round(t, 2)} for g, t in ranked], "_ranked": ranked}
+                "ranked": [{"groups": g, "modelled_us": round(t, 2)} for g, t in ranked], "_ranked": ranked,
+                "note": "comm-stream timeline model used to pick which bucket plans to time; it does not price the "
+                        "extra groups' kernels contending with the main stream -- the calibration's measured "
+                        "timings_ms decide"}
 
     def broadcast_params(self, root: int = 0) -> None:
         """DDP construction semantics: every rank starts from rank 0's parameters (over RCCL, or over the
