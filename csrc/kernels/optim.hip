@@ -9,6 +9,7 @@
 //                 (models.h) and the device step counters are advanced.  Replaces the
 //                 _foreach_add_ multi-tensor apply (survey K15) plus any weight cast kernels.
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 #include "launch.h"
@@ -176,14 +177,19 @@ __global__ __launch_bounds__(NW * 64) void reduce_sgd_kernel(const float* __rest
   }
 }
 
-// Fused reduce + SGD + pack of a parameter range whose slab count is <= DIRECT_MAX: no LDS.
+// Fused reduce + SGD + pack of a parameter range whose slab count is <= DIRECT_MAX: no LDS.  Block size rd_block:
+// the MLP (its update alone on the chip, after the weight gradient) takes one-wave blocks -- bf16 B=8192
+// 0.0312-0.0315 vs 0.0314-0.0317 ms with 256-thread blocks, bitwise equal; LeNet's FC update, which runs beside
+// conv_bwd, keeps 256 (one-wave blocks: 0.0971-0.0972 vs 0.0969-0.0971 ms); profiles/r6_session1/ab_reduce_direct_block.txt
+template <class Model>
+constexpr int rd_block() { return std::is_same<Model, MlpModel>::value ? 64 : 256; }
 template <class Model, typename T>
-__global__ __launch_bounds__(256) void reduce_sgd_direct_kernel(const float* __restrict__ slab, int ld, int ns, int p0,
+__global__ __launch_bounds__(rd_block<Model>()) void reduce_sgd_direct_kernel(const float* __restrict__ slab, int ld, int ns, int p0,
                                                                 int n, float scale, float* __restrict__ params,
                                                                 float* __restrict__ grad, float* __restrict__ mom,
                                                                 T* __restrict__ pack, float lr, float mu,
                                                                 int32_t* step_ptr) {
-  const int p = p0 + blockIdx.x * 256 + threadIdx.x;
+  const int p = p0 + blockIdx.x * rd_block<Model>() + threadIdx.x;
   if (p < n) {
     const float pv = params[p], mv = mom ? mom[p] : 0.f;  // issued with the slab loads
     float g = slab_sum_direct(slab, ld, ns, p) * scale;
@@ -210,7 +216,8 @@ void reduce_sgd_t(const float* sa, int lda, int na, const float* sb, int ldb, in
   if (n <= p0) return;
   const bool only_b = p0 >= split, only_a = n <= split;
   if ((only_b && nb <= DIRECT_MAX) || (only_a && na <= DIRECT_MAX)) {
-    hipLaunchKernelGGL((reduce_sgd_direct_kernel<Model, T>), dim3((n - p0 + 255) / 256), dim3(256), 0, s,
+    constexpr int RB = rd_block<Model>();
+    hipLaunchKernelGGL((reduce_sgd_direct_kernel<Model, T>), dim3((n - p0 + RB - 1) / RB), dim3(RB), 0, s,
                        only_b ? sb : sa, only_b ? ldb : lda, only_b ? nb : na, p0, n, scale, params, grad, mom,
                        reinterpret_cast<T*>(pack), lr, mu, step_ptr);
     return;
