@@ -1071,9 +1071,11 @@ struct BwdRoles {
 
 // phase-B LDS prefetch distance (chunks of fragments in flight ahead of the MFMAs).  LeNet bf16 B=8192, 2000
 // steps (profiles/r4_session2/ab_conv_bwd_pd.txt): PD 1 / 2 / 3 = 0.1038-0.1041 / 0.1024-0.1034 / 0.1036-0.1038
-// ms/step, bitwise-equal parameters; fp32 unchanged (0.439 ms).
+// ms/step, bitwise-equal parameters; fp32 unchanged (0.439 ms).  Re-measured on the round-6 kernels (two boxes,
+// profiles/r6_session1/ab_bwd_pd.txt): PD 3 0.0966-0.0971 vs PD 2 0.0970-0.0974 ms; PD 1 / 4 / 5 no better; fp32
+// unchanged (0.370 ms).
 #ifndef MNIST_AMD_BWD_PD
-#define MNIST_AMD_BWD_PD 2
+#define MNIST_AMD_BWD_PD 3
 #endif
 constexpr int BWD_PD = MNIST_AMD_BWD_PD;
 // One conv_bwd workgroup: block `blk` of `nblk` (the conv_bwd part of the grid).
